@@ -1,0 +1,154 @@
+"""ctypes binding of the C ABI declared in include/aesfhe.h.
+
+The same binding drives either implementation of the ABI:
+  * the product library ``libaesfhe.so`` (HIP, gfx950) -- loaded by :func:`load_product`;
+  * the CPU oracle ``oracle/_build/liboracle_ckks.so`` -- loaded only by tests/ and by
+    bench.py's cpu_baseline leg, which pass the handle to ``Engine(_lib=...)`` explicitly.
+
+The product loader never falls back to anything: if the HIP extension is missing or cannot be
+loaded it raises, so a GPU run can never silently use a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+PRODUCT_LIB = _HERE.parent / "build" / "libaesfhe.so"
+
+c_ct_p = C.c_void_p
+c_key_p = C.c_void_p
+c_pt_p = C.c_void_p
+c_eng_p = C.c_void_p
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("log_n", C.c_int32),
+        ("max_level", C.c_int32),
+        ("special_primes", C.c_int32),
+        ("scale_bits", C.c_int32),
+        ("base_bits", C.c_int32),
+        ("special_bits", C.c_int32),
+        ("device", C.c_int32),
+        ("threads", C.c_int32),
+        ("seed", C.c_uint64),
+        ("primes", C.POINTER(C.c_uint64)),
+    ]
+
+
+# (name, restype, argtypes) for every symbol of include/aesfhe.h
+_P = C.POINTER
+SIGNATURES = [
+    ("aesfhe_last_error", C.c_char_p, []),
+    ("aesfhe_backend_name", C.c_char_p, []),
+    ("aesfhe_engine_create", C.c_int, [_P(Params), _P(c_eng_p)]),
+    ("aesfhe_engine_destroy", None, [c_eng_p]),
+    ("aesfhe_engine_dims", C.c_int, [c_eng_p, _P(C.c_int32)]),
+    ("aesfhe_engine_primes", C.c_int, [c_eng_p, _P(C.c_uint64)]),
+    ("aesfhe_engine_scales", C.c_int, [c_eng_p, _P(C.c_double)]),
+    ("aesfhe_engine_mul_scale", C.c_double, [c_eng_p, C.c_int32]),
+    ("aesfhe_engine_sync", C.c_int, [c_eng_p]),
+    ("aesfhe_engine_profile", C.c_int, [c_eng_p, C.c_int32]),
+    ("aesfhe_engine_profile_read", C.c_int,
+     [c_eng_p, C.c_char_p, _P(C.c_int64), _P(C.c_double), _P(C.c_double)]),
+    ("aesfhe_engine_device_bytes", C.c_int64, [c_eng_p]),
+    ("aesfhe_encode", C.c_int,
+     [C.c_int32, _P(C.c_double), _P(C.c_double), C.c_int64, C.c_double, _P(C.c_int64)]),
+    ("aesfhe_decode", C.c_int,
+     [C.c_int32, _P(C.c_int64), C.c_double, _P(C.c_double), _P(C.c_double)]),
+    ("aesfhe_key_secret", C.c_int, [c_eng_p, C.c_uint64, _P(c_key_p)]),
+    ("aesfhe_key_public", C.c_int, [c_eng_p, c_key_p, _P(c_key_p)]),
+    ("aesfhe_key_relin", C.c_int, [c_eng_p, c_key_p, _P(c_key_p)]),
+    ("aesfhe_key_galois", C.c_int, [c_eng_p, c_key_p, C.c_uint64, _P(c_key_p)]),
+    ("aesfhe_galois_elt", C.c_uint64, [C.c_int32, C.c_int64, C.c_int32]),
+    ("aesfhe_key_info", C.c_int, [c_key_p, _P(C.c_int32), _P(C.c_uint64)]),
+    ("aesfhe_key_free", None, [c_key_p]),
+    ("aesfhe_encrypt", C.c_int,
+     [c_eng_p, c_key_p, _P(C.c_int64), C.c_int32, C.c_int32, C.c_uint64, _P(c_ct_p)]),
+    ("aesfhe_decrypt", C.c_int, [c_eng_p, c_key_p, c_ct_p, _P(C.c_int64)]),
+    ("aesfhe_ct_info", C.c_int, [c_ct_p, _P(C.c_int32)]),
+    ("aesfhe_ct_export", C.c_int, [c_eng_p, c_ct_p, _P(C.c_uint64)]),
+    ("aesfhe_ct_import", C.c_int,
+     [c_eng_p, _P(C.c_uint64), C.c_int32, C.c_int32, C.c_int32, _P(c_ct_p)]),
+    ("aesfhe_ct_copy", C.c_int, [c_eng_p, c_ct_p, _P(c_ct_p)]),
+    ("aesfhe_ct_slice", C.c_int, [c_eng_p, c_ct_p, C.c_int32, C.c_int32, _P(c_ct_p)]),
+    ("aesfhe_ct_concat", C.c_int, [c_eng_p, _P(c_ct_p), C.c_int32, _P(c_ct_p)]),
+    ("aesfhe_ct_zero", C.c_int, [c_eng_p, C.c_int32, C.c_int32, _P(c_ct_p)]),
+    ("aesfhe_ct_free", None, [c_ct_p]),
+    ("aesfhe_pt_create", C.c_int, [c_eng_p, _P(C.c_int64), C.c_int32, _P(c_pt_p)]),
+    ("aesfhe_pt_free", None, [c_pt_p]),
+    ("aesfhe_add", C.c_int, [c_eng_p, c_ct_p, c_ct_p, _P(c_ct_p)]),
+    ("aesfhe_sub", C.c_int, [c_eng_p, c_ct_p, c_ct_p, _P(c_ct_p)]),
+    ("aesfhe_negate", C.c_int, [c_eng_p, c_ct_p, _P(c_ct_p)]),
+    ("aesfhe_add_pt", C.c_int, [c_eng_p, c_ct_p, c_pt_p, _P(c_ct_p)]),
+    ("aesfhe_mul_pt", C.c_int, [c_eng_p, c_ct_p, c_pt_p, _P(c_ct_p)]),
+    ("aesfhe_mul_const", C.c_int, [c_eng_p, c_ct_p, C.c_double, C.c_double, _P(c_ct_p)]),
+    ("aesfhe_tensor", C.c_int, [c_eng_p, c_ct_p, c_ct_p, _P(c_ct_p)]),
+    ("aesfhe_relinearize", C.c_int, [c_eng_p, c_ct_p, c_key_p, _P(c_ct_p)]),
+    ("aesfhe_rescale", C.c_int, [c_eng_p, c_ct_p, _P(c_ct_p)]),
+    ("aesfhe_mul", C.c_int, [c_eng_p, c_ct_p, c_ct_p, c_key_p, _P(c_ct_p)]),
+    ("aesfhe_level_down", C.c_int, [c_eng_p, c_ct_p, C.c_int32, _P(c_ct_p)]),
+    ("aesfhe_galois", C.c_int, [c_eng_p, c_ct_p, c_key_p, _P(c_ct_p)]),
+    ("aesfhe_power_basis", C.c_int, [c_eng_p, c_ct_p, C.c_int32, c_key_p, _P(c_ct_p)]),
+    ("aesfhe_lincomb", C.c_int,
+     [c_eng_p, _P(c_ct_p), C.c_int32, _P(C.c_double), _P(C.c_double), _P(c_ct_p)]),
+    ("aesfhe_dot", C.c_int, [c_eng_p, _P(c_ct_p), _P(c_ct_p), C.c_int32, c_key_p, _P(c_ct_p)]),
+    ("aesfhe_ntt_host", C.c_int,
+     [c_eng_p, _P(C.c_uint64), C.c_int32, _P(C.c_int32), C.c_int32]),
+    ("aesfhe_bench_ntt", C.c_int,
+     [c_eng_p, C.c_int32, C.c_int32, _P(C.c_double), _P(C.c_double)]),
+]
+
+SYMBOLS = [s[0] for s in SIGNATURES]
+
+# error code -> exception message prefix (desilofhe raises RuntimeError with text; the
+# reference matches "should have 3 polynomials" at xor_service.py:114-118)
+ERRORS = {-1: "invalid argument", -2: "out of memory", -3: "device error",
+          -4: "degree error", -5: "level error", -6: "unsupported"}
+
+
+class Lib:
+    """A loaded implementation of the aesfhe ABI."""
+
+    def __init__(self, path: str | os.PathLike):
+        self.path = str(path)
+        self.cdll = C.CDLL(self.path, mode=C.RTLD_LOCAL)
+        for name, res, args in SIGNATURES:
+            fn = getattr(self.cdll, name)
+            fn.restype = res
+            fn.argtypes = args
+            setattr(self, name[len("aesfhe_"):], fn)
+        self.backend = self.backend_name().decode()
+
+    def check(self, rc: int) -> None:
+        if rc != 0:
+            msg = self.last_error().decode(errors="replace")
+            raise RuntimeError(f"[{self.backend}] {ERRORS.get(rc, 'error')}: {msg}")
+
+
+_PRODUCT: Lib | None = None
+
+
+def load_product() -> Lib:
+    """Load the HIP engine.  Raises if the extension has not been built -- there is no
+    fallback implementation on the product path."""
+    global _PRODUCT
+    if _PRODUCT is None:
+        # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (SONAME
+        # libamdhip64.so.7) and loads it by file name, so if our library were loaded first the
+        # process would end up with two HSA runtimes fighting over /dev/kfd.  Importing torch
+        # first makes the dynamic loader resolve our DT_NEEDED libamdhip64.so.7 to that same
+        # runtime (SONAME match), which is also what torch.distributed / RCCL use.
+        try:
+            import torch  # noqa: F401
+        except Exception:  # torch absent: /opt/rocm's runtime is then the only one
+            pass
+        path = Path(os.environ.get("AESFHE_LIB", PRODUCT_LIB))
+        if not path.exists():
+            raise RuntimeError(
+                f"aes-fhe HIP extension not found at {path}; build it with "
+                f"`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+        _PRODUCT = Lib(path)
+    return _PRODUCT

@@ -1,0 +1,489 @@
+"""desilofhe-compatible CKKS engine facade over the MI355X C ABI (include/aesfhe.h).
+
+The reference drives all homomorphic arithmetic through ``desilofhe.Engine`` objects
+(engine_context.py:6,32-85; xor_service.py:36-129).  This module provides the same object
+surface -- ``Engine``, ``Ciphertext``, ``Plaintext`` and the key objects -- with the same
+method names, argument meaning and error behaviour, backed by the HIP engine
+(``libaesfhe.so``).  Swapping ``from desilofhe import Engine`` for
+``from aes_xor_fhe.fhe import Engine`` is the whole integration.
+
+Semantics pinned by the reference's tests:
+  * ``slot_count == N/2`` (test/test_xor_service.py:40-43 assumes 32768 at N = 2^16);
+  * ``rotate(ct, key, k)`` equals ``np.roll(v, k)`` (test/test_engine_rot.py:32-40);
+  * ``relinearize`` of a 2-polynomial ciphertext raises RuntimeError containing
+    "should have 3 polynomials" (matched at xor_service.py:114-118);
+  * every multiplication (ct x ct, ct x pt, ct x scalar) consumes one level.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Sequence
+
+import numpy as np
+
+from ._abi import Lib, Params, c_ct_p, load_product
+
+# HomomorphicEncryption.org 128-bit bound on log2(QP) for ternary secrets
+SECURITY_BUDGET = {11: 54, 12: 109, 13: 218, 14: 438, 15: 881, 16: 1772, 17: 3544}
+
+DEFAULT_PARAMS = dict(log_n=16, max_level=30, special_primes=8, scale_bits=40, base_bits=50,
+                      special_bits=50, seed=0x5EED5EED)
+
+
+def _params_for(log_n=None, max_level=None, special_primes=None, scale_bits=None,
+                base_bits=None, special_bits=None, seed=None, threads=0, device=0):
+    p = dict(DEFAULT_PARAMS)
+    for k, v in dict(log_n=log_n, max_level=max_level, special_primes=special_primes,
+                     scale_bits=scale_bits, base_bits=base_bits, special_bits=special_bits,
+                     seed=seed).items():
+        if v is not None:
+            p[k] = v
+    p["threads"] = threads
+    p["device"] = device
+    return p
+
+
+def _as_ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+class _Handle:
+    """Owns one C handle; frees it when collected (desilofhe objects are GC-managed)."""
+
+    __slots__ = ("_lib", "_h", "_free")
+
+    def __init__(self, lib: Lib, h, free):
+        self._lib, self._h, self._free = lib, h, free
+
+    def __del__(self):
+        try:
+            if self._h:
+                self._free(self._h)
+                self._h = None
+        except Exception:  # interpreter shutdown
+            pass
+
+
+# ------------------------------------------------------------------------------------------
+# keys
+class SecretKey(_Handle):
+    __slots__ = ("engine",)
+
+
+class PublicKey(_Handle):
+    __slots__ = ()
+
+
+class RelinearizationKey(_Handle):
+    __slots__ = ()
+
+
+class GaloisKey(_Handle):
+    __slots__ = ("galois_elt",)
+
+
+class ConjugationKey(GaloisKey):
+    __slots__ = ()
+
+
+class FixedRotationKey(GaloisKey):
+    __slots__ = ("delta",)
+
+
+class RotationKey:
+    """Key set for arbitrary rotations: galois keys for left rotations by +-2^i, generated on
+    first use from the secret key (deterministically: same seed -> same keys) and cached."""
+
+    def __init__(self, engine: "Engine", sk: SecretKey):
+        self._engine, self._sk, self._keys = engine, sk, {}
+
+    def left(self, step: int) -> GaloisKey:
+        if step not in self._keys:
+            eng = self._engine
+            g = eng._lib.galois_elt(eng.log_coeff_count, -step, 0)
+            self._keys[step] = eng._galois_key(self._sk, g, GaloisKey)
+        return self._keys[step]
+
+
+class BootstrapKey:
+    """Placeholder returned by create_(small_)bootstrap_key (engine_context.py:72-73 creates
+    them unconditionally).  Bootstrapping itself is SURVEY.md section 8f item 1 (next)."""
+
+    def __init__(self, small: bool):
+        self.small = small
+
+
+# ------------------------------------------------------------------------------------------
+class Ciphertext(_Handle):
+    """A batch of B ciphertexts at one level.  ``level`` mirrors desilofhe's attribute read at
+    xor_service.py:274-277."""
+
+    __slots__ = ("engine", "level", "batch", "npoly", "is_zero")
+
+    def __init__(self, engine: "Engine", h):
+        super().__init__(engine._lib, h, engine._lib.ct_free)
+        self.engine = engine
+        info = (C.c_int32 * 4)()
+        engine._lib.ct_info(h, info)
+        self.batch, self.npoly, self.level, self.is_zero = info[0], info[1], info[2], bool(info[3])
+
+    def __repr__(self):
+        return f"Ciphertext(level={self.level}, batch={self.batch}, npoly={self.npoly})"
+
+
+class Plaintext:
+    """Host-side slot vector; device encodings are materialised per (level, scale) on use.
+    A constant vector (every slot equal) is multiplied as the polynomial a + b X^{N/2}."""
+
+    def __init__(self, engine: "Engine", values: np.ndarray):
+        self.engine = engine
+        self.values = values
+        self.is_const = bool(values.size and np.all(values == values[0]))
+        self.const = complex(values[0]) if values.size else 0j
+        self._dev = {}
+
+    def device(self, level: int, scale: float):
+        key = (level, scale)
+        h = self._dev.get(key)
+        if h is None:
+            eng = self.engine
+            co = eng._encode_coeffs(self.values, scale)
+            out = C.c_void_p()
+            eng._check(eng._lib.pt_create(eng._h, _as_ptr(co, C.c_int64), level, C.byref(out)))
+            h = _Handle(eng._lib, out.value, eng._lib.pt_free)
+            self._dev[key] = h
+        return h._h
+
+
+# ------------------------------------------------------------------------------------------
+class Engine:
+    """CKKS engine with desilofhe's constructor signatures (engine_context.py:27-31):
+
+    1. ``Engine(mode='cpu', use_bootstrap=False, use_multiparty=False, thread_count=0, device_id=0)``
+    2. ``Engine(max_level, mode='cpu', *, use_multiparty=False, thread_count=0, device_id=0)``
+    3. ``Engine(log_coeff_count, special_prime_count, mode='cpu', ...)``
+
+    ``mode`` is accepted for compatibility; execution is always the HIP engine on
+    ``device_id`` (the product has no CPU path).  Extra keyword overrides (``log_n``,
+    ``special_primes``, ``scale_bits``, ``seed``) select explicit parameters; ``_lib`` injects
+    another implementation of the ABI (tests use it for the CPU oracle).
+    """
+
+    def __init__(self, *args, mode: str = "cpu", use_bootstrap: bool = False,
+                 use_multiparty: bool = False, thread_count: int = 0, device_id: int = 0,
+                 max_level: int | None = None, log_coeff_count: int | None = None,
+                 special_prime_count: int | None = None, log_n: int | None = None,
+                 special_primes: int | None = None, scale_bits: int | None = None,
+                 seed: int | None = None, _lib: Lib | None = None):
+        ints = [a for a in args if isinstance(a, (int, np.integer)) and not isinstance(a, bool)]
+        strs = [a for a in args if isinstance(a, str)]
+        if strs:
+            mode = strs[0]
+        if len(ints) == 1 and max_level is None:
+            max_level = int(ints[0])
+        elif len(ints) >= 2:
+            log_coeff_count, special_prime_count = int(ints[0]), int(ints[1])
+        if log_coeff_count is not None:          # signature 3
+            ln = log_coeff_count
+            k = special_prime_count or DEFAULT_PARAMS["special_primes"]
+            budget = SECURITY_BUDGET.get(ln, 1772)
+            lvl = max_level if max_level is not None else max(
+                1, (budget - DEFAULT_PARAMS["base_bits"] - k * DEFAULT_PARAMS["special_bits"])
+                // DEFAULT_PARAMS["scale_bits"])
+            p = _params_for(log_n=log_n or ln, max_level=lvl, special_primes=special_primes or k,
+                            scale_bits=scale_bits, seed=seed, threads=thread_count,
+                            device=device_id)
+        else:                                    # signatures 1 and 2
+            p = _params_for(log_n=log_n, max_level=max_level, special_primes=special_primes,
+                            scale_bits=scale_bits, seed=seed, threads=thread_count,
+                            device=device_id)
+        self.mode = mode
+        self.use_bootstrap = use_bootstrap
+        self.use_multiparty = use_multiparty
+        self.thread_count = thread_count
+        self.device_id = device_id
+        self._lib = _lib if _lib is not None else load_product()
+        self._params = p
+        cp = Params(p["log_n"], p["max_level"], p["special_primes"], p["scale_bits"],
+                    p["base_bits"], p["special_bits"], p["device"], p["threads"], p["seed"], None)
+        h = C.c_void_p()
+        self._check(self._lib.engine_create(C.byref(cp), C.byref(h)))
+        self._h = h.value
+        dims = (C.c_int32 * 4)()
+        self._lib.engine_dims(self._h, dims)
+        self.log_coeff_count, self.max_level, self.special_prime_count, self.dnum = list(dims)
+        self.slot_count = 1 << (self.log_coeff_count - 1)
+        np_ = self.max_level + 1 + self.special_prime_count
+        primes = (C.c_uint64 * np_)()
+        self._lib.engine_primes(self._h, primes)
+        self.primes = [int(x) for x in primes]
+        scales = (C.c_double * (self.max_level + 1))()
+        self._lib.engine_scales(self._h, scales)
+        self.scales = [float(x) for x in scales]
+        self._nonce = 0
+
+    # -- plumbing ---------------------------------------------------------------------------
+    def _check(self, rc):
+        self._lib.check(rc)
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                self._lib.engine_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def _ct(self, h) -> Ciphertext:
+        return Ciphertext(self, h)
+
+    def _call_ct(self, fn, *args) -> Ciphertext:
+        out = C.c_void_p()
+        self._check(fn(self._h, *args, C.byref(out)))
+        return self._ct(out.value)
+
+    def _vec(self, data) -> np.ndarray:
+        v = np.asarray(data)
+        if v.ndim != 1:
+            raise ValueError("expected a 1-D slot vector")
+        if v.size > self.slot_count:
+            raise ValueError(f"{v.size} values exceed slot_count {self.slot_count}")
+        return v.astype(np.complex128, copy=False)
+
+    def _encode_coeffs(self, values: np.ndarray, scale: float) -> np.ndarray:
+        v = np.ascontiguousarray(values, dtype=np.complex128)
+        re = np.ascontiguousarray(v.real)
+        im = np.ascontiguousarray(v.imag)
+        co = np.empty(1 << self.log_coeff_count, dtype=np.int64)
+        self._check(self._lib.encode(self.log_coeff_count, _as_ptr(re, C.c_double),
+                                     _as_ptr(im, C.c_double), v.size, scale,
+                                     _as_ptr(co, C.c_int64)))
+        return co
+
+    def _galois_key(self, sk: SecretKey, g: int, cls):
+        out = C.c_void_p()
+        self._check(self._lib.key_galois(self._h, sk._h, g, C.byref(out)))
+        k = cls(self._lib, out.value, self._lib.key_free)
+        k.galois_elt = g
+        return k
+
+    # -- keys (engine_context.py:62-73) -------------------------------------------------------
+    def create_secret_key(self, seed: int = 0) -> SecretKey:
+        out = C.c_void_p()
+        self._check(self._lib.key_secret(self._h, seed, C.byref(out)))
+        sk = SecretKey(self._lib, out.value, self._lib.key_free)
+        sk.engine = self
+        return sk
+
+    def create_public_key(self, sk: SecretKey) -> PublicKey:
+        out = C.c_void_p()
+        self._check(self._lib.key_public(self._h, sk._h, C.byref(out)))
+        return PublicKey(self._lib, out.value, self._lib.key_free)
+
+    def create_relinearization_key(self, sk: SecretKey) -> RelinearizationKey:
+        out = C.c_void_p()
+        self._check(self._lib.key_relin(self._h, sk._h, C.byref(out)))
+        return RelinearizationKey(self._lib, out.value, self._lib.key_free)
+
+    def create_conjugation_key(self, sk: SecretKey) -> ConjugationKey:
+        g = self._lib.galois_elt(self.log_coeff_count, 0, 1)
+        return self._galois_key(sk, g, ConjugationKey)
+
+    def create_rotation_key(self, sk: SecretKey) -> RotationKey:
+        return RotationKey(self, sk)
+
+    def create_fixed_rotation_key(self, sk: SecretKey, delta: int) -> FixedRotationKey:
+        g = self._lib.galois_elt(self.log_coeff_count, int(delta), 0)
+        k = self._galois_key(sk, g, FixedRotationKey)
+        k.delta = int(delta)
+        return k
+
+    def create_small_bootstrap_key(self, sk: SecretKey) -> BootstrapKey:
+        return BootstrapKey(small=True)
+
+    def create_bootstrap_key(self, sk: SecretKey) -> BootstrapKey:
+        return BootstrapKey(small=False)
+
+    # -- codec --------------------------------------------------------------------------------
+    def encode(self, vec, level: int | None = None, scale: float | None = None) -> Plaintext:
+        return Plaintext(self, self._vec(vec))
+
+    def encrypt(self, data, key, level: int | None = None) -> Ciphertext:
+        """Encrypt a slot vector (or a (B, <=slots) array as one batched ciphertext) under a
+        public key (or, symmetrically, the secret key), zero-padded to slot_count."""
+        level = self.max_level if level is None else int(level)
+        arr = np.asarray(data)
+        rows = arr[None, :] if arr.ndim == 1 else arr
+        if rows.ndim != 2 or rows.shape[1] > self.slot_count:
+            raise ValueError(f"data must be (<= {self.slot_count},) or (B, <= {self.slot_count})")
+        n = 1 << self.log_coeff_count
+        co = np.empty((rows.shape[0], n), dtype=np.int64)
+        for b in range(rows.shape[0]):
+            co[b] = self._encode_coeffs(rows[b].astype(np.complex128), self.scales[level])
+        nonce = self._nonce
+        self._nonce += 1
+        out = C.c_void_p()
+        self._check(self._lib.encrypt(self._h, key._h, _as_ptr(co, C.c_int64), rows.shape[0],
+                                      level, nonce, C.byref(out)))
+        return self._ct(out.value)
+
+    def decrypt(self, ct: Ciphertext, sk: SecretKey) -> np.ndarray:
+        n = 1 << self.log_coeff_count
+        co = np.empty((ct.batch, n), dtype=np.int64)
+        self._check(self._lib.decrypt(self._h, sk._h, ct._h, _as_ptr(co, C.c_int64)))
+        out = np.empty((ct.batch, self.slot_count), dtype=np.complex128)
+        re = np.empty(self.slot_count)
+        im = np.empty(self.slot_count)
+        scale = self.scales[ct.level]
+        for b in range(ct.batch):
+            row = np.ascontiguousarray(co[b])
+            self._check(self._lib.decode(self.log_coeff_count, _as_ptr(row, C.c_int64), scale,
+                                         _as_ptr(re, C.c_double), _as_ptr(im, C.c_double)))
+            out[b] = re + 1j * im
+        return out[0] if ct.batch == 1 else out
+
+    # -- arithmetic ---------------------------------------------------------------------------
+    def _as_plain(self, x) -> Plaintext:
+        if isinstance(x, Plaintext):
+            return x
+        if np.isscalar(x):
+            return Plaintext(self, np.full(self.slot_count, complex(x), dtype=np.complex128))
+        return Plaintext(self, self._vec(x))
+
+    def add(self, a, b) -> Ciphertext:
+        if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
+            return self._call_ct(self._lib.add, a._h, b._h)
+        if not isinstance(a, Ciphertext):
+            a, b = b, a
+        pt = self._as_plain(b)
+        return self._call_ct(self._lib.add_pt, a._h, pt.device(a.level, self.scales[a.level]))
+
+    def subtract(self, a, b) -> Ciphertext:
+        if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
+            return self._call_ct(self._lib.sub, a._h, b._h)
+        if isinstance(a, Ciphertext):
+            return self.add(a, self._as_plain(b).values * -1)
+        return self.add(self.negate(b), a)
+
+    sub = subtract
+
+    def negate(self, a: Ciphertext) -> Ciphertext:
+        return self._call_ct(self._lib.negate, a._h)
+
+    def multiply(self, a, b, relinearization_key: RelinearizationKey | None = None) -> Ciphertext:
+        if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
+            if relinearization_key is not None:
+                return self._call_ct(self._lib.mul, a._h, b._h, relinearization_key._h)
+            t = self._call_ct(self._lib.tensor, a._h, b._h)
+            return self._call_ct(self._lib.rescale, t._h)
+        if not isinstance(a, Ciphertext):
+            a, b = b, a
+        if not isinstance(a, Ciphertext):
+            raise TypeError("multiply needs at least one Ciphertext")
+        pt = self._as_plain(b)
+        if pt.is_const:
+            c = pt.const
+            return self._call_ct(self._lib.mul_const, a._h, c.real, c.imag)
+        scale = self._lib.engine_mul_scale(self._h, a.level)
+        return self._call_ct(self._lib.mul_pt, a._h, pt.device(a.level, scale))
+
+    def relinearize(self, ct: Ciphertext, relinearization_key: RelinearizationKey) -> Ciphertext:
+        return self._call_ct(self._lib.relinearize, ct._h, relinearization_key._h)
+
+    def rescale(self, ct: Ciphertext) -> Ciphertext:
+        return self._call_ct(self._lib.rescale, ct._h)
+
+    def level_down(self, ct: Ciphertext, level: int) -> Ciphertext:
+        return self._call_ct(self._lib.level_down, ct._h, int(level))
+
+    def make_power_basis(self, ct: Ciphertext, degree: int,
+                         relinearization_key: RelinearizationKey) -> list:
+        outs = (c_ct_p * degree)()
+        self._check(self._lib.power_basis(self._h, ct._h, int(degree), relinearization_key._h,
+                                          outs))
+        return [self._ct(outs[i]) for i in range(degree)]
+
+    def conjugate(self, ct: Ciphertext, conjugation_key: ConjugationKey) -> Ciphertext:
+        return self._call_ct(self._lib.galois, ct._h, conjugation_key._h)
+
+    def rotate(self, ct: Ciphertext, key, delta: int | None = None) -> Ciphertext:
+        """np.roll semantics: rotate(ct, key, k) decrypts to np.roll(v, k)."""
+        if isinstance(key, FixedRotationKey):
+            if delta is not None and int(delta) % self.slot_count != key.delta % self.slot_count:
+                raise RuntimeError(f"fixed rotation key is for {key.delta}, not {delta}")
+            return self._call_ct(self._lib.galois, ct._h, key._h)
+        if not isinstance(key, RotationKey):
+            raise TypeError("rotate needs a RotationKey or FixedRotationKey")
+        n = self.slot_count
+        left = (-int(delta)) % n
+        out = ct
+        for step in _naf_steps(left, n):
+            out = self._call_ct(self._lib.galois, out._h, key.left(step)._h)
+        if out is ct:
+            out = self._call_ct(self._lib.ct_copy, ct._h)
+        return out
+
+    def bootstrap(self, ct, *keys):
+        raise NotImplementedError(
+            "CKKS bootstrapping is not implemented yet (SURVEY.md section 8f item 1)")
+
+    # -- fused building blocks used by the optimised AES round ---------------------------------
+    def lincomb(self, cts: Sequence[Ciphertext], coeffs: Sequence[complex]) -> Ciphertext:
+        n = len(cts)
+        arr = (c_ct_p * n)(*[c._h for c in cts])
+        co = np.asarray(coeffs, dtype=np.complex128)
+        re = np.ascontiguousarray(co.real)
+        im = np.ascontiguousarray(co.imag)
+        return self._call_ct(self._lib.lincomb, arr, n, _as_ptr(re, C.c_double),
+                             _as_ptr(im, C.c_double))
+
+    def dot(self, a: Sequence[Ciphertext], b: Sequence[Ciphertext],
+            relinearization_key: RelinearizationKey) -> Ciphertext:
+        n = len(a)
+        aa = (c_ct_p * n)(*[c._h for c in a])
+        bb = (c_ct_p * n)(*[c._h for c in b])
+        return self._call_ct(self._lib.dot, aa, bb, n, relinearization_key._h)
+
+    def zeros(self, batch: int = 1, level: int | None = None) -> Ciphertext:
+        level = self.max_level if level is None else level
+        return self._call_ct(self._lib.ct_zero, batch, level)
+
+    def concat(self, cts: Sequence[Ciphertext]) -> Ciphertext:
+        arr = (c_ct_p * len(cts))(*[c._h for c in cts])
+        return self._call_ct(self._lib.ct_concat, arr, len(cts))
+
+    def slice(self, ct: Ciphertext, start: int, count: int) -> Ciphertext:
+        return self._call_ct(self._lib.ct_slice, ct._h, start, count)
+
+    def export_residues(self, ct: Ciphertext) -> np.ndarray:
+        n = 1 << self.log_coeff_count
+        out = np.empty((ct.batch, ct.npoly, ct.level + 1, n), dtype=np.uint64)
+        self._check(self._lib.ct_export(self._h, ct._h, _as_ptr(out, C.c_uint64)))
+        return out
+
+    def import_residues(self, arr: np.ndarray) -> Ciphertext:
+        a = np.ascontiguousarray(arr, dtype=np.uint64)
+        b, p, l1, _ = a.shape
+        return self._call_ct(self._lib.ct_import, _as_ptr(a, C.c_uint64), b, p, l1 - 1)
+
+    def synchronize(self):
+        self._check(self._lib.engine_sync(self._h))
+
+
+def _naf_steps(r: int, n: int) -> list:
+    """Signed power-of-two steps summing to r (mod n), fewest terms (NAF of r or r - n)."""
+    def naf(x):
+        out, i = [], 0
+        while x:
+            if x & 1:
+                d = 2 - (x & 3)
+                out.append(d << i)
+                x -= d
+            x >>= 1
+            i += 1
+        return out
+    if r == 0:
+        return []
+    a, b = naf(r), [-s for s in naf(n - r)]
+    return a if len(a) <= len(b) else b

@@ -1,0 +1,1404 @@
+// engine.hip -- MI355X (gfx950) RNS-CKKS engine implementing include/aesfhe.h.
+//
+// Replaces the closed desilofhe.Engine the reference calls (engine_context.py:6,32-85;
+// xor_service.py:36-129).  One HIP stream per engine; every operation is enqueued
+// asynchronously and host reads (decrypt / export) synchronise.  Device memory is recycled
+// through a size-bucketed pool, so steady-state operations never call hipMalloc.
+// Specification of every integer step: DESIGN.md section 3 (restated by oracle/ckks_oracle.c).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/aesfhe.h"
+#include "kernels_ops.h"
+
+using namespace aesfhe;
+
+// -----------------------------------------------------------------------------------------------
+// errors
+static thread_local char g_err[512];
+
+static int set_err(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+struct ApiError {
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] static void throw_err(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    throw ApiError{code, buf};
+}
+
+#define HIPC(x)                                                                              \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) throw_err(AESFHE_EDEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+#define API_BEGIN try {
+#define API_END                                                   \
+    }                                                             \
+    catch (const ApiError& e) {                                   \
+        return set_err(e.code, "%s", e.msg.c_str());              \
+    }                                                             \
+    catch (const std::bad_alloc&) {                               \
+        return set_err(AESFHE_ENOMEM, "host allocation failed");  \
+    }                                                             \
+    catch (const std::exception& e) {                             \
+        return set_err(AESFHE_EARG, "%s", e.what());              \
+    }                                                             \
+    return AESFHE_OK;
+
+extern "C" const char* aesfhe_last_error(void) { return g_err; }
+extern "C" const char* aesfhe_backend_name(void) { return "hip-gfx950"; }
+
+// -----------------------------------------------------------------------------------------------
+// engine state
+struct Pool {
+    std::map<size_t, std::vector<void*>> free_;
+    size_t held = 0, live = 0;
+    void* get(size_t bytes) {
+        bytes = (bytes + 255) & ~(size_t)255;
+        auto it = free_.find(bytes);
+        if (it != free_.end() && !it->second.empty()) {
+            void* p = it->second.back();
+            it->second.pop_back();
+            live += bytes;
+            return p;
+        }
+        void* p = nullptr;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            // release cached blocks and retry once
+            (void)hipGetLastError();
+            trim();
+            e = hipMalloc(&p, bytes);
+            if (e != hipSuccess) throw_err(AESFHE_ENOMEM, "hipMalloc(%zu) failed", bytes);
+        }
+        held += bytes;
+        live += bytes;
+        return p;
+    }
+    void put(void* p, size_t bytes) {
+        if (!p) return;
+        bytes = (bytes + 255) & ~(size_t)255;
+        free_[bytes].push_back(p);
+        live -= bytes;
+    }
+    void trim() {
+        hipDeviceSynchronize();
+        for (auto& kv : free_)
+            for (void* p : kv.second) {
+                hipFree(p);
+                held -= kv.first;
+            }
+        free_.clear();
+    }
+};
+
+struct ProfRec {
+    int fam;
+    hipEvent_t a, b;
+    double bytes;
+};
+
+struct aesfhe_engine {
+    int logN, N, L, K, dnum, np, Lp1;
+    int device;
+    u64 seed;
+    Chain chain;
+    hipStream_t stream;
+    Pool pool;
+    // device tables
+    u64 *q, *psi, *ipsi, *ninv;
+    double *qinv, *psif, *ipsif, *ninvf;
+    u64* iroot;  // host copy only needed
+    std::vector<u64> h_iroot;
+    // base conversion tables
+    u64 *mu_hatinv, *mu_hat, *md_phatinv, *md_phat, *md_pinv, *rs_inv, *rs_mod, *pmod;
+    double *mu_hatinvf, *mu_hatf, *md_phatinvf, *md_phatf, *md_pinvf, *rs_invf;
+    // small-argument upload ring (device) + pinned staging
+    char* ring_d = nullptr;
+    char* ring_h = nullptr;
+    size_t ring_size = 8u << 20, ring_off = 0;
+    // profiling
+    bool prof = false;
+    std::vector<ProfRec> recs;
+    std::vector<hipEvent_t> spare;
+    double prof_ms[4] = {0, 0, 0, 0};
+    double prof_bytes[4] = {0, 0, 0, 0};
+    int64_t prof_n[4] = {0, 0, 0, 0};
+
+    Tabs tabs() const {
+        Tabs t;
+        t.q = q;
+        t.qinv = qinv;
+        t.psi = psi;
+        t.psif = psif;
+        t.ipsi = ipsi;
+        t.ipsif = ipsif;
+        t.ninv = ninv;
+        t.ninvf = ninvf;
+        t.logN = logN;
+        t.Lp1 = Lp1;
+        return t;
+    }
+};
+
+struct aesfhe_key {
+    aesfhe_engine* eng;
+    int kind;
+    u64 galois;
+    u64 keyseed;
+    u64* d;
+    size_t bytes;
+};
+
+struct aesfhe_ct {
+    aesfhe_engine* eng;
+    int B, np, level, is_zero;
+    u64* d;
+    size_t bytes;
+};
+
+struct aesfhe_pt {
+    aesfhe_engine* eng;
+    int level;
+    u64* d;
+    size_t bytes;
+};
+
+// -----------------------------------------------------------------------------------------------
+// helpers
+static const int FAM_NTT = 0, FAM_KS = 1, FAM_EW = 2;
+
+struct ProfScope {
+    aesfhe_engine* e;
+    int fam;
+    double bytes;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(aesfhe_engine* e_, int f, double by) : e(e_), fam(f), bytes(by) {
+        if (!e->prof) return;
+        a = take();
+        b = take();
+        hipEventRecord(a, e->stream);
+    }
+    hipEvent_t take() {
+        if (!e->spare.empty()) {
+            hipEvent_t x = e->spare.back();
+            e->spare.pop_back();
+            return x;
+        }
+        hipEvent_t x;
+        hipEventCreate(&x);
+        return x;
+    }
+    ~ProfScope() {
+        if (!e->prof) return;
+        hipEventRecord(b, e->stream);
+        e->recs.push_back({fam, a, b, bytes});
+    }
+};
+
+static void prof_flush(aesfhe_engine* e) {
+    if (e->recs.empty()) return;
+    hipStreamSynchronize(e->stream);
+    for (auto& r : e->recs) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, r.a, r.b);
+        e->prof_ms[r.fam] += ms;
+        e->prof_bytes[r.fam] += r.bytes;
+        e->prof_n[r.fam] += 1;
+        e->spare.push_back(r.a);
+        e->spare.push_back(r.b);
+    }
+    e->recs.clear();
+}
+
+template <typename T>
+static T* upload_small(aesfhe_engine* e, const T* src, size_t count) {
+    size_t bytes = (count * sizeof(T) + 255) & ~(size_t)255;
+    if (bytes > e->ring_size) throw_err(AESFHE_EARG, "argument upload too large");
+    if (e->ring_off + bytes > e->ring_size) {
+        HIPC(hipStreamSynchronize(e->stream));
+        e->ring_off = 0;
+    }
+    memcpy(e->ring_h + e->ring_off, src, count * sizeof(T));
+    T* dst = (T*)(e->ring_d + e->ring_off);
+    HIPC(hipMemcpyAsync(dst, e->ring_h + e->ring_off, count * sizeof(T), hipMemcpyHostToDevice, e->stream));
+    e->ring_off += bytes;
+    return dst;
+}
+
+static u64* dalloc(aesfhe_engine* e, size_t words) { return (u64*)e->pool.get(words * 8); }
+static void dfree(aesfhe_engine* e, u64* p, size_t words) { e->pool.put(p, words * 8); }
+
+struct Tmp {  // RAII temporary device buffer from the pool
+    aesfhe_engine* e;
+    u64* p;
+    size_t w;
+    Tmp(aesfhe_engine* e_, size_t words) : e(e_), p(dalloc(e_, words)), w(words) {}
+    ~Tmp() { dfree(e, p, w); }
+};
+
+static aesfhe_ct* ct_new(aesfhe_engine* e, int B, int np, int level) {
+    auto* c = new aesfhe_ct;
+    c->eng = e;
+    c->B = B;
+    c->np = np;
+    c->level = level;
+    c->is_zero = 0;
+    c->bytes = (size_t)B * np * (level + 1) * e->N * 8;
+    c->d = (u64*)e->pool.get(c->bytes);
+    return c;
+}
+
+static aesfhe_ct* ct_zero_new(aesfhe_engine* e, int B, int np, int level) {
+    aesfhe_ct* c = ct_new(e, B, np, level);
+    HIPC(hipMemsetAsync(c->d, 0, c->bytes, e->stream));
+    c->is_zero = 1;
+    return c;
+}
+
+// A (possibly strided / truncated / broadcast) view of ciphertext data.
+struct View {
+    const u64* d;
+    int B, np, level;
+    long ps, bs;  // poly stride, batch stride (0 = broadcast)
+    bool zero;
+};
+
+static View view_of(const aesfhe_ct* c) {
+    View v;
+    v.d = c->d;
+    v.B = c->B;
+    v.np = c->np;
+    v.level = c->level;
+    v.ps = (long)(c->level + 1) * c->eng->N;
+    v.bs = (long)c->np * v.ps;
+    v.zero = c->is_zero;
+    return v;
+}
+
+static Opnd opnd(const View& v, int outB) {
+    Opnd o;
+    o.ptr = v.zero ? nullptr : v.d;
+    o.bs = (v.B == 1 && outB > 1) ? 0 : v.bs;
+    o.ps = v.ps;
+    o.np = v.np;
+    return o;
+}
+
+static Out out_of(aesfhe_ct* c) {
+    Out o;
+    o.ptr = c->d;
+    o.ps = (long)(c->level + 1) * c->eng->N;
+    o.bs = (long)c->np * o.ps;
+    return o;
+}
+
+static dim3 ew_grid(aesfhe_engine* e, int y, int z) { return dim3(e->N / 256, y, z); }
+
+// -----------------------------------------------------------------------------------------------
+// NTT dispatch
+template <int R1>
+static void ntt_fwd_t(aesfhe_engine* e, Span src, Span dst, int total) {
+    constexpr int CW = (kTile / R1) < kC2 ? (kTile / R1) : kC2;
+    constexpr int RW = (kTile / kC2) < R1 ? (kTile / kC2) : R1;
+    Tabs T = e->tabs();
+    hipLaunchKernelGGL(k_ntt_fwd_cols<R1>, dim3(kC2 / CW, total), dim3(256), 0, e->stream, src, dst, T);
+    hipLaunchKernelGGL(k_ntt_fwd_rows<R1>, dim3(R1 / RW, total), dim3(256), 0, e->stream, dst, T);
+}
+template <int R1>
+static void ntt_inv_t(aesfhe_engine* e, Span src, Span dst, int total) {
+    constexpr int CW = (kTile / R1) < kC2 ? (kTile / R1) : kC2;
+    constexpr int RW = (kTile / kC2) < R1 ? (kTile / kC2) : R1;
+    Tabs T = e->tabs();
+    hipLaunchKernelGGL(k_ntt_inv_rows<R1>, dim3(R1 / RW, total), dim3(256), 0, e->stream, src, dst, T);
+    hipLaunchKernelGGL(k_ntt_inv_cols<R1>, dim3(kC2 / CW, total), dim3(256), 0, e->stream, dst, T);
+}
+
+static void ntt(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
+    if (total <= 0) return;
+    ProfScope ps(e, FAM_NTT, 16.0 * e->N * (double)total);
+    switch (e->logN) {
+#define CASE(LG, R)                                                        \
+    case LG:                                                               \
+        if (inverse) ntt_inv_t<R>(e, src, dst, total);                     \
+        else ntt_fwd_t<R>(e, src, dst, total);                             \
+        break;
+        CASE(10, 4)
+        CASE(11, 8)
+        CASE(12, 16)
+        CASE(13, 32)
+        CASE(14, 64)
+        CASE(15, 128)
+        CASE(16, 256)
+        CASE(17, 512)
+#undef CASE
+        default:
+            throw_err(AESFHE_EUNSUPPORTED, "log_n %d not supported by the HIP NTT", e->logN);
+    }
+    HIPC(hipGetLastError());
+}
+
+static Span span_s(u64* base, long pstride, int nl, int nq, int qpid0, int spid0) {
+    Span s;
+    s.base = base;
+    s.pstride = pstride;
+    s.nl = nl;
+    s.nq = nq;
+    s.qpid0 = qpid0;
+    s.spid0 = spid0;
+    return s;
+}
+
+// -----------------------------------------------------------------------------------------------
+// engine creation: tables
+static void build_tables(aesfhe_engine* e) {
+    const int N = e->N, np = e->np, L = e->L, K = e->K, Lp1 = e->Lp1;
+    const auto& Q = e->chain.q;
+    std::vector<u64> hq(Q), hpsi((size_t)np * N), hipsi((size_t)np * N), hninv(np);
+    std::vector<double> hqinv(np), hpsif((size_t)np * N), hipsif((size_t)np * N), hninvf(np);
+    e->h_iroot.resize(np);
+    for (int p = 0; p < np; p++) {
+        u64 qq = Q[p];
+        hqinv[p] = 1.0 / (double)qq;
+        u64 psi = min_primitive_root(qq, N), ip = h_invmod(psi, qq);
+        std::vector<u64> pw(N), ipw(N);
+        pw[0] = ipw[0] = 1;
+        for (int k = 1; k < N; k++) {
+            pw[k] = h_mulmod(pw[k - 1], psi, qq);
+            ipw[k] = h_mulmod(ipw[k - 1], ip, qq);
+        }
+        for (int k = 0; k < N; k++) {
+            unsigned r = bit_reverse((unsigned)k, e->logN);
+            hpsi[(size_t)p * N + k] = pw[r];
+            hipsi[(size_t)p * N + k] = ipw[r];
+            hpsif[(size_t)p * N + k] = (double)pw[r] / (double)qq;
+            hipsif[(size_t)p * N + k] = (double)ipw[r] / (double)qq;
+        }
+        e->h_iroot[p] = pw[N / 2];
+        hninv[p] = h_invmod((u64)N, qq);
+        hninvf[p] = (double)hninv[p] / (double)qq;
+    }
+    auto up = [&](auto& vec, auto** dst) {
+        using T = typename std::remove_reference<decltype(vec)>::type::value_type;
+        size_t bytes = vec.size() * sizeof(T);
+        HIPC(hipMalloc((void**)dst, std::max<size_t>(bytes, 8)));
+        HIPC(hipMemcpy(*dst, vec.data(), bytes, hipMemcpyHostToDevice));
+    };
+    up(hq, &e->q);
+    up(hqinv, &e->qinv);
+    up(hpsi, &e->psi);
+    up(hpsif, &e->psif);
+    up(hipsi, &e->ipsi);
+    up(hipsif, &e->ipsif);
+    up(hninv, &e->ninv);
+    up(hninvf, &e->ninvf);
+
+    // ModUp tables per (digit j, alpha a): hatinv[i], hat[i][pid]
+    const size_t mu_sets = (size_t)e->dnum * K;
+    std::vector<u64> hhatinv(mu_sets * K, 0), hhat(mu_sets * K * np, 0);
+    std::vector<double> hhatinvf(mu_sets * K, 0), hhatf(mu_sets * K * np, 0);
+    for (int j = 0; j < e->dnum; j++)
+        for (int a = 1; a <= K; a++) {
+            int lo = j * K, hi = lo + a;
+            if (hi > Lp1) continue;
+            size_t set = (size_t)j * K + (a - 1);
+            for (int i = lo; i < hi; i++) {
+                u64 prod = 1;
+                for (int i2 = lo; i2 < hi; i2++)
+                    if (i2 != i) prod = h_mulmod(prod, Q[i2] % Q[i], Q[i]);
+                u64 hv = h_invmod(prod, Q[i]);
+                hhatinv[set * K + (i - lo)] = hv;
+                hhatinvf[set * K + (i - lo)] = (double)hv / (double)Q[i];
+                for (int pid = 0; pid < np; pid++) {
+                    u64 qt = Q[pid], h = 1;
+                    for (int i2 = lo; i2 < hi; i2++)
+                        if (i2 != i) h = h_mulmod(h, Q[i2] % qt, qt);
+                    hhat[(set * K + (i - lo)) * np + pid] = h;
+                    hhatf[(set * K + (i - lo)) * np + pid] = (double)h / (double)qt;
+                }
+            }
+        }
+    up(hhatinv, &e->mu_hatinv);
+    up(hhatinvf, &e->mu_hatinvf);
+    up(hhat, &e->mu_hat);
+    up(hhatf, &e->mu_hatf);
+
+    // ModDown tables
+    std::vector<u64> hphatinv(K), hphat((size_t)K * Lp1), hpinv(Lp1), hpmod(np, 0);
+    std::vector<double> hphatinvf(K), hphatf((size_t)K * Lp1), hpinvf(Lp1);
+    for (int k = 0; k < K; k++) {
+        u64 pk = Q[Lp1 + k], prod = 1;
+        for (int k2 = 0; k2 < K; k2++)
+            if (k2 != k) prod = h_mulmod(prod, Q[Lp1 + k2] % pk, pk);
+        hphatinv[k] = h_invmod(prod, pk);
+        hphatinvf[k] = (double)hphatinv[k] / (double)pk;
+        for (int i = 0; i < Lp1; i++) {
+            u64 qi = Q[i], h = 1;
+            for (int k2 = 0; k2 < K; k2++)
+                if (k2 != k) h = h_mulmod(h, Q[Lp1 + k2] % qi, qi);
+            hphat[(size_t)k * Lp1 + i] = h;
+            hphatf[(size_t)k * Lp1 + i] = (double)h / (double)qi;
+        }
+    }
+    for (int i = 0; i < Lp1; i++) {
+        u64 qi = Q[i], P = 1;
+        for (int k = 0; k < K; k++) P = h_mulmod(P, Q[Lp1 + k] % qi, qi);
+        hpmod[i] = P;
+        hpinv[i] = h_invmod(P, qi);
+        hpinvf[i] = (double)hpinv[i] / (double)qi;
+    }
+    up(hphatinv, &e->md_phatinv);
+    up(hphatinvf, &e->md_phatinvf);
+    up(hphat, &e->md_phat);
+    up(hphatf, &e->md_phatf);
+    up(hpinv, &e->md_pinv);
+    up(hpinvf, &e->md_pinvf);
+    up(hpmod, &e->pmod);
+
+    // rescale tables rs_inv[l][i] = q_l^{-1} mod q_i, rs_mod[l][i] = q_l mod q_i
+    std::vector<u64> hrinv((size_t)Lp1 * Lp1, 0), hrmod((size_t)Lp1 * Lp1, 0);
+    std::vector<double> hrinvf((size_t)Lp1 * Lp1, 0);
+    for (int l = 1; l <= L; l++)
+        for (int i = 0; i < l; i++) {
+            u64 qi = Q[i];
+            hrmod[(size_t)l * Lp1 + i] = Q[l] % qi;
+            hrinv[(size_t)l * Lp1 + i] = h_invmod(Q[l] % qi, qi);
+            hrinvf[(size_t)l * Lp1 + i] = (double)hrinv[(size_t)l * Lp1 + i] / (double)qi;
+        }
+    up(hrinv, &e->rs_inv);
+    up(hrinvf, &e->rs_invf);
+    up(hrmod, &e->rs_mod);
+}
+
+extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out) {
+    API_BEGIN
+    if (!pp || !out) throw_err(AESFHE_EARG, "null argument");
+    if (pp->log_n < 10 || pp->log_n > 17) throw_err(AESFHE_EARG, "log_n must be in [10, 17]");
+    if (pp->max_level < 1 || pp->special_primes < 1 || pp->special_primes > 16 ||
+        pp->max_level + 1 + pp->special_primes > kMaxPrimes)
+        throw_err(AESFHE_EARG, "bad level / special prime count");
+    if (pp->scale_bits < 20 || pp->scale_bits > 50 || pp->base_bits > 51 || pp->special_bits > 51)
+        throw_err(AESFHE_EARG, "bit sizes must keep every prime below 2^51");
+    std::unique_ptr<aesfhe_engine> e(new aesfhe_engine());
+    e->logN = pp->log_n;
+    e->N = 1 << pp->log_n;
+    e->L = pp->max_level;
+    e->K = pp->special_primes;
+    e->Lp1 = e->L + 1;
+    e->np = e->L + 1 + e->K;
+    e->dnum = (e->L + 1 + e->K - 1) / e->K;
+    e->device = pp->device;
+    e->seed = pp->seed;
+    if (pp->primes) {
+        e->chain.q.assign(pp->primes, pp->primes + e->np);
+        e->chain.scale = scales_from_primes(e->chain.q, e->L, pp->scale_bits);
+    } else {
+        e->chain = make_chain(e->logN, e->L, e->K, pp->base_bits, pp->special_bits, pp->scale_bits);
+    }
+    for (u64 x : e->chain.q)
+        if (x >> 51) throw_err(AESFHE_EARG, "prime %llu exceeds 2^51", (unsigned long long)x);
+    HIPC(hipSetDevice(e->device));
+    HIPC(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    build_tables(e.get());
+    HIPC(hipMalloc(&e->ring_d, e->ring_size));
+    HIPC(hipHostMalloc((void**)&e->ring_h, e->ring_size, hipHostMallocDefault));
+    *out = e.release();
+    API_END
+}
+
+extern "C" void aesfhe_engine_destroy(aesfhe_engine* e) {
+    if (!e) return;
+    hipSetDevice(e->device);
+    hipStreamSynchronize(e->stream);
+    for (auto& r : e->recs) {
+        hipEventDestroy(r.a);
+        hipEventDestroy(r.b);
+    }
+    for (auto ev : e->spare) hipEventDestroy(ev);
+    e->pool.trim();
+    void* ptrs[] = {e->q, e->psi, e->ipsi, e->ninv, e->qinv, e->psif, e->ipsif, e->ninvf,
+                    e->mu_hatinv, e->mu_hat, e->md_phatinv, e->md_phat, e->md_pinv, e->rs_inv,
+                    e->rs_mod, e->pmod, e->mu_hatinvf, e->mu_hatf, e->md_phatinvf, e->md_phatf,
+                    e->md_pinvf, e->rs_invf, e->ring_d};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    if (e->ring_h) hipHostFree(e->ring_h);
+    hipStreamDestroy(e->stream);
+    delete e;
+}
+
+extern "C" int aesfhe_engine_dims(const aesfhe_engine* e, int32_t d[4]) {
+    d[0] = e->logN;
+    d[1] = e->L;
+    d[2] = e->K;
+    d[3] = e->dnum;
+    return 0;
+}
+extern "C" int aesfhe_engine_primes(const aesfhe_engine* e, uint64_t* o) {
+    std::copy(e->chain.q.begin(), e->chain.q.end(), o);
+    return 0;
+}
+extern "C" int aesfhe_engine_scales(const aesfhe_engine* e, double* o) {
+    std::copy(e->chain.scale.begin(), e->chain.scale.end(), o);
+    return 0;
+}
+extern "C" double aesfhe_engine_mul_scale(const aesfhe_engine* e, int32_t l) {
+    if (l < 1 || l > e->L) return 0.0;
+    return e->chain.scale[l - 1] * (double)e->chain.q[l] / e->chain.scale[l];
+}
+extern "C" int aesfhe_engine_sync(aesfhe_engine* e) {
+    API_BEGIN
+    HIPC(hipStreamSynchronize(e->stream));
+    API_END
+}
+extern "C" int aesfhe_engine_profile(aesfhe_engine* e, int32_t en) {
+    API_BEGIN
+    prof_flush(e);
+    e->prof = en != 0;
+    if (en)
+        for (int i = 0; i < 4; i++) e->prof_ms[i] = e->prof_bytes[i] = 0, e->prof_n[i] = 0;
+    API_END
+}
+extern "C" int aesfhe_engine_profile_read(aesfhe_engine* e, const char* fam, int64_t* n,
+                                          double* ms, double* bytes) {
+    API_BEGIN
+    prof_flush(e);
+    int f = !strcmp(fam, "ntt") ? FAM_NTT : !strcmp(fam, "keyswitch") ? FAM_KS : !strcmp(fam, "elementwise") ? FAM_EW : 3;
+    if (f == 3) {
+        *n = e->prof_n[0] + e->prof_n[1] + e->prof_n[2];
+        *ms = e->prof_ms[0] + e->prof_ms[1] + e->prof_ms[2];
+        if (bytes) *bytes = e->prof_bytes[0] + e->prof_bytes[1] + e->prof_bytes[2];
+    } else {
+        *n = e->prof_n[f];
+        *ms = e->prof_ms[f];
+        if (bytes) *bytes = e->prof_bytes[f];
+    }
+    API_END
+}
+extern "C" int64_t aesfhe_engine_device_bytes(const aesfhe_engine* e) { return (int64_t)e->pool.held; }
+
+// -----------------------------------------------------------------------------------------------
+// host codec
+extern "C" int aesfhe_encode(int32_t logN, const double* re, const double* im, int64_t n_slots,
+                             double scale, int64_t* co) {
+    API_BEGIN
+    if (logN < 2 || logN > 17) throw_err(AESFHE_EARG, "log_n out of range");
+    Codec c(logN);
+    if (n_slots < 0 || n_slots > c.n) throw_err(AESFHE_EARG, "too many slots: %lld > %d", (long long)n_slots, c.n);
+    std::vector<double> vr(c.n, 0.0), vi(c.n, 0.0);
+    for (int64_t i = 0; i < n_slots; i++) {
+        vr[i] = re ? re[i] : 0.0;
+        vi[i] = im ? im[i] : 0.0;
+    }
+    c.special_inv(vr.data(), vi.data());
+    for (int i = 0; i < c.n; i++) {
+        double a = vr[i] * scale, b = vi[i] * scale;
+        if (!(std::fabs(a) < 9.0e18) || !(std::fabs(b) < 9.0e18))
+            throw_err(AESFHE_EARG, "encoded coefficient overflows int64 (scale too large?)");
+        co[i] = llround(a);
+        co[i + c.n] = llround(b);
+    }
+    API_END
+}
+
+extern "C" int aesfhe_decode(int32_t logN, const int64_t* co, double scale, double* re, double* im) {
+    API_BEGIN
+    if (logN < 2 || logN > 17) throw_err(AESFHE_EARG, "log_n out of range");
+    Codec c(logN);
+    for (int i = 0; i < c.n; i++) {
+        re[i] = (double)co[i] / scale;
+        im[i] = (double)co[i + c.n] / scale;
+    }
+    c.special(re, im);
+    API_END
+}
+
+// -----------------------------------------------------------------------------------------------
+// keys
+extern "C" void aesfhe_key_free(aesfhe_key* k) {
+    if (!k) return;
+    k->eng->pool.put(k->d, k->bytes);
+    delete k;
+}
+extern "C" int aesfhe_key_info(const aesfhe_key* k, int32_t* kind, uint64_t* g) {
+    *kind = k->kind;
+    *g = k->galois;
+    return 0;
+}
+extern "C" uint64_t aesfhe_galois_elt(int32_t logN, int64_t rot, int32_t conj) {
+    u64 M = 2ULL << logN, n = 1ULL << (logN - 1);
+    if (conj) return M - 1;
+    int64_t r = rot % (int64_t)n;
+    if (r < 0) r += (int64_t)n;
+    u64 ex = (n - (u64)r) % n;
+    return h_powmod(5, ex, M);
+}
+
+static aesfhe_key* key_new(aesfhe_engine* e, int kind, size_t words) {
+    auto* k = new aesfhe_key;
+    k->eng = e;
+    k->kind = kind;
+    k->galois = 0;
+    k->keyseed = 0;
+    k->bytes = words * 8;
+    k->d = (u64*)e->pool.get(k->bytes);
+    return k;
+}
+
+// residues of a small sampled polynomial for every prime (pid-major [np][N]) in NTT form
+static void sample_small_ntt(aesfhe_engine* e, u64* dst, int nprimes, u64 key, int kind) {
+    Span s = span_s(dst, 0, nprimes, std::min(nprimes, e->Lp1), 0, e->Lp1);
+    s.pstride = (long)nprimes * e->N;
+    hipLaunchKernelGGL(k_sample_small, dim3(e->N / 256, nprimes), dim3(256), 0, e->stream, s, key, kind, e->q, e->logN, e->Lp1);
+    ntt(e, s, s, nprimes, false);
+}
+
+extern "C" int aesfhe_key_secret(aesfhe_engine* e, uint64_t seed, aesfhe_key** out) {
+    API_BEGIN
+    aesfhe_key* k = key_new(e, 0, (size_t)e->np * e->N);
+    k->keyseed = derive(e->seed, seed);
+    sample_small_ntt(e, k->d, e->np, derive(k->keyseed, 1), 0);
+    *out = k;
+    API_END
+}
+
+extern "C" int aesfhe_key_public(aesfhe_engine* e, const aesfhe_key* sk, aesfhe_key** out) {
+    API_BEGIN
+    if (!sk || sk->kind != 0) throw_err(AESFHE_EARG, "public key needs a secret key");
+    const int N = e->N, nq = e->Lp1;
+    aesfhe_key* k = key_new(e, 1, (size_t)2 * nq * N);
+    k->keyseed = sk->keyseed;
+    u64* b = k->d;
+    u64* a = k->d + (size_t)nq * N;
+    Span sa = span_s(a, 0, nq, nq, 0, e->Lp1);
+    hipLaunchKernelGGL(k_sample_uniform, dim3(N / 256, nq), dim3(256), 0, e->stream, sa, derive(sk->keyseed, 2), e->q, e->logN, e->Lp1);
+    Tmp et(e, (size_t)nq * N);
+    sample_small_ntt(e, et.p, nq, derive(sk->keyseed, 3), 1);
+    hipLaunchKernelGGL(k_key_combine, dim3(N / 256, nq), dim3(256), 0, e->stream, a, sk->d, et.p, (const u64*)nullptr, (const u64*)nullptr, 0, 0, b, e->q, e->qinv, e->logN);
+    HIPC(hipGetLastError());
+    *out = k;
+    API_END
+}
+
+static aesfhe_key* make_ksk(aesfhe_engine* e, const aesfhe_key* sk, const u64* sprime, int kind, u64 g) {
+    const int N = e->N, np = e->np;
+    aesfhe_key* k = key_new(e, kind, (size_t)e->dnum * 2 * np * N);
+    k->galois = g;
+    k->keyseed = sk->keyseed;
+    u64 base = derive(derive(sk->keyseed, 4 + (u64)kind), g);
+    Tmp et(e, (size_t)np * N);
+    for (int d = 0; d < e->dnum; d++) {
+        u64* kb = k->d + ((size_t)d * 2 + 0) * np * N;
+        u64* ka = k->d + ((size_t)d * 2 + 1) * np * N;
+        Span sa = span_s(ka, 0, np, e->Lp1, 0, e->Lp1);
+        hipLaunchKernelGGL(k_sample_uniform, dim3(N / 256, np), dim3(256), 0, e->stream, sa, derive(base, 2 * (u64)d), e->q, e->logN, e->Lp1);
+        sample_small_ntt(e, et.p, np, derive(base, 2 * (u64)d + 1), 1);
+        int lo = d * e->K, hi = std::min(lo + e->K, e->Lp1);
+        hipLaunchKernelGGL(k_key_combine, dim3(N / 256, np), dim3(256), 0, e->stream, (const u64*)ka, sk->d, et.p, sprime, e->pmod, lo, hi, kb, e->q, e->qinv, e->logN);
+    }
+    HIPC(hipGetLastError());
+    return k;
+}
+
+extern "C" int aesfhe_key_relin(aesfhe_engine* e, const aesfhe_key* sk, aesfhe_key** out) {
+    API_BEGIN
+    if (!sk || sk->kind != 0) throw_err(AESFHE_EARG, "relinearization key needs a secret key");
+    Tmp s2(e, (size_t)e->np * e->N);
+    hipLaunchKernelGGL(k_square, dim3(e->N / 256, e->np), dim3(256), 0, e->stream, sk->d, s2.p, e->q, e->qinv, e->logN);
+    *out = make_ksk(e, sk, s2.p, 2, 0);
+    API_END
+}
+
+extern "C" int aesfhe_key_galois(aesfhe_engine* e, const aesfhe_key* sk, uint64_t g, aesfhe_key** out) {
+    API_BEGIN
+    if (!sk || sk->kind != 0) throw_err(AESFHE_EARG, "galois key needs a secret key");
+    if (!(g & 1) || g >= 2ULL * e->N) throw_err(AESFHE_EARG, "bad galois element");
+    Tmp sg(e, (size_t)e->np * e->N);
+    Span src = span_s(sk->d, 0, e->np, e->Lp1, 0, e->Lp1), dst = span_s(sg.p, 0, e->np, e->Lp1, 0, e->Lp1);
+    hipLaunchKernelGGL(k_galois, dim3(e->N / 256, e->np), dim3(256), 0, e->stream, src, dst, (u64)g, e->logN, e->Lp1);
+    *out = make_ksk(e, sk, sg.p, 3, g);
+    API_END
+}
+
+// -----------------------------------------------------------------------------------------------
+// ciphertext management
+extern "C" void aesfhe_ct_free(aesfhe_ct* c) {
+    if (!c) return;
+    c->eng->pool.put(c->d, c->bytes);
+    delete c;
+}
+extern "C" int aesfhe_ct_info(const aesfhe_ct* c, int32_t info[4]) {
+    info[0] = c->B;
+    info[1] = c->np;
+    info[2] = c->level;
+    info[3] = c->is_zero;
+    return 0;
+}
+extern "C" int aesfhe_ct_export(aesfhe_engine* e, const aesfhe_ct* c, uint64_t* out) {
+    API_BEGIN
+    HIPC(hipMemcpyAsync(out, c->d, c->bytes, hipMemcpyDeviceToHost, e->stream));
+    HIPC(hipStreamSynchronize(e->stream));
+    API_END
+}
+extern "C" int aesfhe_ct_import(aesfhe_engine* e, const uint64_t* in, int32_t B, int32_t np,
+                                int32_t level, aesfhe_ct** out) {
+    API_BEGIN
+    if (B < 1 || np < 1 || np > 3 || level < 0 || level > e->L) throw_err(AESFHE_EARG, "bad shape");
+    aesfhe_ct* c = ct_new(e, B, np, level);
+    HIPC(hipMemcpyAsync(c->d, in, c->bytes, hipMemcpyHostToDevice, e->stream));
+    HIPC(hipStreamSynchronize(e->stream));
+    *out = c;
+    API_END
+}
+extern "C" int aesfhe_ct_copy(aesfhe_engine* e, const aesfhe_ct* c, aesfhe_ct** out) {
+    API_BEGIN
+    aesfhe_ct* r = ct_new(e, c->B, c->np, c->level);
+    HIPC(hipMemcpyAsync(r->d, c->d, c->bytes, hipMemcpyDeviceToDevice, e->stream));
+    r->is_zero = c->is_zero;
+    *out = r;
+    API_END
+}
+extern "C" int aesfhe_ct_slice(aesfhe_engine* e, const aesfhe_ct* c, int32_t start, int32_t count, aesfhe_ct** out) {
+    API_BEGIN
+    if (start < 0 || count < 1 || start + count > c->B) throw_err(AESFHE_EARG, "bad slice");
+    aesfhe_ct* r = ct_new(e, count, c->np, c->level);
+    size_t per = c->bytes / c->B;
+    HIPC(hipMemcpyAsync(r->d, (char*)c->d + per * start, per * count, hipMemcpyDeviceToDevice, e->stream));
+    r->is_zero = c->is_zero;
+    *out = r;
+    API_END
+}
+extern "C" int aesfhe_ct_concat(aesfhe_engine* e, const aesfhe_ct* const* parts, int32_t n, aesfhe_ct** out) {
+    API_BEGIN
+    if (n < 1) throw_err(AESFHE_EARG, "empty concat");
+    int B = 0, allz = 1;
+    for (int i = 0; i < n; i++) {
+        if (parts[i]->level != parts[0]->level || parts[i]->np != parts[0]->np)
+            throw_err(AESFHE_EARG, "concat parts differ in level/npoly");
+        B += parts[i]->B;
+        allz &= parts[i]->is_zero;
+    }
+    aesfhe_ct* r = ct_new(e, B, parts[0]->np, parts[0]->level);
+    size_t off = 0;
+    for (int i = 0; i < n; i++) {
+        HIPC(hipMemcpyAsync((char*)r->d + off, parts[i]->d, parts[i]->bytes, hipMemcpyDeviceToDevice, e->stream));
+        off += parts[i]->bytes;
+    }
+    r->is_zero = allz;
+    *out = r;
+    API_END
+}
+extern "C" int aesfhe_ct_zero(aesfhe_engine* e, int32_t B, int32_t level, aesfhe_ct** out) {
+    API_BEGIN
+    if (B < 1 || level < 0 || level > e->L) throw_err(AESFHE_EARG, "bad zero shape");
+    *out = ct_zero_new(e, B, 2, level);
+    API_END
+}
+
+extern "C" int aesfhe_pt_create(aesfhe_engine* e, const int64_t* co, int32_t level, aesfhe_pt** out) {
+    API_BEGIN
+    if (level < 0 || level > e->L) throw_err(AESFHE_EARG, "bad plaintext level");
+    const int N = e->N, nl = level + 1;
+    auto* p = new aesfhe_pt;
+    p->eng = e;
+    p->level = level;
+    p->bytes = (size_t)nl * N * 8;
+    p->d = (u64*)e->pool.get(p->bytes);
+    Tmp dco(e, N);
+    HIPC(hipMemcpyAsync(dco.p, co, (size_t)N * 8, hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, nl, 1), dim3(256), 0, e->stream, (const i64*)dco.p, p->d, nl, e->q, e->logN);
+    Span s = span_s(p->d, 0, nl, nl, 0, e->Lp1);
+    ntt(e, s, s, nl, false);
+    // the host buffer `co` may be reused by the caller once we return
+    HIPC(hipStreamSynchronize(e->stream));
+    *out = p;
+    API_END
+}
+extern "C" void aesfhe_pt_free(aesfhe_pt* p) {
+    if (!p) return;
+    p->eng->pool.put(p->d, p->bytes);
+    delete p;
+}
+
+// -----------------------------------------------------------------------------------------------
+// encryption / decryption
+extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int64_t* co, int32_t B,
+                              int32_t level, uint64_t nonce, aesfhe_ct** out) {
+    API_BEGIN
+    if (!key || (key->kind != 0 && key->kind != 1)) throw_err(AESFHE_EARG, "encryption key must be pk or sk");
+    if (level < 0 || level > e->L || B < 1) throw_err(AESFHE_EARG, "bad level/batch");
+    const int N = e->N, nl = level + 1;
+    const long step = (long)nl * N;
+    aesfhe_ct* c = ct_new(e, B, 2, level);
+    Tmp vem(e, (size_t)B * 4 * step);
+    Tmp dco(e, (size_t)B * N);
+    HIPC(hipMemcpyAsync(dco.p, co, (size_t)B * N * 8, hipMemcpyHostToDevice, e->stream));
+    const u64 base = derive(derive(e->seed, 0xE0CULL), nonce);
+    std::vector<u64> k0s(B);
+    for (int b = 0; b < B; b++) {
+        u64 k0 = derive(base, 3 * (u64)b), k1 = derive(base, 3 * (u64)b + 1), k2 = derive(base, 3 * (u64)b + 2);
+        k0s[b] = k0;
+        u64* vb = vem.p + (size_t)b * 4 * step;
+        Span sv = span_s(vb, 0, nl, nl, 0, e->Lp1), se0 = span_s(vb + step, 0, nl, nl, 0, e->Lp1), se1 = span_s(vb + 2 * step, 0, nl, nl, 0, e->Lp1);
+        if (key->kind == 1)
+            hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, sv, k0, 0, e->q, e->logN, e->Lp1);
+        hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, se0, k1, 1, e->q, e->logN, e->Lp1);
+        if (key->kind == 1)
+            hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, se1, k2, 1, e->q, e->logN, e->Lp1);
+        hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, nl, 1), dim3(256), 0, e->stream, (const i64*)(dco.p + (size_t)b * N), vb + 3 * step, nl, e->q, e->logN);
+    }
+    // NTT everything: B * 4 groups of nl limbs (pid = limb index)
+    Span all = span_s(vem.p, step, nl, nl, 0, e->Lp1);
+    ntt(e, all, all, B * 4 * nl, false);
+    if (key->kind == 1) {
+        const u64* pk0 = key->d;
+        const u64* pk1 = key->d + (size_t)e->Lp1 * N;
+        hipLaunchKernelGGL(k_enc_pk, dim3(N / 256, nl, B), dim3(256), 0, e->stream, (const u64*)vem.p, pk0, pk1, c->d, nl, e->q, e->qinv, e->logN);
+    } else {
+        u64* dk = upload_small(e, k0s.data(), k0s.size());
+        hipLaunchKernelGGL(k_enc_sk, dim3(N / 256, nl, B), dim3(256), 0, e->stream, (const u64*)vem.p, (const u64*)key->d, c->d, nl, e->q, e->qinv, (const u64*)dk, e->logN);
+    }
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(e->stream));  // host coefficient buffer may be reused by caller
+    *out = c;
+    API_END
+}
+
+extern "C" int aesfhe_decrypt(aesfhe_engine* e, const aesfhe_key* sk, const aesfhe_ct* c, int64_t* out) {
+    API_BEGIN
+    if (!sk || sk->kind != 0) throw_err(AESFHE_EARG, "decryption needs the secret key");
+    const int N = e->N;
+    Tmp t(e, (size_t)c->B * N);
+    View v = view_of(c);
+    hipLaunchKernelGGL(k_dec_limb0, dim3(N / 256, 1, c->B), dim3(256), 0, e->stream, v.d, v.bs, v.ps, c->np, (const u64*)sk->d, t.p, e->chain.q[0], 1.0 / (double)e->chain.q[0], e->logN);
+    Span s = span_s(t.p, N, 1, 1, 0, e->Lp1);
+    ntt(e, s, s, c->B, true);
+    std::vector<u64> h((size_t)c->B * N);
+    HIPC(hipMemcpyAsync(h.data(), t.p, h.size() * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPC(hipStreamSynchronize(e->stream));
+    const u64 q = e->chain.q[0];
+    for (size_t i = 0; i < h.size(); i++) out[i] = h[i] > q / 2 ? (int64_t)h[i] - (int64_t)q : (int64_t)h[i];
+    API_END
+}
+
+// -----------------------------------------------------------------------------------------------
+// core primitives
+// rescale a view (level l >= 1) into a new ct at level l-1
+static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in) {
+    const int N = e->N, l = in.level, P = in.B * in.np;
+    aesfhe_ct* r = ct_new(e, in.B, in.np, l - 1);
+    ProfScope ps(e, FAM_EW, 0);
+    Tmp x(e, (size_t)P * N), t(e, (size_t)P * l * N);
+    // INTT of limb l of every poly: source poly p of batch b at d + b*bs + p*ps + l*N
+    // (expressed as a Span over the flattened polys; requires bs == np*ps, true for compact views)
+    Span src = span_s((u64*)in.d + (long)l * N, in.ps, 1, 1, l, e->Lp1);
+    Span dx = span_s(x.p, N, 1, 1, l, e->Lp1);
+    if (in.bs != (long)in.np * in.ps && in.B > 1) throw_err(AESFHE_EARG, "rescale of non-compact view");
+    ntt(e, src, dx, P, true);
+    hipLaunchKernelGGL(k_rescale_spread, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN);
+    Span st = span_s(t.p, (long)l * N, l, l, 0, e->Lp1);
+    ntt(e, st, st, P * l, false);
+    Opnd c = opnd(in, in.B);
+    hipLaunchKernelGGL(k_rescale_finish, dim3(N / 256, l, P), dim3(256), 0, e->stream, c, (const u64*)t.p, out_of(r), in.np, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN);
+    HIPC(hipGetLastError());
+    return r;
+}
+
+// constant factor tables for A + B X^{N/2} over limbs 0..nl-1
+static void const_factors(aesfhe_engine* e, int64_t A, int64_t Bc, int nl, std::vector<u64>& f, std::vector<double>& ff) {
+    f.resize(2 * nl);
+    ff.resize(2 * nl);
+    for (int i = 0; i < nl; i++) {
+        u64 q = e->chain.q[i];
+        u64 a = h_smod(A, q), b = h_smod(Bc, q);
+        u64 bi = h_mulmod(b, e->h_iroot[i], q);
+        f[2 * i] = h_addmod(a, bi, q);
+        f[2 * i + 1] = h_submod(a, bi, q);
+        ff[2 * i] = (double)f[2 * i] / (double)q;
+        ff[2 * i + 1] = (double)f[2 * i + 1] / (double)q;
+    }
+}
+
+// out (compact ct at in.level) (+)= in * (A + B X^{N/2})
+static void mul_const_into(aesfhe_engine* e, const View& in, int64_t A, int64_t Bc, aesfhe_ct* o, int acc) {
+    const int nl = in.level + 1;
+    std::vector<u64> f;
+    std::vector<double> ff;
+    const_factors(e, A, Bc, nl, f, ff);
+    u64* df = upload_small(e, f.data(), f.size());
+    double* dff = upload_small(e, ff.data(), ff.size());
+    ProfScope ps(e, FAM_EW, 0);
+    hipLaunchKernelGGL(k_mul_const, ew_grid(e, nl, o->B * in.np), dim3(256), 0, e->stream, opnd(in, o->B), out_of(o), in.np, (const u64*)df, (const double*)dff, e->q, acc, e->logN);
+    HIPC(hipGetLastError());
+}
+
+static View truncated(const View& v, int level) {
+    View t = v;
+    t.level = level;
+    return t;
+}
+
+static aesfhe_ct* level_down_view(aesfhe_engine* e, const View& v, int lt) {
+    if (lt == v.level) {
+        aesfhe_ct* r = ct_new(e, v.B, v.np, v.level);
+        if (v.zero) {
+            HIPC(hipMemsetAsync(r->d, 0, r->bytes, e->stream));
+            r->is_zero = 1;
+        } else if (v.bs == (long)v.np * v.ps) {
+            HIPC(hipMemcpyAsync(r->d, v.d, r->bytes, hipMemcpyDeviceToDevice, e->stream));
+        } else {
+            throw_err(AESFHE_EARG, "copy of non-compact view");
+        }
+        return r;
+    }
+    if (v.zero) return ct_zero_new(e, v.B, v.np, lt);
+    View t = truncated(v, lt + 1);
+    int64_t C = llround(e->chain.scale[lt] * (double)e->chain.q[lt + 1] / e->chain.scale[v.level]);
+    aesfhe_ct* tmp = ct_new(e, v.B, v.np, lt + 1);
+    mul_const_into(e, t, C, 0, tmp, 0);
+    aesfhe_ct* r = rescale_view(e, view_of(tmp));
+    aesfhe_ct_free(tmp);
+    return r;
+}
+
+// owned-or-borrowed aligned operand
+struct Aligned {
+    aesfhe_ct* owned = nullptr;
+    View v;
+    ~Aligned() {
+        if (owned) aesfhe_ct_free(owned);
+    }
+};
+
+static void align_to(aesfhe_engine* e, const aesfhe_ct* c, int l, Aligned& a) {
+    if (c->level == l) {
+        a.v = view_of(c);
+    } else {
+        a.owned = level_down_view(e, view_of(c), l);
+        a.v = view_of(a.owned);
+    }
+}
+
+static void check_bcast(int a, int b) {
+    if (a != b && a != 1 && b != 1) throw_err(AESFHE_EARG, "batch mismatch %d vs %d", a, b);
+}
+
+extern "C" int aesfhe_rescale(aesfhe_engine* e, const aesfhe_ct* c, aesfhe_ct** out) {
+    API_BEGIN
+    if (c->level < 1) throw_err(AESFHE_ELEVEL, "cannot rescale a level-0 ciphertext");
+    if (c->is_zero) *out = ct_zero_new(e, c->B, c->np, c->level - 1);
+    else *out = rescale_view(e, view_of(c));
+    API_END
+}
+
+extern "C" int aesfhe_level_down(aesfhe_engine* e, const aesfhe_ct* c, int32_t lt, aesfhe_ct** out) {
+    API_BEGIN
+    if (lt < 0 || lt > c->level) throw_err(AESFHE_EARG, "level_down target %d not in [0,%d]", lt, c->level);
+    *out = level_down_view(e, view_of(c), lt);
+    API_END
+}
+
+static int addsub(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* b, int sub, aesfhe_ct** out) {
+    API_BEGIN
+    check_bcast(a->B, b->B);
+    int l = std::min(a->level, b->level);
+    Aligned A, Bv;
+    align_to(e, a, l, A);
+    align_to(e, b, l, Bv);
+    int B = std::max(a->B, b->B), np = std::max(a->np, b->np);
+    aesfhe_ct* r = ct_new(e, B, np, l);
+    ProfScope ps(e, FAM_EW, 0);
+    hipLaunchKernelGGL(k_addsub, ew_grid(e, l + 1, B * np), dim3(256), 0, e->stream, opnd(A.v, B), opnd(Bv.v, B), out_of(r), np, e->q, sub, e->logN);
+    HIPC(hipGetLastError());
+    r->is_zero = a->is_zero && b->is_zero;
+    *out = r;
+    API_END
+}
+extern "C" int aesfhe_add(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* b, aesfhe_ct** out) { return addsub(e, a, b, 0, out); }
+extern "C" int aesfhe_sub(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* b, aesfhe_ct** out) { return addsub(e, a, b, 1, out); }
+extern "C" int aesfhe_negate(aesfhe_engine* e, const aesfhe_ct* a, aesfhe_ct** out) {
+    API_BEGIN
+    aesfhe_ct* r = ct_new(e, a->B, a->np, a->level);
+    View z = view_of(a);
+    z.zero = true;
+    hipLaunchKernelGGL(k_addsub, ew_grid(e, a->level + 1, a->B * a->np), dim3(256), 0, e->stream, opnd(z, a->B), opnd(view_of(a), a->B), out_of(r), a->np, e->q, 1, e->logN);
+    HIPC(hipGetLastError());
+    r->is_zero = a->is_zero;
+    *out = r;
+    API_END
+}
+
+extern "C" int aesfhe_add_pt(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_pt* pt, aesfhe_ct** out) {
+    API_BEGIN
+    if (pt->level < c->level) throw_err(AESFHE_EARG, "plaintext level %d below ciphertext level %d", pt->level, c->level);
+    aesfhe_ct* r = ct_new(e, c->B, c->np, c->level);
+    hipLaunchKernelGGL(k_add_pt, ew_grid(e, c->level + 1, c->B * c->np), dim3(256), 0, e->stream, opnd(view_of(c), c->B), (const u64*)pt->d, out_of(r), c->np, e->q, e->logN);
+    HIPC(hipGetLastError());
+    *out = r;
+    API_END
+}
+
+extern "C" int aesfhe_mul_pt(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_pt* pt, aesfhe_ct** out) {
+    API_BEGIN
+    if (c->level < 1) throw_err(AESFHE_ELEVEL, "no level left for a plaintext multiplication");
+    if (pt->level < c->level) throw_err(AESFHE_EARG, "plaintext level %d below ciphertext level %d", pt->level, c->level);
+    if (c->is_zero) {
+        *out = ct_zero_new(e, c->B, c->np, c->level - 1);
+    } else {
+        aesfhe_ct* t = ct_new(e, c->B, c->np, c->level);
+        hipLaunchKernelGGL(k_mul_pt, ew_grid(e, c->level + 1, c->B * c->np), dim3(256), 0, e->stream, opnd(view_of(c), c->B), (const u64*)pt->d, out_of(t), c->np, e->q, e->qinv, e->logN);
+        HIPC(hipGetLastError());
+        *out = rescale_view(e, view_of(t));
+        aesfhe_ct_free(t);
+    }
+    API_END
+}
+
+extern "C" int aesfhe_mul_const(aesfhe_engine* e, const aesfhe_ct* c, double re, double im, aesfhe_ct** out) {
+    API_BEGIN
+    if (c->level < 1) throw_err(AESFHE_ELEVEL, "no level left for a constant multiplication");
+    double s = aesfhe_engine_mul_scale(e, c->level);
+    int64_t A = llround(re * s), Bc = llround(im * s);
+    if (c->is_zero || (A == 0 && Bc == 0)) {
+        *out = ct_zero_new(e, c->B, c->np, c->level - 1);
+    } else {
+        aesfhe_ct* t = ct_new(e, c->B, c->np, c->level);
+        mul_const_into(e, view_of(c), A, Bc, t, 0);
+        *out = rescale_view(e, view_of(t));
+        aesfhe_ct_free(t);
+    }
+    API_END
+}
+
+// -----------------------------------------------------------------------------------------------
+// key switching of one polynomial per batch element.
+// d: NTT-domain polynomial of batch element b at d + b*dbs (level l, limbs contiguous).
+// Result: out poly 0/1 = addend_{0/1} + KS(d)_{0/1}, written into ct `o` (2 polys, level l).
+static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, const aesfhe_key* k,
+                      Opnd addend, aesfhe_ct* o) {
+    const int N = e->N, K = e->K, ne = l + 1 + K;
+    const long lN = (long)(l + 1) * N, neN = (long)ne * N;
+    ProfScope ps(e, FAM_KS, 0);
+    Tmp dc(e, (size_t)B * lN), ext(e, (size_t)B * neN), acc(e, (size_t)B * 2 * neN);
+    // 1. INTT copy of the input
+    Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1), sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
+    ntt(e, sd, sdc, B * (l + 1), true);
+    const int beta = (l + 1 + K - 1) / K;
+    for (int j = 0; j < beta; j++) {
+        const int lo = j * K, hi = std::min(lo + K, l + 1), alpha = hi - lo;
+        const size_t set = (size_t)j * K + (alpha - 1);
+        // 2. ModUp base conversion to every other limb, then NTT those limbs
+        hipLaunchKernelGGL(k_modup, dim3(N / 256, (ne + 7) / 8, B), dim3(256), 0, e->stream, (const u64*)dc.p, lN, ext.p, neN, lo, alpha, l, ne,
+                           (const u64*)(e->mu_hatinv + set * K), (const double*)(e->mu_hatinvf + set * K),
+                           (const u64*)(e->mu_hat + set * K * e->np), (const double*)(e->mu_hatf + set * K * e->np),
+                           e->np, e->q, e->Lp1, e->logN);
+        HIPC(hipGetLastError());
+        // NTT of targets: limbs [0, lo) and [hi, ne) of every batch element
+        if (lo > 0) {
+            Span s1 = span_s(ext.p, neN, lo, lo, 0, e->Lp1);
+            ntt(e, s1, s1, B * lo, false);
+        }
+        {
+            int nrest = ne - hi, nq_rest = (l + 1) - hi;
+            Span s2 = span_s(ext.p + (long)hi * N, neN, nrest, nq_rest, hi, e->Lp1);
+            ntt(e, s2, s2, B * nrest, false);
+        }
+        // 3. inner product with the key digit
+        const u64* kb = k->d + ((size_t)j * 2 + 0) * e->np * N;
+        const u64* ka = k->d + ((size_t)j * 2 + 1) * e->np * N;
+        hipLaunchKernelGGL(k_ks_inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, (const u64*)ext.p, neN, kb, ka, acc.p, 2 * neN, neN, B, lo, hi, l, e->q, e->qinv, e->Lp1, j == 0 ? 1 : 0, e->logN);
+        HIPC(hipGetLastError());
+    }
+    // 4. ModDown: INTT special limbs of both accumulators
+    {
+        Span ssp = span_s(acc.p + lN, neN, K, 0, 0, e->Lp1);
+        ntt(e, ssp, ssp, B * 2 * K, true);
+    }
+    Tmp conv(e, (size_t)B * 2 * lN);
+    hipLaunchKernelGGL(k_moddown, dim3(N / 256, (l + 1 + 7) / 8, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, conv.p, 2 * lN, lN, K,
+                       (const u64*)e->md_phatinv, (const double*)e->md_phatinvf, (const u64*)e->md_phat, (const double*)e->md_phatf, e->Lp1, e->q, e->logN);
+    HIPC(hipGetLastError());
+    {
+        Span sc = span_s(conv.p, lN, l + 1, l + 1, 0, e->Lp1);
+        ntt(e, sc, sc, B * 2 * (l + 1), false);
+    }
+    hipLaunchKernelGGL(k_moddown_finish, dim3(N / 256, l + 1, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, (const u64*)conv.p, 2 * lN, lN, addend, out_of(o), e->q, (const u64*)e->md_pinv, (const double*)e->md_pinvf, e->logN);
+    HIPC(hipGetLastError());
+}
+
+static aesfhe_ct* relin_ct(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_key* rlk) {
+    const int l = c->level;
+    aesfhe_ct* r = ct_new(e, c->B, 2, l);
+    View v = view_of(c);
+    Opnd add = opnd(v, c->B);
+    add.np = 2;  // d0, d1 are the addends of outputs 0, 1
+    keyswitch(e, c->d + 2 * v.ps, v.bs, c->B, l, rlk, add, r);
+    return r;
+}
+
+static aesfhe_ct* tensor_ct(aesfhe_engine* e, const View& a, const View& b, int B) {
+    const int l = a.level;
+    aesfhe_ct* t = ct_new(e, B, 3, l);
+    ProfScope ps(e, FAM_EW, 0);
+    hipLaunchKernelGGL(k_tensor, ew_grid(e, l + 1, B), dim3(256), 0, e->stream, opnd(a, B), opnd(b, B), out_of(t), e->q, e->qinv, 0, e->logN);
+    HIPC(hipGetLastError());
+    return t;
+}
+
+extern "C" int aesfhe_tensor(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* b, aesfhe_ct** out) {
+    API_BEGIN
+    if (a->np != 2 || b->np != 2) throw_err(AESFHE_EDEGREE, "tensor inputs should have 2 polynomials");
+    check_bcast(a->B, b->B);
+    int l = std::min(a->level, b->level), B = std::max(a->B, b->B);
+    if (a->is_zero || b->is_zero) {
+        *out = ct_zero_new(e, B, 3, l);
+    } else {
+        Aligned A, Bv;
+        align_to(e, a, l, A);
+        align_to(e, b, l, Bv);
+        *out = tensor_ct(e, A.v, Bv.v, B);
+    }
+    API_END
+}
+
+extern "C" int aesfhe_relinearize(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_key* rlk, aesfhe_ct** out) {
+    API_BEGIN
+    if (c->np != 3) throw_err(AESFHE_EDEGREE, "Input ciphertext should have 3 polynomials");
+    if (!rlk || rlk->kind != 2) throw_err(AESFHE_EARG, "relinearize needs a relinearization key");
+    if (c->is_zero) *out = ct_zero_new(e, c->B, 2, c->level);
+    else *out = relin_ct(e, c, rlk);
+    API_END
+}
+
+static aesfhe_ct* mul_ct(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* b, const aesfhe_key* rlk) {
+    check_bcast(a->B, b->B);
+    int l = std::min(a->level, b->level), B = std::max(a->B, b->B);
+    if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a ciphertext multiplication");
+    if (a->is_zero || b->is_zero) return ct_zero_new(e, B, 2, l - 1);
+    Aligned A, Bv;
+    align_to(e, a, l, A);
+    align_to(e, b, l, Bv);
+    aesfhe_ct* t = tensor_ct(e, A.v, Bv.v, B);
+    aesfhe_ct* rl = relin_ct(e, t, rlk);
+    aesfhe_ct_free(t);
+    aesfhe_ct* r = rescale_view(e, view_of(rl));
+    aesfhe_ct_free(rl);
+    return r;
+}
+
+extern "C" int aesfhe_mul(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* b, const aesfhe_key* rlk, aesfhe_ct** out) {
+    API_BEGIN
+    if (!rlk || rlk->kind != 2) throw_err(AESFHE_EARG, "multiply needs a relinearization key");
+    if (a->np != 2 || b->np != 2) throw_err(AESFHE_EDEGREE, "multiply inputs should have 2 polynomials");
+    *out = mul_ct(e, a, b, rlk);
+    API_END
+}
+
+extern "C" int aesfhe_galois(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_key* gk, aesfhe_ct** out) {
+    API_BEGIN
+    if (!gk || gk->kind != 3) throw_err(AESFHE_EARG, "galois needs a rotation/conjugation key");
+    if (c->np != 2) throw_err(AESFHE_EDEGREE, "Input ciphertext should have 2 polynomials");
+    const int N = e->N, l = c->level;
+    if (c->is_zero) {
+        *out = ct_zero_new(e, c->B, 2, l);
+    } else {
+        // permute both polynomials into a temporary ct, then key-switch poly 1
+        aesfhe_ct* p = ct_new(e, c->B, 2, l);
+        Span src = span_s(c->d, (long)(l + 1) * N, l + 1, l + 1, 0, e->Lp1), dst = span_s(p->d, (long)(l + 1) * N, l + 1, l + 1, 0, e->Lp1);
+        hipLaunchKernelGGL(k_galois, dim3(N / 256, c->B * 2 * (l + 1)), dim3(256), 0, e->stream, src, dst, (u64)gk->galois, e->logN, e->Lp1);
+        HIPC(hipGetLastError());
+        aesfhe_ct* r = ct_new(e, c->B, 2, l);
+        View pv = view_of(p);
+        Opnd add = opnd(pv, c->B);
+        add.np = 1;  // only output 0 gets sigma(c0)
+        keyswitch(e, p->d + pv.ps, pv.bs, c->B, l, gk, add, r);
+        aesfhe_ct_free(p);
+        *out = r;
+    }
+    API_END
+}
+
+extern "C" int aesfhe_power_basis(aesfhe_engine* e, const aesfhe_ct* c, int32_t d, const aesfhe_key* rlk, aesfhe_ct** outs) {
+    API_BEGIN
+    if (d < 1) throw_err(AESFHE_EARG, "degree must be >= 1");
+    if (!rlk || rlk->kind != 2) throw_err(AESFHE_EARG, "power basis needs a relinearization key");
+    if (c->np != 2) throw_err(AESFHE_EDEGREE, "power basis input should have 2 polynomials");
+    int need = 0;
+    while ((1 << need) < d) need++;
+    if (c->level < need) throw_err(AESFHE_ELEVEL, "power basis of degree %d needs %d levels, have %d", d, need, c->level);
+    std::vector<aesfhe_ct*> pw(d + 1, nullptr);
+    // memo of level-downed powers: (k, level) -> ct
+    std::map<std::pair<int, int>, aesfhe_ct*> memo;
+    try {
+        aesfhe_ct_copy(e, c, &pw[1]);
+        auto at_level = [&](int k, int lv) -> aesfhe_ct* {
+            if (pw[k]->level == lv) return pw[k];
+            auto key = std::make_pair(k, lv);
+            auto it = memo.find(key);
+            if (it != memo.end()) return it->second;
+            aesfhe_ct* x = level_down_view(e, view_of(pw[k]), lv);
+            memo[key] = x;
+            return x;
+        };
+        for (int k = 2; k <= d; k++) {
+            int hi = 1;
+            while (hi * 2 <= k) hi *= 2;
+            int k1 = (hi == k) ? k / 2 : hi, k2 = (hi == k) ? k / 2 : k - hi;
+            int lv = std::min(pw[k1]->level, pw[k2]->level);
+            pw[k] = mul_ct(e, at_level(k1, lv), at_level(k2, lv), rlk);
+        }
+    } catch (...) {
+        for (auto* p : pw) aesfhe_ct_free(p);
+        for (auto& kv : memo) aesfhe_ct_free(kv.second);
+        throw;
+    }
+    for (auto& kv : memo) aesfhe_ct_free(kv.second);
+    for (int k = 1; k <= d; k++) outs[k - 1] = pw[k];
+    API_END
+}
+
+extern "C" int aesfhe_lincomb(aesfhe_engine* e, const aesfhe_ct* const* cts, int32_t n, const double* re, const double* im, aesfhe_ct** out) {
+    API_BEGIN
+    if (n < 1) throw_err(AESFHE_EARG, "empty linear combination");
+    int l = cts[0]->level, B = 1, np = 2;
+    for (int i = 0; i < n; i++) {
+        l = std::min(l, cts[i]->level);
+        B = std::max(B, cts[i]->B);
+        np = std::max(np, cts[i]->np);
+    }
+    for (int i = 0; i < n; i++)
+        if (cts[i]->B != B && cts[i]->B != 1) throw_err(AESFHE_EARG, "batch mismatch");
+    if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a linear combination");
+    double s = aesfhe_engine_mul_scale(e, l);
+    aesfhe_ct* acc = ct_new(e, B, np, l);
+    bool any = false;
+    for (int i = 0; i < n; i++) {
+        int64_t A = llround(re[i] * s), Bc = llround(im[i] * s);
+        if (cts[i]->is_zero || (A == 0 && Bc == 0)) continue;
+        Aligned a;
+        align_to(e, cts[i], l, a);
+        // the first contributing input writes every polynomial it has; a missing third
+        // polynomial (2-poly input into a 3-poly sum) is zero-filled first
+        if (!any && a.v.np < np) HIPC(hipMemsetAsync(acc->d, 0, acc->bytes, e->stream));
+        mul_const_into(e, a.v, A, Bc, acc, (any || a.v.np < np) ? 1 : 0);
+        any = true;
+    }
+    if (!any) {
+        aesfhe_ct_free(acc);
+        *out = ct_zero_new(e, B, np, l - 1);
+    } else {
+        *out = rescale_view(e, view_of(acc));
+        aesfhe_ct_free(acc);
+    }
+    API_END
+}
+
+extern "C" int aesfhe_dot(aesfhe_engine* e, const aesfhe_ct* const* a, const aesfhe_ct* const* b, int32_t n, const aesfhe_key* rlk, aesfhe_ct** out) {
+    API_BEGIN
+    if (n < 1) throw_err(AESFHE_EARG, "empty dot product");
+    if (!rlk || rlk->kind != 2) throw_err(AESFHE_EARG, "dot needs a relinearization key");
+    int l = a[0]->level, B = 1;
+    for (int i = 0; i < n; i++) {
+        if (a[i]->np != 2 || b[i]->np != 2) throw_err(AESFHE_EDEGREE, "dot inputs should have 2 polynomials");
+        l = std::min(l, std::min(a[i]->level, b[i]->level));
+        B = std::max(B, std::max(a[i]->B, b[i]->B));
+    }
+    for (int i = 0; i < n; i++)
+        if ((a[i]->B != B && a[i]->B != 1) || (b[i]->B != B && b[i]->B != 1)) throw_err(AESFHE_EARG, "batch mismatch");
+    if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a dot product");
+    aesfhe_ct* acc = ct_new(e, B, 3, l);
+    bool any = false;
+    for (int i = 0; i < n; i++) {
+        if (a[i]->is_zero || b[i]->is_zero) continue;
+        Aligned x, y;
+        align_to(e, a[i], l, x);
+        align_to(e, b[i], l, y);
+        hipLaunchKernelGGL(k_tensor, ew_grid(e, l + 1, B), dim3(256), 0, e->stream, opnd(x.v, B), opnd(y.v, B), out_of(acc), e->q, e->qinv, any ? 1 : 0, e->logN);
+        HIPC(hipGetLastError());
+        any = true;
+    }
+    if (!any) {
+        aesfhe_ct_free(acc);
+        *out = ct_zero_new(e, B, 2, l - 1);
+    } else {
+        aesfhe_ct* rl = relin_ct(e, acc, rlk);
+        aesfhe_ct_free(acc);
+        *out = rescale_view(e, view_of(rl));
+        aesfhe_ct_free(rl);
+    }
+    API_END
+}
+
+// -----------------------------------------------------------------------------------------------
+// raw NTT entry points
+extern "C" int aesfhe_ntt_host(aesfhe_engine* e, uint64_t* limbs, int32_t nlimb, const int32_t* pids, int32_t inv) {
+    API_BEGIN
+    const int N = e->N;
+    for (int i = 0; i < nlimb; i++)
+        if (pids[i] < 0 || pids[i] >= e->np) throw_err(AESFHE_EARG, "bad prime index");
+    Tmp buf(e, (size_t)N);
+    for (int i = 0; i < nlimb; i++) {
+        HIPC(hipMemcpyAsync(buf.p, limbs + (size_t)i * N, (size_t)N * 8, hipMemcpyHostToDevice, e->stream));
+        // one limb: a Q prime (nq = 1, qpid0 = pid) or a special prime (nq = 0, spid0 = pid)
+        const int pid = pids[i];
+        Span s = pid < e->Lp1 ? span_s(buf.p, N, 1, 1, pid, e->Lp1) : span_s(buf.p, N, 1, 0, 0, pid);
+        ntt(e, s, s, 1, inv != 0);
+        HIPC(hipMemcpyAsync(limbs + (size_t)i * N, buf.p, (size_t)N * 8, hipMemcpyDeviceToHost, e->stream));
+        HIPC(hipStreamSynchronize(e->stream));
+    }
+    API_END
+}
+
+extern "C" int aesfhe_bench_ntt(aesfhe_engine* e, int32_t nlimb, int32_t iters, double* fwd_ms, double* inv_ms) {
+    API_BEGIN
+    const int N = e->N;
+    const int nq = std::min(nlimb, e->Lp1);
+    const int groups = (nlimb + nq - 1) / nq;
+    Tmp buf(e, (size_t)groups * nq * N);
+    HIPC(hipMemsetAsync(buf.p, 0, (size_t)groups * nq * N * 8, e->stream));
+    Span s = span_s(buf.p, (long)nq * N, nq, nq, 0, e->Lp1);
+    hipEvent_t a, b, c;
+    HIPC(hipEventCreate(&a));
+    HIPC(hipEventCreate(&b));
+    HIPC(hipEventCreate(&c));
+    ntt(e, s, s, groups * nq, false);  // warm up
+    ntt(e, s, s, groups * nq, true);
+    HIPC(hipEventRecord(a, e->stream));
+    for (int i = 0; i < iters; i++) ntt(e, s, s, groups * nq, false);
+    HIPC(hipEventRecord(b, e->stream));
+    for (int i = 0; i < iters; i++) ntt(e, s, s, groups * nq, true);
+    HIPC(hipEventRecord(c, e->stream));
+    HIPC(hipEventSynchronize(c));
+    float t1 = 0, t2 = 0;
+    hipEventElapsedTime(&t1, a, b);
+    hipEventElapsedTime(&t2, b, c);
+    *fwd_ms = t1 / iters;
+    *inv_ms = t2 / iters;
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    hipEventDestroy(c);
+    API_END
+}

@@ -1,0 +1,359 @@
+// kernels_ops.h -- elementwise, base-conversion, key-switching, sampling and automorphism
+// kernels of the MI355X CKKS engine.  Specification: DESIGN.md section 3 (shared with the CPU
+// oracle, oracle/ckks_oracle.c, which these kernels must match residue for residue).
+#pragma once
+#include "kernels.h"
+
+namespace aesfhe {
+
+// fp64-quotient reduction of x < 2^52
+__device__ __forceinline__ u64 red_m(u64 x, u64 q, double qinv) {
+    u64 qh = (u64)((double)x * qinv);
+    return fix_m(x - qh * q, q);
+}
+
+// An operand for elementwise kernels: element (b, p, l, k) at ptr + b*bs + p*ps + l*N + k.
+// ptr == nullptr or p >= np reads as zero.
+struct Opnd {
+    const u64* ptr;
+    long bs;
+    long ps;
+    int np;
+};
+
+__device__ __forceinline__ u64 opnd_get(const Opnd& o, int b, int p, int l, int k, int logN) {
+    if (!o.ptr || p >= o.np) return 0;
+    return o.ptr[(long)b * o.bs + (long)p * o.ps + ((long)l << logN) + k];
+}
+
+struct Out {
+    u64* ptr;
+    long bs;
+    long ps;
+};
+
+// out = a +- b ; grid (N/256, nl, B*np)
+__global__ void k_addsub(Opnd a, Opnd b, Out o, int np, const u64* __restrict__ qs, int sub,
+                         int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z / np, p = blockIdx.z - bb * np;
+    const u64 q = qs[l];
+    u64 va = opnd_get(a, bb, p, l, k, logN), vb = opnd_get(b, bb, p, l, k, logN);
+    o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)l << logN) + k] = sub ? sub_m(va, vb, q) : add_m(va, vb, q);
+}
+
+// Constant factors for x * (A + B X^{N/2}): f[2*l] for k < N/2, f[2*l+1] for k >= N/2.
+// out (+)= in * f ; grid (N/256, nl, B*np)
+__global__ void k_mul_const(Opnd in, Out o, int np, const u64* __restrict__ f,
+                            const double* __restrict__ ff, const u64* __restrict__ qs, int acc,
+                            int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z / np, p = blockIdx.z - bb * np;
+    const u64 q = qs[l];
+    const int h = k >> (logN - 1);
+    u64 v = mul_w(opnd_get(in, bb, p, l, k, logN), f[2 * l + h], ff[2 * l + h], q);
+    u64* dst = o.ptr + (long)bb * o.bs + (long)p * o.ps + ((long)l << logN) + k;
+    *dst = acc ? add_m(*dst, v, q) : v;
+}
+
+// out = in * pt (pt limbs [l][N]) ; grid (N/256, nl, B*np)
+__global__ void k_mul_pt(Opnd in, const u64* __restrict__ pt, Out o, int np,
+                         const u64* __restrict__ qs, const double* __restrict__ qinv, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z / np, p = blockIdx.z - bb * np;
+    u64 v = mul_m(opnd_get(in, bb, p, l, k, logN), pt[((long)l << logN) + k], qs[l], qinv[l]);
+    o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)l << logN) + k] = v;
+}
+
+// out = in (+ pt on poly 0) ; grid (N/256, nl, B*np)
+__global__ void k_add_pt(Opnd in, const u64* __restrict__ pt, Out o, int np,
+                         const u64* __restrict__ qs, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z / np, p = blockIdx.z - bb * np;
+    u64 v = opnd_get(in, bb, p, l, k, logN);
+    if (p == 0) v = add_m(v, pt[((long)l << logN) + k], qs[l]);
+    o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)l << logN) + k] = v;
+}
+
+// (d0,d1,d2) (+)= (a0 b0, a0 b1 + a1 b0, a1 b1) ; grid (N/256, nl, B)
+__global__ void k_tensor(Opnd a, Opnd b, Out o, const u64* __restrict__ qs,
+                         const double* __restrict__ qinv, int acc, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z;
+    const u64 q = qs[l];
+    const double qi = qinv[l];
+    u64 a0 = opnd_get(a, bb, 0, l, k, logN), a1 = opnd_get(a, bb, 1, l, k, logN);
+    u64 b0 = opnd_get(b, bb, 0, l, k, logN), b1 = opnd_get(b, bb, 1, l, k, logN);
+    u64 d0 = mul_m(a0, b0, q, qi);
+    u64 d1 = add_m(mul_m(a0, b1, q, qi), mul_m(a1, b0, q, qi), q);
+    u64 d2 = mul_m(a1, b1, q, qi);
+    u64* base = o.ptr + (long)bb * o.bs + ((long)l << logN) + k;
+    if (acc) {
+        base[0] = add_m(base[0], d0, q);
+        base[o.ps] = add_m(base[o.ps], d1, q);
+        base[2 * o.ps] = add_m(base[2 * o.ps], d2, q);
+    } else {
+        base[0] = d0;
+        base[o.ps] = d1;
+        base[2 * o.ps] = d2;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// rescale
+// t[P][i][k] = centered(x[P][k]) mod q_i for i < l ; grid (N/256, l, P)
+__global__ void k_rescale_spread(const u64* __restrict__ x, u64* __restrict__ t, u64 ql,
+                                 const u64* __restrict__ qs, const double* __restrict__ qinv,
+                                 const u64* __restrict__ qlmod, int l, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y, P = blockIdx.z;
+    const u64 q = qs[i];
+    u64 v = x[((long)P << logN) + k];
+    u64 r = red_m(v, q, qinv[i]);
+    if (v > (ql >> 1)) r = sub_m(r, qlmod[i], q);
+    t[(((long)P * l + i) << logN) + k] = r;
+}
+
+// out[P][i] = (c[P][i] - t[P][i]) * q_l^{-1} ; grid (N/256, l, P) with P = b*np + p
+__global__ void k_rescale_finish(Opnd c, const u64* __restrict__ t, Out o, int np, int l,
+                                 const u64* __restrict__ qs, const u64* __restrict__ inv,
+                                 const double* __restrict__ invf, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y, P = blockIdx.z, bb = P / np, p = P - bb * np;
+    const u64 q = qs[i];
+    u64 cv = opnd_get(c, bb, p, i, k, logN);
+    u64 tv = t[(((long)P * l + i) << logN) + k];
+    o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)i << logN) + k] = mul_w(sub_m(cv, tv, q), inv[i], invf[i], q);
+}
+
+// ---------------------------------------------------------------------------------------------
+// hybrid key switching
+// ModUp fast base conversion of one digit: dc[b][i][k] (coef, i in [lo, lo+alpha)) to every
+// extended limb t in [0, ne) outside the digit.  ext[b][t][k].  grid (N/256, ceil(ne/8), B)
+// hatinv/hatinvf: [alpha]; hat/hatf: [alpha][np] (row stride np)
+__global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ ext, long exs,
+                        int lo, int alpha, int l, int ne, const u64* __restrict__ hatinv,
+                        const double* __restrict__ hatinvf, const u64* __restrict__ hat,
+                        const double* __restrict__ hatf, int np, const u64* __restrict__ qall,
+                        int Lp1, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int bb = blockIdx.z;
+    u64 y[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        if (i < alpha) {
+            const int pi = lo + i;
+            y[i] = mul_w(dc[(long)bb * dcs + ((long)pi << logN) + k], hatinv[i], hatinvf[i], qall[pi]);
+        }
+    }
+    const int t0 = blockIdx.y * 8;
+    for (int t = t0; t < t0 + 8 && t < ne; t++) {
+        if (t >= lo && t < lo + alpha) continue;
+        const int pid = t <= l ? t : Lp1 + (t - l - 1);
+        const u64 qt = qall[pid];
+        u64 s = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            if (i < alpha) s = add_m(s, mul_w(y[i], hat[i * np + pid], hatf[i * np + pid], qt), qt);
+        ext[(long)bb * exs + ((long)t << logN) + k] = s;
+    }
+}
+
+// acc[b][c][t] (+)= e[b][t] * key_c[pid(t)], e = d (own digit limbs, NTT) or ext (others)
+// grid (N/256, ne, 1); loops over the batch so each key word is read once
+__global__ void k_ks_inner(const u64* __restrict__ d, long dbs, const u64* __restrict__ ext,
+                           long exs, const u64* __restrict__ kb, const u64* __restrict__ ka,
+                           u64* __restrict__ acc, long abs_, long acs, int B, int lo, int hi,
+                           int l, const u64* __restrict__ qall, const double* __restrict__ qinvall,
+                           int Lp1, int first, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.y;
+    const int pid = t <= l ? t : Lp1 + (t - l - 1);
+    const u64 q = qall[pid];
+    const double qi = qinvall[pid];
+    const u64 vb = kb[((long)pid << logN) + k], va = ka[((long)pid << logN) + k];
+    const bool own = t >= lo && t < hi;
+    for (int bb = 0; bb < B; bb++) {
+        u64 e = own ? d[(long)bb * dbs + ((long)t << logN) + k] : ext[(long)bb * exs + ((long)t << logN) + k];
+        u64* a0 = acc + (long)bb * abs_ + ((long)t << logN) + k;
+        u64* a1 = a0 + acs;
+        u64 m0 = mul_m(e, vb, q, qi), m1 = mul_m(e, va, q, qi);
+        if (first) {
+            *a0 = m0;
+            *a1 = m1;
+        } else {
+            *a0 = add_m(*a0, m0, q);
+            *a1 = add_m(*a1, m1, q);
+        }
+    }
+}
+
+// ModDown base conversion P -> Q_l: acc special limbs already in coefficient form.
+// conv[b][c][i][k] = sum_k' (z_k' * Phatinv_k' mod p_k') * Phat[k'][i] mod q_i
+// grid (N/256, ceil((l+1)/8), B*2)
+__global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int l,
+                          u64* __restrict__ conv, long cbs, long ccs, int K,
+                          const u64* __restrict__ phatinv, const double* __restrict__ phatinvf,
+                          const u64* __restrict__ phat, const double* __restrict__ phatf,
+                          int Lp1, const u64* __restrict__ qall, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int bb = blockIdx.z >> 1, c = blockIdx.z & 1;
+    const u64* src = acc + (long)bb * abs_ + (long)c * acs;
+    u64 y[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+        if (j < K) y[j] = mul_w(src[((long)(l + 1 + j) << logN) + k], phatinv[j], phatinvf[j], qall[Lp1 + j]);
+    const int i0 = blockIdx.y * 8;
+    for (int i = i0; i < i0 + 8 && i <= l; i++) {
+        const u64 q = qall[i];
+        u64 s = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            if (j < K) s = add_m(s, mul_w(y[j], phat[j * Lp1 + i], phatf[j * Lp1 + i], q), q);
+        conv[(long)bb * cbs + (long)c * ccs + ((long)i << logN) + k] = s;
+    }
+}
+
+// out[b][c][i] = addend_c + (acc[b][c][i] - conv[b][c][i]) * P^{-1} ; grid (N/256, l+1, B*2)
+__global__ void k_moddown_finish(const u64* __restrict__ acc, long abs_, long acs,
+                                 const u64* __restrict__ conv, long cbs, long ccs, Opnd addend,
+                                 Out o, const u64* __restrict__ qs, const u64* __restrict__ pinv,
+                                 const double* __restrict__ pinvf, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y, bb = blockIdx.z >> 1, c = blockIdx.z & 1;
+    const u64 q = qs[i];
+    u64 a = acc[(long)bb * abs_ + (long)c * acs + ((long)i << logN) + k];
+    u64 v = conv[(long)bb * cbs + (long)c * ccs + ((long)i << logN) + k];
+    u64 r = mul_w(sub_m(a, v, q), pinv[i], pinvf[i], q);
+    r = add_m(r, opnd_get(addend, bb, c, i, k, logN), q);
+    o.ptr[(long)bb * o.bs + (long)c * o.ps + ((long)i << logN) + k] = r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// automorphism X -> X^g in the NTT domain: out[k] = in[brv((g e(k) mod 2N - 1)/2)],
+// e(k) = 2 brv(k) + 1.  grid (N/256, total limbs); src/dst Spans share the limb indexing.
+__global__ void k_galois(Span src, Span dst, u64 g, int logN, int Lp1) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    int pid;
+    const u64* in = span_ptr(src, blockIdx.y, logN, Lp1, pid);
+    u64* out = span_ptr(dst, blockIdx.y, logN, Lp1, pid);
+    const u64 M = 2ULL << logN;
+    const unsigned rk = __brev((unsigned)k) >> (32 - logN);
+    const u64 e = 2 * (u64)rk + 1;
+    const u64 t = (g * e) & (M - 1);
+    const unsigned idx = __brev((unsigned)((t - 1) >> 1)) >> (32 - logN);
+    out[k] = in[idx];
+}
+
+// ---------------------------------------------------------------------------------------------
+// sampling.  Uniform residues directly in the NTT domain, index pid*N + k.
+__global__ void k_sample_uniform(Span dst, u64 key, const u64* __restrict__ qall, int logN,
+                                 int Lp1) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    int pid;
+    u64* out = span_ptr(dst, blockIdx.y, logN, Lp1, pid);
+    out[k] = __umul64hi(rnd(key, ((u64)pid << logN) + k), qall[pid]);
+}
+
+// small coefficient polynomial (kind 0 ternary, 1 CBD-21) -> residues of every limb (coef form)
+__global__ void k_sample_small(Span dst, u64 key, int kind, const u64* __restrict__ qall,
+                               int logN, int Lp1) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    int pid;
+    u64* out = span_ptr(dst, blockIdx.y, logN, Lp1, pid);
+    const u64 r = rnd(key, (u64)k);
+    const i64 v = kind == 0 ? ternary(r) : cbd21(r);
+    const u64 q = qall[pid];
+    out[k] = v >= 0 ? (u64)v : q - (u64)(-v);
+}
+
+// signed 64-bit coefficients (device copy of host input) -> residues ; grid (N/256, nl, B)
+__global__ void k_coeffs_res(const i64* __restrict__ co, u64* __restrict__ out, int nl,
+                             const u64* __restrict__ qs, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z;
+    const i64 v = co[((long)bb << logN) + k];
+    const u64 q = qs[l];
+    u64 r;
+    if (v >= 0) r = (u64)v % q;
+    else r = q - 1 - ((u64)(-(v + 1)) % q);
+    out[(((long)bb * nl + l) << logN) + k] = r;
+}
+
+// key material: out = -a*s + e (+ pmod[pid] * sp) over the limbs of a Span-indexed set
+// a, e, sp, out share the Span limb indexing (pid-major tables with row stride N)
+__global__ void k_key_combine(const u64* __restrict__ a, const u64* __restrict__ s,
+                              const u64* __restrict__ e, const u64* __restrict__ sp,
+                              const u64* __restrict__ pmod, int lo, int hi, u64* __restrict__ out,
+                              const u64* __restrict__ qall, const double* __restrict__ qinvall,
+                              int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int pid = blockIdx.y;
+    const long off = ((long)pid << logN) + k;
+    const u64 q = qall[pid];
+    const double qi = qinvall[pid];
+    u64 v = add_m(sub_m(0, mul_m(a[off], s[off], q, qi), q), e[off], q);
+    if (sp && pid >= lo && pid < hi) v = add_m(v, mul_m(pmod[pid], sp[off], q, qi), q);
+    out[off] = v;
+}
+
+// public-key encryption: c0 = v pk0 + e0 + m, c1 = v pk1 + e1 (all NTT, limbs 0..l)
+// vem: [B][4][l+1][N] = (v, e0, e1, m) ; grid (N/256, l+1, B)
+__global__ void k_enc_pk(const u64* __restrict__ vem, const u64* __restrict__ pk0,
+                         const u64* __restrict__ pk1, u64* __restrict__ ct, int nl,
+                         const u64* __restrict__ qs, const double* __restrict__ qinv, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z;
+    const u64 q = qs[l];
+    const double qi = qinv[l];
+    const long lo = ((long)l << logN) + k;
+    const long step = (long)nl << logN;
+    const u64* base = vem + (long)bb * 4 * step + lo;
+    u64 v = base[0], e0 = base[step], e1 = base[2 * step], m = base[3 * step];
+    u64* c = ct + (long)bb * 2 * step + lo;
+    c[0] = add_m(add_m(mul_m(v, pk0[lo], q, qi), e0, q), m, q);
+    c[step] = add_m(mul_m(v, pk1[lo], q, qi), e1, q);
+}
+
+// secret-key encryption: c1 = a (uniform, NTT), c0 = -a s + e0 + m ; vem as above with v unused
+__global__ void k_enc_sk(const u64* __restrict__ vem, const u64* __restrict__ s,
+                         u64* __restrict__ ct, int nl, const u64* __restrict__ qs,
+                         const double* __restrict__ qinv, const u64* __restrict__ keys, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z;
+    const u64 q = qs[l];
+    const double qi = qinv[l];
+    const long lo = ((long)l << logN) + k;
+    const long step = (long)nl << logN;
+    const u64* base = vem + (long)bb * 4 * step + lo;
+    u64 e0 = base[step], m = base[3 * step];
+    u64 a = __umul64hi(rnd(keys[bb], ((u64)l << logN) + k), q);
+    u64* c = ct + (long)bb * 2 * step + lo;
+    c[step] = a;
+    c[0] = add_m(add_m(sub_m(0, mul_m(a, s[lo], q, qi), q), e0, q), m, q);
+}
+
+// limb-0 decryption combine: t[b][k] = c0 + c1 s (+ c2 s^2) ; grid (N/256, 1, B)
+__global__ void k_dec_limb0(const u64* __restrict__ ct, long bs, long ps, int np,
+                            const u64* __restrict__ s, u64* __restrict__ t, u64 q, double qinv,
+                            int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int bb = blockIdx.z;
+    const u64* c = ct + (long)bb * bs + k;
+    u64 sv = s[k];
+    u64 v = c[0];
+    if (np >= 2) v = add_m(v, mul_m(c[ps], sv, q, qinv), q);
+    if (np == 3) v = add_m(v, mul_m(c[2 * ps], mul_m(sv, sv, q, qinv), q, qinv), q);
+    t[((long)bb << logN) + k] = v;
+}
+
+// elementwise square (s^2 for the relinearisation key) over np pid-major limbs
+__global__ void k_square(const u64* __restrict__ s, u64* __restrict__ o,
+                         const u64* __restrict__ qall, const double* __restrict__ qinvall,
+                         int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const long off = ((long)blockIdx.y << logN) + k;
+    o[off] = mul_m(s[off], s[off], qall[blockIdx.y], qinvall[blockIdx.y]);
+}
+
+}  // namespace aesfhe

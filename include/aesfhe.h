@@ -1,0 +1,215 @@
+/*
+ * aesfhe.h -- C ABI of the MI355X-native RNS-CKKS engine behind the aes-fhe services.
+ *
+ * This is the drop-in boundary for the hot path named in BASELINE.json: the reference
+ * (songhayeong/aes-fhe) drives every homomorphic operation through the closed
+ * `desilofhe.Engine` object, wrapped by `EngineContext` (engine_context.py:9-85) and
+ * `EngineWrapper` (xor_service.py:36-129).  Each entry point below replaces one method
+ * of that object as the reference calls it (file:line of the call site in the reference):
+ *
+ *   aesfhe_engine_create        Engine(...) three signatures        engine_context.py:32-58
+ *   aesfhe_key_secret           engine.create_secret_key()          engine_context.py:62
+ *   aesfhe_key_public           engine.create_public_key(sk)        engine_context.py:63
+ *   aesfhe_key_relin            engine.create_relinearization_key   engine_context.py:64
+ *   aesfhe_key_galois           create_conjugation_key /            engine_context.py:65-66
+ *                               create_rotation_key /               engine_context.py:70
+ *                               create_fixed_rotation_key
+ *   aesfhe_encode/_decode       engine.encode(vec) (host codec)     xor_service.py:65-66,
+ *                                                                    sbox/sbox_service.py:85-88
+ *   aesfhe_encrypt/_decrypt     engine.encrypt(data, pk) / decrypt  engine_context.py:81-85
+ *   aesfhe_add / _sub / _add_pt engine.add(a, b)                    xor_service.py:75-76
+ *   aesfhe_mul                  engine.multiply(ct, ct, rlk)        xor_service.py:68-71
+ *   aesfhe_mul_pt               engine.multiply(ct, pt)             xor_service.py:73,285
+ *   aesfhe_mul_const            engine.multiply(ct, scalar)         xor_service.py:282
+ *   aesfhe_tensor/_relinearize  engine.relinearize(ct, rlk)         xor_service.py:107-118
+ *   aesfhe_galois               engine.rotate(ct, key, k) /         xor_service.py:100-105
+ *                               engine.conjugate(ct, cjk)           xor_service.py:88-89
+ *   aesfhe_power_basis          engine.make_power_basis(ct, d, rlk) xor_service.py:85-86,
+ *                                                                    sbox/sbox_service.py:93
+ *   aesfhe_lincomb / aesfhe_dot  (no reference counterpart: fused BSGS building blocks used
+ *                               by the optimised AES round; the reference's per-term loops
+ *                               xor_service.py:283-285 / sbox_service.py:124-136 are the
+ *                               unfused equivalent)
+ *
+ * Conventions
+ *   - Plain C types only: pointers, sizes, int64 coefficients, doubles.  No torch types.
+ *   - Every function returns 0 on success or a negative AESFHE_E* code; the message of the
+ *     last failure on the calling thread is returned by aesfhe_last_error().  The Python
+ *     facade maps codes to RuntimeError with desilofhe-compatible substrings (e.g.
+ *     "should have 3 polynomials", matched at xor_service.py:116).
+ *   - Handles are immutable values (every op returns a new handle, as desilofhe objects are);
+ *     the caller frees them with the matching *_free.
+ *   - A ciphertext handle holds a BATCH of B ciphertexts at one level; binary operations
+ *     accept B_a == B_b or a broadcast operand with B == 1.
+ *   - Residues are kept in the NTT (evaluation) domain, canonical in [0, q).
+ *
+ * Two implementations export exactly this ABI:
+ *   libaesfhe.so        (aes-fhe_amd/csrc, HIP for gfx950)      -- the product
+ *   oracle/_build/liboracle_ckks.so (oracle/ckks_oracle.c, CPU) -- test-only checker
+ */
+#ifndef AESFHE_H
+#define AESFHE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AESFHE_OK 0
+#define AESFHE_EARG (-1)      /* bad argument / shape / level mismatch */
+#define AESFHE_ENOMEM (-2)    /* host or device allocation failed */
+#define AESFHE_EDEVICE (-3)   /* HIP runtime error */
+#define AESFHE_EDEGREE (-4)   /* ciphertext has the wrong number of polynomials */
+#define AESFHE_ELEVEL (-5)    /* out of levels */
+#define AESFHE_EUNSUPPORTED (-6)
+
+typedef struct aesfhe_engine aesfhe_engine;
+typedef struct aesfhe_ct aesfhe_ct;
+typedef struct aesfhe_pt aesfhe_pt;
+typedef struct aesfhe_key aesfhe_key;
+
+typedef struct aesfhe_params {
+    int32_t log_n;          /* log2 of the ring degree N (slots = N/2) */
+    int32_t max_level;      /* L: the ciphertext modulus chain has L+1 primes q_0..q_L */
+    int32_t special_primes; /* K = alpha: special primes p_0..p_{K-1}; dnum = ceil((L+1)/K) */
+    int32_t scale_bits;     /* log2 of the top-level scale Delta_L */
+    int32_t base_bits;      /* bit size of q_0 */
+    int32_t special_bits;   /* bit size of the special primes */
+    int32_t device;         /* HIP device ordinal (ignored by the CPU oracle) */
+    int32_t threads;        /* host threads (oracle only; 0 = default) */
+    uint64_t seed;          /* engine seed: all key / encryption randomness derives from it */
+    const uint64_t *primes; /* optional explicit chain q_0..q_L,p_0..p_{K-1} (NULL = generate) */
+} aesfhe_params;
+
+/* ---- diagnostics ---------------------------------------------------------------------- */
+const char *aesfhe_last_error(void);
+const char *aesfhe_backend_name(void);
+
+/* ---- engine ----------------------------------------------------------------------------- */
+int aesfhe_engine_create(const aesfhe_params *params, aesfhe_engine **out);
+void aesfhe_engine_destroy(aesfhe_engine *eng);
+/* dims[0]=log_n dims[1]=max_level dims[2]=special_primes dims[3]=dnum */
+int aesfhe_engine_dims(const aesfhe_engine *eng, int32_t dims[4]);
+/* primes: L+1+K words; scales: L+1 doubles (canonical scale Delta_l of every level) */
+int aesfhe_engine_primes(const aesfhe_engine *eng, uint64_t *primes_out);
+int aesfhe_engine_scales(const aesfhe_engine *eng, double *scales_out);
+/* Scale at which a plaintext/constant multiplied into a level-`level` ciphertext must be
+ * encoded so that the rescaled product lands exactly on the canonical Delta_{level-1}. */
+double aesfhe_engine_mul_scale(const aesfhe_engine *eng, int32_t level);
+int aesfhe_engine_sync(aesfhe_engine *eng);
+/* Per-kernel-family timing (HIP events on the engine stream; CPU wall time in the oracle).
+ * family: "ntt" | "keyswitch" | "elementwise" | "all".  enable=1 starts recording, 0 stops. */
+int aesfhe_engine_profile(aesfhe_engine *eng, int32_t enable);
+int aesfhe_engine_profile_read(aesfhe_engine *eng, const char *family, int64_t *launches,
+                               double *total_ms, double *bytes);
+/* device bytes currently held by the engine (keys + pool); 0 in the oracle */
+int64_t aesfhe_engine_device_bytes(const aesfhe_engine *eng);
+
+/* ---- host codec (no engine / device needed) --------------------------------------------- */
+/* Canonical-embedding encode: n_slots <= N/2 complex values (zero padded) -> N integer
+ * coefficients round(scale * m_i). */
+int aesfhe_encode(int32_t log_n, const double *re, const double *im, int64_t n_slots,
+                  double scale, int64_t *coeffs_out);
+/* Decode N centered integer coefficients (already divided by nothing) at `scale` -> N/2 slots */
+int aesfhe_decode(int32_t log_n, const int64_t *coeffs, double scale, double *re_out,
+                  double *im_out);
+
+/* ---- keys ------------------------------------------------------------------------------- */
+int aesfhe_key_secret(aesfhe_engine *eng, uint64_t seed, aesfhe_key **out);
+int aesfhe_key_public(aesfhe_engine *eng, const aesfhe_key *sk, aesfhe_key **out);
+int aesfhe_key_relin(aesfhe_engine *eng, const aesfhe_key *sk, aesfhe_key **out);
+/* galois_elt odd in [1, 2N): conjugation = 2N-1, rotation by k slots (np.roll(v, k)) =
+ * 5^(-k mod N/2) mod 2N.  Use aesfhe_galois_elt() to compute it. */
+int aesfhe_key_galois(aesfhe_engine *eng, const aesfhe_key *sk, uint64_t galois_elt,
+                      aesfhe_key **out);
+uint64_t aesfhe_galois_elt(int32_t log_n, int64_t rotation, int32_t conjugate);
+/* kind: 0 secret 1 public 2 relin 3 galois; galois_elt for kind 3 */
+int aesfhe_key_info(const aesfhe_key *key, int32_t *kind, uint64_t *galois_elt);
+void aesfhe_key_free(aesfhe_key *key);
+
+/* ---- ciphertexts ------------------------------------------------------------------------ */
+/* coeffs: batch*N integer coefficients (encoded at the canonical scale of `level`);
+ * key: public key (or secret key: symmetric encryption).  nonce selects the randomness. */
+int aesfhe_encrypt(aesfhe_engine *eng, const aesfhe_key *key, const int64_t *coeffs,
+                   int32_t batch, int32_t level, uint64_t nonce, aesfhe_ct **out);
+/* Decrypt to batch*N centered coefficients modulo q_0. */
+int aesfhe_decrypt(aesfhe_engine *eng, const aesfhe_key *sk, const aesfhe_ct *ct,
+                   int64_t *coeffs_out);
+/* info[0]=batch info[1]=npoly info[2]=level info[3]=is_zero */
+int aesfhe_ct_info(const aesfhe_ct *ct, int32_t info[4]);
+/* NTT-domain residues, layout [batch][poly][limb 0..level][N] */
+int aesfhe_ct_export(aesfhe_engine *eng, const aesfhe_ct *ct, uint64_t *out);
+int aesfhe_ct_import(aesfhe_engine *eng, const uint64_t *in, int32_t batch, int32_t npoly,
+                     int32_t level, aesfhe_ct **out);
+int aesfhe_ct_copy(aesfhe_engine *eng, const aesfhe_ct *ct, aesfhe_ct **out);
+/* batch slicing / concatenation (all parts at one level and npoly) */
+int aesfhe_ct_slice(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t start, int32_t count,
+                    aesfhe_ct **out);
+int aesfhe_ct_concat(aesfhe_engine *eng, const aesfhe_ct *const *parts, int32_t n,
+                     aesfhe_ct **out);
+/* an all-zero ciphertext (flagged is_zero) */
+int aesfhe_ct_zero(aesfhe_engine *eng, int32_t batch, int32_t level, aesfhe_ct **out);
+void aesfhe_ct_free(aesfhe_ct *ct);
+
+/* plaintext from N integer coefficients, materialised at `level` (NTT residues) */
+int aesfhe_pt_create(aesfhe_engine *eng, const int64_t *coeffs, int32_t level,
+                     aesfhe_pt **out);
+void aesfhe_pt_free(aesfhe_pt *pt);
+
+/* ---- arithmetic ------------------------------------------------------------------------- */
+/* Operands at different levels are aligned by an exact-scale level-down of the higher one. */
+int aesfhe_add(aesfhe_engine *eng, const aesfhe_ct *a, const aesfhe_ct *b, aesfhe_ct **out);
+int aesfhe_sub(aesfhe_engine *eng, const aesfhe_ct *a, const aesfhe_ct *b, aesfhe_ct **out);
+int aesfhe_negate(aesfhe_engine *eng, const aesfhe_ct *a, aesfhe_ct **out);
+/* pt must be encoded at the canonical scale of ct's level and created at that level */
+int aesfhe_add_pt(aesfhe_engine *eng, const aesfhe_ct *ct, const aesfhe_pt *pt,
+                  aesfhe_ct **out);
+/* pt encoded at aesfhe_engine_mul_scale(level); output rescaled to level-1 */
+int aesfhe_mul_pt(aesfhe_engine *eng, const aesfhe_ct *ct, const aesfhe_pt *pt,
+                  aesfhe_ct **out);
+/* ct * (re + i*im), output at level-1 (exact canonical scale) */
+int aesfhe_mul_const(aesfhe_engine *eng, const aesfhe_ct *ct, double re, double im,
+                     aesfhe_ct **out);
+/* ct (*) ct -> 3-polynomial ciphertext, same level, scale Delta^2 (no relin, no rescale) */
+int aesfhe_tensor(aesfhe_engine *eng, const aesfhe_ct *a, const aesfhe_ct *b,
+                  aesfhe_ct **out);
+/* 3 -> 2 polynomials (fails with AESFHE_EDEGREE "should have 3 polynomials" otherwise) */
+int aesfhe_relinearize(aesfhe_engine *eng, const aesfhe_ct *ct, const aesfhe_key *rlk,
+                       aesfhe_ct **out);
+int aesfhe_rescale(aesfhe_engine *eng, const aesfhe_ct *ct, aesfhe_ct **out);
+/* tensor + relinearize + rescale */
+int aesfhe_mul(aesfhe_engine *eng, const aesfhe_ct *a, const aesfhe_ct *b,
+               const aesfhe_key *rlk, aesfhe_ct **out);
+/* exact-scale level reduction */
+int aesfhe_level_down(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t level,
+                      aesfhe_ct **out);
+/* automorphism X -> X^g followed by key switching back to s (rotation / conjugation) */
+int aesfhe_galois(aesfhe_engine *eng, const aesfhe_ct *ct, const aesfhe_key *gk,
+                  aesfhe_ct **out);
+/* outs[0..d-1] = ct^1 .. ct^d, ct^k at level(ct) - ceil(log2 k) */
+int aesfhe_power_basis(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t d,
+                       const aesfhe_key *rlk, aesfhe_ct **outs);
+/* sum_i (re_i + i*im_i) * cts[i], aligned to the lowest input level, output at that - 1 */
+int aesfhe_lincomb(aesfhe_engine *eng, const aesfhe_ct *const *cts, int32_t n,
+                   const double *re, const double *im, aesfhe_ct **out);
+/* sum_i a_i (*) b_i, one relinearisation + one rescale for the whole sum */
+int aesfhe_dot(aesfhe_engine *eng, const aesfhe_ct *const *a, const aesfhe_ct *const *b,
+               int32_t n, const aesfhe_key *rlk, aesfhe_ct **out);
+
+/* ---- raw kernels (known-answer tests and roofline measurement) ------------------------- */
+/* In-place forward (inverse=0) / inverse NTT of nlimb host limbs; limb i uses prime pids[i]
+ * (index into the q_0..q_L,p_0.. chain). */
+int aesfhe_ntt_host(aesfhe_engine *eng, uint64_t *limbs, int32_t nlimb, const int32_t *pids,
+                    int32_t inverse);
+/* Time `iters` forward+inverse NTT launches over `nlimb` device-resident limbs (primes
+ * cycled over the Q chain).  Reports the average per-launch duration of each direction
+ * measured with HIP events on the engine stream. */
+int aesfhe_bench_ntt(aesfhe_engine *eng, int32_t nlimb, int32_t iters, double *fwd_ms,
+                     double *inv_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AESFHE_H */

@@ -1,0 +1,133 @@
+"""GPU parity: the HIP engine (libaesfhe.so) against the CPU oracle, residue for residue.
+
+Both implement include/aesfhe.h; the oracle restates the CKKS algorithm desilofhe performs for
+the reference (see oracle/ckks_oracle.c header).  Every comparison here is bit-exact on the
+NTT-domain residues (integer work), after identical seeded key generation and encryption.
+"""
+import numpy as np
+import pytest
+
+from aes_xor_fhe.fhe import Engine
+
+pytestmark = pytest.mark.gpu
+
+SMALL = dict(log_n=12, max_level=6, special_primes=2, seed=1234)
+
+
+def _pair(product_lib, oracle_lib, **kw):
+    g = Engine(_lib=product_lib, **kw)
+    o = Engine(_lib=oracle_lib, **kw)
+    assert g.primes == o.primes
+    assert g.scales == o.scales
+    return g, o
+
+
+def _keys(eng):
+    sk = eng.create_secret_key(7)
+    return dict(sk=sk, pk=eng.create_public_key(sk), rlk=eng.create_relinearization_key(sk),
+                cjk=eng.create_conjugation_key(sk), rot=eng.create_rotation_key(sk))
+
+
+def _same(g, o, cg, co):
+    assert (cg.level, cg.batch, cg.npoly) == (co.level, co.batch, co.npoly)
+    a, b = g.export_residues(cg), o.export_residues(co)
+    if not np.array_equal(a, b):
+        bad = np.argwhere(a != b)
+        raise AssertionError(f"{len(bad)} residues differ; first at {bad[0].tolist()}")
+
+
+@pytest.mark.parametrize("log_n", [10, 12, 14, 16])
+def test_ntt_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
+    kw = dict(log_n=log_n, max_level=4, special_primes=2, seed=1)
+    g, o = _pair(product_lib, oracle_lib, **kw)
+    import ctypes as C
+    n = 1 << log_n
+    npr = len(g.primes)
+    rng = np.random.default_rng(log_n)
+    limbs = np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in g.primes])
+    pids = np.arange(npr, dtype=np.int32)
+    for inverse in (0, 1):
+        out = []
+        for eng in (g, o):
+            buf = limbs.copy()
+            eng._check(eng._lib.ntt_host(eng._h, buf.ctypes.data_as(C.POINTER(C.c_uint64)), npr,
+                                         pids.ctypes.data_as(C.POINTER(C.c_int32)), inverse))
+            out.append(buf)
+        np.testing.assert_array_equal(out[0], out[1])
+
+
+def test_keygen_encrypt_bit_exact(product_lib, oracle_lib, gpu_available):
+    g, o = _pair(product_lib, oracle_lib, **SMALL)
+    kg, ko = _keys(g), _keys(o)
+    rng = np.random.default_rng(0)
+    v = np.exp(-2j * np.pi * rng.integers(0, 16, g.slot_count) / 16)
+    cg, co = g.encrypt(v, kg["pk"]), o.encrypt(v, ko["pk"])
+    _same(g, o, cg, co)
+    np.testing.assert_allclose(g.decrypt(cg, kg["sk"]), v, atol=1e-6)
+    # symmetric encryption and batches
+    vb = np.stack([v, np.roll(v, 3)])
+    _same(g, o, g.encrypt(vb, kg["sk"]), o.encrypt(vb, ko["sk"]))
+
+
+def test_ops_bit_exact(product_lib, oracle_lib, gpu_available):
+    g, o = _pair(product_lib, oracle_lib, **SMALL)
+    kg, ko = _keys(g), _keys(o)
+    rng = np.random.default_rng(1)
+    z = np.exp(-2j * np.pi * rng.integers(0, 16, g.slot_count) / 16)
+    w = np.exp(-2j * np.pi * rng.integers(0, 16, g.slot_count) / 16)
+    cg, co = g.encrypt(z, kg["pk"]), o.encrypt(z, ko["pk"])
+    dg, do = g.encrypt(w, kg["pk"]), o.encrypt(w, ko["pk"])
+    _same(g, o, g.multiply(cg, dg, kg["rlk"]), o.multiply(co, do, ko["rlk"]))
+    _same(g, o, g.add(cg, dg), o.add(co, do))
+    _same(g, o, g.subtract(cg, dg), o.subtract(co, do))
+    _same(g, o, g.multiply(cg, 0.25 - 0.5j), o.multiply(co, 0.25 - 0.5j))
+    mask = (np.arange(g.slot_count) % 4 == 1).astype(float)
+    _same(g, o, g.multiply(cg, g.encode(mask)), o.multiply(co, o.encode(mask)))
+    _same(g, o, g.add(cg, g.encode(mask)), o.add(co, o.encode(mask)))
+    _same(g, o, g.conjugate(cg, kg["cjk"]), o.conjugate(co, ko["cjk"]))
+    for k in (1, -4, 5, 1000):
+        _same(g, o, g.rotate(cg, kg["rot"], k), o.rotate(co, ko["rot"], k))
+    _same(g, o, g.level_down(cg, 3), o.level_down(co, 3))
+    pg = g.make_power_basis(cg, 8, kg["rlk"])
+    po = o.make_power_basis(co, 8, ko["rlk"])
+    for a, b in zip(pg, po):
+        _same(g, o, a, b)
+    coeffs = [0.5, 0.25j, -1.0, 2.0 + 1j]
+    _same(g, o, g.lincomb(pg[:4], coeffs), o.lincomb(po[:4], coeffs))
+    _same(g, o, g.dot(pg[:3], pg[1:4], kg["rlk"]), o.dot(po[:3], po[1:4], ko["rlk"]))
+    # mixed levels: add aligns by exact-scale level-down
+    _same(g, o, g.add(pg[7], cg), o.add(po[7], co))
+    # 3-polynomial path and the reference's relinearize error string
+    t3g, t3o = g.multiply(cg, dg), o.multiply(co, do)
+    _same(g, o, t3g, t3o)
+    _same(g, o, g.relinearize(t3g, kg["rlk"]), o.relinearize(t3o, ko["rlk"]))
+    with pytest.raises(RuntimeError, match="should have 3 polynomials"):
+        g.relinearize(cg, kg["rlk"])
+
+
+def test_batched_ops_bit_exact(product_lib, oracle_lib, gpu_available):
+    g, o = _pair(product_lib, oracle_lib, **SMALL)
+    kg, ko = _keys(g), _keys(o)
+    rng = np.random.default_rng(2)
+    zb = np.exp(-2j * np.pi * rng.integers(0, 16, (3, g.slot_count)) / 16)
+    cg, co = g.encrypt(zb, kg["pk"]), o.encrypt(zb, ko["pk"])
+    kgc, koc = g.encrypt(zb[0], kg["pk"]), o.encrypt(zb[0], ko["pk"])  # broadcast operand
+    _same(g, o, g.multiply(cg, kgc, kg["rlk"]), o.multiply(co, koc, ko["rlk"]))
+    _same(g, o, g.rotate(cg, kg["rot"], -3), o.rotate(co, ko["rot"], -3))
+    _same(g, o, g.conjugate(cg, kg["cjk"]), o.conjugate(co, ko["cjk"]))
+    dec = g.decrypt(g.multiply(cg, kgc, kg["rlk"]), kg["sk"])
+    np.testing.assert_allclose(dec, zb * zb[0], atol=1e-5)
+
+
+def test_full_params_mul_bit_exact(product_lib, oracle_lib, gpu_available):
+    """BASELINE.json's parameter set: N = 2^16, L = 30 (one ct x ct multiply + rotation)."""
+    kw = dict(log_n=16, max_level=30, special_primes=8, seed=99)
+    g, o = _pair(product_lib, oracle_lib, **kw)
+    kg, ko = _keys(g), _keys(o)
+    rng = np.random.default_rng(3)
+    z = np.exp(-2j * np.pi * rng.integers(0, 256, g.slot_count) / 256)
+    cg, co = g.encrypt(z, kg["pk"]), o.encrypt(z, ko["pk"])
+    mg, mo = g.multiply(cg, cg, kg["rlk"]), o.multiply(co, co, ko["rlk"])
+    _same(g, o, mg, mo)
+    np.testing.assert_allclose(g.decrypt(mg, kg["sk"]), z * z, atol=1e-5)
+    _same(g, o, g.rotate(mg, kg["rot"], -2048), o.rotate(mo, ko["rot"], -2048))
