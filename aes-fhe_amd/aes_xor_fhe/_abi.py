@@ -83,6 +83,7 @@ SIGNATURES = [
     ("aesfhe_sub", C.c_int, [c_eng_p, c_ct_p, c_ct_p, _P(c_ct_p)]),
     ("aesfhe_negate", C.c_int, [c_eng_p, c_ct_p, _P(c_ct_p)]),
     ("aesfhe_add_pt", C.c_int, [c_eng_p, c_ct_p, c_pt_p, _P(c_ct_p)]),
+    ("aesfhe_add_const", C.c_int, [c_eng_p, c_ct_p, C.c_double, C.c_double, _P(c_ct_p)]),
     ("aesfhe_mul_pt", C.c_int, [c_eng_p, c_ct_p, c_pt_p, _P(c_ct_p)]),
     ("aesfhe_mul_const", C.c_int, [c_eng_p, c_ct_p, C.c_double, C.c_double, _P(c_ct_p)]),
     ("aesfhe_tensor", C.c_int, [c_eng_p, c_ct_p, c_ct_p, _P(c_ct_p)]),

@@ -357,6 +357,9 @@ class Engine:
         if not isinstance(a, Ciphertext):
             a, b = b, a
         pt = self._as_plain(b)
+        if pt.is_const:
+            c = pt.const
+            return self._call_ct(self._lib.add_const, a._h, c.real, c.imag)
         return self._call_ct(self._lib.add_pt, a._h, pt.device(a.level, self.scales[a.level]))
 
     def subtract(self, a, b) -> Ciphertext:
@@ -444,6 +447,11 @@ class Engine:
         aa = (c_ct_p * n)(*[c._h for c in a])
         bb = (c_ct_p * n)(*[c._h for c in b])
         return self._call_ct(self._lib.dot, aa, bb, n, relinearization_key._h)
+
+    def align(self, cts: Sequence[Ciphertext], level: int | None = None) -> list:
+        """Exact-scale level-down of every ciphertext to `level` (default: the lowest)."""
+        level = min(c.level for c in cts) if level is None else level
+        return [c if c.level == level else self.level_down(c, level) for c in cts]
 
     def zeros(self, batch: int = 1, level: int | None = None) -> Ciphertext:
         level = self.max_level if level is None else level

@@ -1,0 +1,291 @@
+"""4-bit homomorphic XOR over Zeta-encoded nibbles, plus the engine adapter the services share.
+
+Restates the reference's xor_service.py on the MI355X engine:
+  * ``XORConfig`` / ``EngineWrapper`` (xor_service.py:16-129): config holder and the adapter
+    that routes ct x ct multiplies through the relinearisation key, falls back from
+    ``add_plain`` to encode+add, swallows the "should have 3 polynomials" relinearise error
+    and forwards rotate / conjugate / bootstrap;
+  * ``ZetaEncoder`` (:132-145), ``CoefficientCache`` (:148-196);
+  * ``XORService.xor_cipher`` (:271-286): P(x, y) = sum_{i,j odd} c_ij x^i y^j evaluated with
+    the power basis x^1..x^8 plus conjugates for x^9..x^15 (:245-254), one ct x ct and one
+    ct x pt per term -- the reference's op order, kept as is;
+  * ``xor_cipher_bsgs``: the same polynomial as sum_i x^i * (sum_j c_ij y^j) with one fused
+    linear combination per i and a single relinearisation for the whole sum (engine.dot);
+  * ``recombine_nibbles`` / ``extract_nibbles`` / ``add_round_key``: repaired versions of the
+    reference's (:256-269, :434-547), which return wrong values or crash.
+"""
+from __future__ import annotations
+
+import json
+from functools import lru_cache
+from pathlib import Path
+from typing import Any, Dict, Tuple
+
+import numpy as np
+
+from . import coeffs_gen
+from .engine_context import EngineContext
+from .fhe import Ciphertext, Engine
+
+COEFF_DIR = Path(__file__).resolve().parent / "coeffs"
+
+
+class XORConfig:
+    """Engine configuration (xor_service.py:16-33).  Extra keyword arguments (the reference's
+    tests pass e.g. ``nibble_hi_path``) are kept as attributes; ``engine_kwargs`` reaches the
+    Engine constructor (explicit parameters, seed, or a test ABI implementation)."""
+
+    def __init__(self, coeffs_path: Path = COEFF_DIR / "xor_mono_coeffs.json",
+                 max_level: int = 33, mode: str = "parallel", thread_count: int = 8,
+                 device_id: int = 0, engine_kwargs: dict | None = None, **extra):
+        self.coeffs_path = Path(coeffs_path)
+        self.max_level = max_level
+        self.mode = mode
+        self.thread_count = thread_count
+        self.device_id = device_id
+        self.engine_kwargs = dict(engine_kwargs or {})
+        for k, v in extra.items():
+            setattr(self, k, v)
+
+
+class EngineWrapper:
+    """Adapter over EngineContext (xor_service.py:36-129).  As in the reference the context is
+    built with signature 1, so ``config.max_level`` does not select the chain (engine_context
+    signature 1 has no max_level); pass ``engine_kwargs`` for explicit parameters."""
+
+    def __init__(self, config: XORConfig, ctx: EngineContext | None = None):
+        if ctx is None:
+            ctx = EngineContext(signature=1, use_bootstrap=True, max_level=config.max_level,
+                                mode=config.mode, thread_count=config.thread_count,
+                                device_id=config.device_id, **config.engine_kwargs)
+        self.ctx = ctx
+        self.engine: Engine = ctx.engine
+        self.public_key = ctx.public_key
+        self.secret_key = ctx.secret_key
+        self.relin_key = ctx.relinearization_key
+        self.conj_key = ctx.conjugation_key
+        self.rot_key = ctx.rotation_key
+        self.boot_key = ctx.bootstrap_key
+
+    def encrypt(self, data: np.ndarray):
+        return self.engine.encrypt(data, self.public_key)
+
+    def decrypt(self, ct) -> np.ndarray:
+        return self.engine.decrypt(ct, self.secret_key)
+
+    def encode(self, vec: np.ndarray):
+        return self.engine.encode(vec)
+
+    def multiply(self, a, b, relin_key=None):
+        if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
+            return self.engine.multiply(a, b, relin_key or self.relin_key)
+        return self.engine.multiply(a, b)
+
+    def add(self, a, b):
+        return self.engine.add(a, b)
+
+    def add_plain(self, ct, val):
+        try:
+            return self.engine.add_plain(ct, val)
+        except AttributeError:
+            pt = self.engine.encode(np.full(self.engine.slot_count, val, dtype=np.complex128))
+            return self.engine.add(ct, pt)
+
+    def make_power_basis(self, ct, degree: int):
+        return self.engine.make_power_basis(ct, degree, self.relin_key)
+
+    def conjugate(self, ct):
+        return self.engine.conjugate(ct, self.conj_key)
+
+    def multiply_plain(self, ct, val):
+        if np.isscalar(val):
+            return self.engine.multiply(ct, val)
+        return self.engine.multiply(ct, self.engine.encode(np.array(val, dtype=np.complex128)))
+
+    def rotate(self, ct, steps: int):
+        return self.engine.rotate(ct, self.rot_key, steps)
+
+    def relinearize(self, ct, relin_key=None):
+        try:
+            return self.engine.relinearize(ct, relin_key or self.relin_key)
+        except RuntimeError as e:
+            if "should have 3 polynomials" in str(e):
+                return ct
+            raise
+
+    def bootstrap(self, ct):
+        return self.engine.bootstrap(ct, self.relin_key, self.conj_key, self.boot_key)
+
+
+class ZetaEncoder:
+    """k <-> exp(-2 pi i k / m) (xor_service.py:132-145).  Inputs are widened to int64 before
+    the modulus is applied, which is what the reference computes under numpy 1.x (under
+    numpy 2 its uint8 % 256 raises)."""
+
+    @staticmethod
+    def to_zeta(arr: np.ndarray, modulus: int = 16) -> np.ndarray:
+        a = np.asarray(arr).astype(np.int64)
+        return np.exp(-2j * np.pi * (a % modulus) / modulus)
+
+    @staticmethod
+    def from_zeta(z_arr: np.ndarray, modulus: int = 16) -> np.ndarray:
+        k = (-np.angle(z_arr) * modulus) / (2 * np.pi)
+        return np.mod(np.rint(k), modulus).astype(np.uint8)
+
+
+class CoefficientCache:
+    """LUT coefficients from JSON plus their plaintext encodings per slot count
+    (xor_service.py:148-196).  Keys are ``i`` (1-D files) or ``(i, j)`` (2-D files)."""
+
+    def __init__(self, path: Path):
+        self.path = Path(path)
+        self._plain_cache: Dict[int, Dict[Any, object]] = {}
+
+    @lru_cache(maxsize=1)
+    def load_coeffs(self) -> Dict[Any, complex]:
+        data = json.loads(self.path.read_text(encoding="utf-8"))
+        out: Dict[Any, complex] = {}
+        for entry in data["entries"]:
+            if len(entry) == 3:
+                out[int(entry[0])] = entry[1] + 1j * entry[2]
+            elif len(entry) == 4:
+                out[(int(entry[0]), int(entry[1]))] = entry[2] + 1j * entry[3]
+            else:
+                raise ValueError(f"Unrecognized entry format: {entry}")
+        return out
+
+    def get_plaintext_coeffs(self, engine_wrapper: EngineWrapper) -> Dict[Any, object]:
+        sc = engine_wrapper.engine.slot_count
+        if sc not in self._plain_cache:
+            self._plain_cache[sc] = {
+                key: engine_wrapper.encode(np.full(sc, val, dtype=np.complex128))
+                for key, val in self.load_coeffs().items()}
+        return self._plain_cache[sc]
+
+
+class XORService:
+    """Homomorphic 4-bit XOR (xor_service.py:227-328)."""
+
+    def __init__(self, engine_wrapper: EngineWrapper, coeff_cache: CoefficientCache | None = None,
+                 **unused):
+        self.eng_wrap = engine_wrapper
+        self.coeff_cache = coeff_cache or CoefficientCache(COEFF_DIR / "xor_mono_coeffs.json")
+        self._lut16_to_256 = None
+
+    @property
+    def eng(self) -> EngineWrapper:
+        return self.eng_wrap
+
+    # -- reference-faithful path ---------------------------------------------------------------
+    def _build_power_basis(self, ct) -> Dict[int, object]:
+        """t^0..t^8 by products, t^9..t^15 as conjugates of t^7..t^1 (xor_service.py:245-254)."""
+        eng = self.eng_wrap
+        pos = eng.make_power_basis(ct, 8)
+        basis = {0: eng.add_plain(ct, 1.0)}
+        for i, c in enumerate(pos, 1):
+            basis[i] = c
+        for k in range(1, 8):
+            basis[16 - k] = eng.conjugate(pos[k - 1])
+        return basis
+
+    def xor_cipher(self, enc_a, enc_b):
+        """sum over the 64 odd x odd terms of the 16x16 XOR LUT (xor_service.py:271-286)."""
+        eng = self.eng_wrap
+        if enc_a.level < 8:
+            enc_a = eng.bootstrap(enc_a)
+        if enc_b.level < 8:
+            enc_b = eng.bootstrap(enc_b)
+        bx = self._build_power_basis(enc_a)
+        by = self._build_power_basis(enc_b)
+        pts = self.coeff_cache.get_plaintext_coeffs(eng)
+        res = eng.multiply(enc_a, 0.0)
+        for (i, j), pt in pts.items():
+            term = eng.multiply(bx[i], by[j], eng.relin_key)
+            res = eng.add(res, eng.multiply(term, pt))
+        return res
+
+    def xor(self, a_int: np.ndarray, b_int: np.ndarray) -> np.ndarray:
+        za, zb = ZetaEncoder.to_zeta(a_int), ZetaEncoder.to_zeta(b_int)
+        res = self.xor_cipher(self.eng_wrap.encrypt(za), self.eng_wrap.encrypt(zb))
+        return ZetaEncoder.from_zeta(self.eng_wrap.decrypt(res))
+
+    # -- fused path (same polynomial, BSGS + one relinearisation) --------------------------
+    def odd_basis(self, ct) -> Dict[int, object]:
+        """x^1, x^3, ..., x^15: x^2, x^4 squarings, three products, conjugates for 9..15."""
+        e = self.eng_wrap.engine
+        rlk = self.eng_wrap.relin_key
+        x2 = e.multiply(ct, ct, rlk)
+        x4 = e.multiply(x2, x2, rlk)
+        x3 = e.multiply(x2, ct, rlk)
+        x5 = e.multiply(x4, ct, rlk)
+        x7 = e.multiply(x4, x3, rlk)
+        basis = {1: ct, 3: x3, 5: x5, 7: x7}
+        for k in (1, 3, 5, 7):
+            basis[16 - k] = e.conjugate(basis[k], self.eng_wrap.conj_key)
+        return basis
+
+    def xor_cipher_bsgs(self, enc_a, enc_b, basis_a=None, basis_b=None):
+        """Same LUT polynomial as xor_cipher: sum_i x^i * L_i(y), L_i = sum_j c_ij y^j."""
+        e = self.eng_wrap.engine
+        coeffs = self.coeff_cache.load_coeffs()
+        bx = basis_a or self.odd_basis(enc_a)
+        by = basis_b or self.odd_basis(enc_b)
+        rows = sorted({i for i, _ in coeffs})
+        inner = []
+        for i in rows:
+            js = sorted(j for (ii, j) in coeffs if ii == i)
+            inner.append(e.lincomb([by[j] for j in js], [coeffs[(i, j)] for j in js]))
+        return e.dot([bx[i] for i in rows], inner, self.eng_wrap.relin_key)
+
+    # -- repaired nibble <-> byte conversions -------------------------------------------------
+    def recombine_nibbles(self, hi_ct, lo_ct, lo_domain: int = 256):
+        """zeta_256^{16 h + l} from hi = zeta_16^h (== zeta_256^{16 h}) and lo = zeta_256^l
+        (lo_domain=256, the GF-LUT outputs of gf_service) or lo = zeta_16^l (lo_domain=16,
+        mapped to zeta_256^l by a degree-15 LUT first).  The reference's version
+        (xor_service.py:256-269) raises hi to the 16th power, which collapses it to 1."""
+        eng = self.eng_wrap
+        if lo_domain == 16:
+            lo_ct = self._lut_16_to_256(lo_ct)
+        return eng.multiply(hi_ct, lo_ct, eng.relin_key)
+
+    def _lut_16_to_256(self, ct):
+        if self._lut16_to_256 is None:
+            self._lut16_to_256 = coeffs_gen.lut_1d(lambda x: x, 16, out_mod=256)
+        return eval_lut_1d(self.eng_wrap, ct, self._lut16_to_256)
+
+    def extract_nibbles(self, enc_vec):
+        """zeta_256^b -> (zeta_16^{b >> 4}, zeta_16^{b & 15}) with two degree-255 LUTs over one
+        shared power basis (replaces xor_service.py:434-496, which reads an unset cache)."""
+        hi_c = coeffs_gen.lut_1d(lambda x: x >> 4, 256, out_mod=16)
+        lo_c = coeffs_gen.lut_1d(lambda x: x & 15, 256, out_mod=16)
+        powers = self.eng_wrap.make_power_basis(enc_vec, 255)
+        return (eval_lut_1d(self.eng_wrap, enc_vec, hi_c, powers),
+                eval_lut_1d(self.eng_wrap, enc_vec, lo_c, powers))
+
+    def add_round_key(self, enc_state, round_key: np.ndarray):
+        """Byte-domain AddRoundKey: split both operands into nibbles, 4-bit XOR each half,
+        recombine to zeta_256^{s ^ k} (repairs xor_service.py:499-547)."""
+        eng = self.eng_wrap
+        sc = eng.engine.slot_count
+        zk = ZetaEncoder.to_zeta(np.asarray(round_key), modulus=256)
+        if zk.size < sc:
+            zk = np.pad(zk, (0, sc - zk.size), constant_values=1.0)
+        enc_key = eng.encrypt(zk)
+        s_hi, s_lo = self.extract_nibbles(enc_state)
+        k_hi, k_lo = self.extract_nibbles(enc_key)
+        x_hi = self.xor_cipher_bsgs(s_hi, k_hi)
+        x_lo = self.xor_cipher_bsgs(s_lo, k_lo)
+        return self.recombine_nibbles(x_hi, x_lo, lo_domain=16)
+
+
+def eval_lut_1d(eng_wrap: EngineWrapper, ct, coeffs: np.ndarray, powers=None):
+    """sum_k c_k ct^k with a fused linear combination (constant term added as a plaintext)."""
+    e = eng_wrap.engine
+    deg = int(np.max(np.nonzero(np.abs(coeffs) > 1e-12)[0])) if np.any(np.abs(coeffs) > 1e-12) else 0
+    if powers is None:
+        powers = eng_wrap.make_power_basis(ct, max(deg, 1))
+    ks = [k for k in range(1, deg + 1) if abs(coeffs[k]) > 1e-12]
+    out = e.lincomb([powers[k - 1] for k in ks], [coeffs[k] for k in ks])
+    if abs(coeffs[0]) > 1e-12:
+        out = e.add(out, complex(coeffs[0]))
+    return out

@@ -320,26 +320,41 @@ static dim3 ew_grid(aesfhe_engine* e, int y, int z) { return dim3(e->N / 256, y,
 
 // -----------------------------------------------------------------------------------------------
 // NTT dispatch
+// Each pass launch is profiled separately (family "ntt"): algorithmic bytes of one pass =
+// 8 B * N * limbs, half of the NTT's read-once + write-once 16 B per coefficient.
 template <int R1>
 static void ntt_fwd_t(aesfhe_engine* e, Span src, Span dst, int total) {
     constexpr int CW = (kTile / R1) < kC2 ? (kTile / R1) : kC2;
     constexpr int RW = (kTile / kC2) < R1 ? (kTile / kC2) : R1;
     Tabs T = e->tabs();
-    hipLaunchKernelGGL(k_ntt_fwd_cols<R1>, dim3(kC2 / CW, total), dim3(256), 0, e->stream, src, dst, T);
-    hipLaunchKernelGGL(k_ntt_fwd_rows<R1>, dim3(R1 / RW, total), dim3(256), 0, e->stream, dst, T);
+    const double by = 8.0 * e->N * (double)total;
+    {
+        ProfScope ps(e, FAM_NTT, by);
+        hipLaunchKernelGGL(k_ntt_fwd_cols<R1>, dim3(kC2 / CW, total), dim3(256), 0, e->stream, src, dst, T);
+    }
+    {
+        ProfScope ps(e, FAM_NTT, by);
+        hipLaunchKernelGGL(k_ntt_fwd_rows<R1>, dim3(R1 / RW, total), dim3(256), 0, e->stream, dst, T);
+    }
 }
 template <int R1>
 static void ntt_inv_t(aesfhe_engine* e, Span src, Span dst, int total) {
     constexpr int CW = (kTile / R1) < kC2 ? (kTile / R1) : kC2;
     constexpr int RW = (kTile / kC2) < R1 ? (kTile / kC2) : R1;
     Tabs T = e->tabs();
-    hipLaunchKernelGGL(k_ntt_inv_rows<R1>, dim3(R1 / RW, total), dim3(256), 0, e->stream, src, dst, T);
-    hipLaunchKernelGGL(k_ntt_inv_cols<R1>, dim3(kC2 / CW, total), dim3(256), 0, e->stream, dst, T);
+    const double by = 8.0 * e->N * (double)total;
+    {
+        ProfScope ps(e, FAM_NTT, by);
+        hipLaunchKernelGGL(k_ntt_inv_rows<R1>, dim3(R1 / RW, total), dim3(256), 0, e->stream, src, dst, T);
+    }
+    {
+        ProfScope ps(e, FAM_NTT, by);
+        hipLaunchKernelGGL(k_ntt_inv_cols<R1>, dim3(kC2 / CW, total), dim3(256), 0, e->stream, dst, T);
+    }
 }
 
 static void ntt(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
     if (total <= 0) return;
-    ProfScope ps(e, FAM_NTT, 16.0 * e->N * (double)total);
     switch (e->logN) {
 #define CASE(LG, R)                                                        \
     case LG:                                                               \
@@ -910,7 +925,6 @@ extern "C" int aesfhe_decrypt(aesfhe_engine* e, const aesfhe_key* sk, const aesf
 static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in) {
     const int N = e->N, l = in.level, P = in.B * in.np;
     aesfhe_ct* r = ct_new(e, in.B, in.np, l - 1);
-    ProfScope ps(e, FAM_EW, 0);
     Tmp x(e, (size_t)P * N), t(e, (size_t)P * l * N);
     // INTT of limb l of every poly: source poly p of batch b at d + b*bs + p*ps + l*N
     // (expressed as a Span over the flattened polys; requires bs == np*ps, true for compact views)
@@ -1061,6 +1075,22 @@ extern "C" int aesfhe_add_pt(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_
     API_END
 }
 
+extern "C" int aesfhe_add_const(aesfhe_engine* e, const aesfhe_ct* c, double re, double im, aesfhe_ct** out) {
+    API_BEGIN
+    const double s = e->chain.scale[c->level];
+    const int64_t A = llround(re * s), Bc = llround(im * s);
+    std::vector<u64> f;
+    std::vector<double> ff;
+    const_factors(e, A, Bc, c->level + 1, f, ff);
+    u64* df = upload_small(e, f.data(), f.size());
+    aesfhe_ct* r = ct_new(e, c->B, c->np, c->level);
+    hipLaunchKernelGGL(k_add_const, ew_grid(e, c->level + 1, c->B * c->np), dim3(256), 0, e->stream, opnd(view_of(c), c->B), out_of(r), c->np, (const u64*)df, e->q, e->logN);
+    HIPC(hipGetLastError());
+    r->is_zero = c->is_zero && A == 0 && Bc == 0;
+    *out = r;
+    API_END
+}
+
 extern "C" int aesfhe_mul_pt(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_pt* pt, aesfhe_ct** out) {
     API_BEGIN
     if (c->level < 1) throw_err(AESFHE_ELEVEL, "no level left for a plaintext multiplication");
@@ -1101,7 +1131,6 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
                       Opnd addend, aesfhe_ct* o) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long lN = (long)(l + 1) * N, neN = (long)ne * N;
-    ProfScope ps(e, FAM_KS, 0);
     Tmp dc(e, (size_t)B * lN), ext(e, (size_t)B * neN), acc(e, (size_t)B * 2 * neN);
     // 1. INTT copy of the input
     Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1), sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
@@ -1111,10 +1140,13 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
         const int lo = j * K, hi = std::min(lo + K, l + 1), alpha = hi - lo;
         const size_t set = (size_t)j * K + (alpha - 1);
         // 2. ModUp base conversion to every other limb, then NTT those limbs
+        {
+        ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
         hipLaunchKernelGGL(k_modup, dim3(N / 256, (ne + 7) / 8, B), dim3(256), 0, e->stream, (const u64*)dc.p, lN, ext.p, neN, lo, alpha, l, ne,
                            (const u64*)(e->mu_hatinv + set * K), (const double*)(e->mu_hatinvf + set * K),
                            (const u64*)(e->mu_hat + set * K * e->np), (const double*)(e->mu_hatf + set * K * e->np),
                            e->np, e->q, e->Lp1, e->logN);
+        }
         HIPC(hipGetLastError());
         // NTT of targets: limbs [0, lo) and [hi, ne) of every batch element
         if (lo > 0) {
@@ -1129,7 +1161,10 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
         // 3. inner product with the key digit
         const u64* kb = k->d + ((size_t)j * 2 + 0) * e->np * N;
         const u64* ka = k->d + ((size_t)j * 2 + 1) * e->np * N;
+        {
+        ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (B + 2 + (j == 0 ? 2 : 4) * B));
         hipLaunchKernelGGL(k_ks_inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, (const u64*)ext.p, neN, kb, ka, acc.p, 2 * neN, neN, B, lo, hi, l, e->q, e->qinv, e->Lp1, j == 0 ? 1 : 0, e->logN);
+        }
         HIPC(hipGetLastError());
     }
     // 4. ModDown: INTT special limbs of both accumulators
@@ -1138,13 +1173,17 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
         ntt(e, ssp, ssp, B * 2 * K, true);
     }
     Tmp conv(e, (size_t)B * 2 * lN);
+    {
+    ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + l + 1));
     hipLaunchKernelGGL(k_moddown, dim3(N / 256, (l + 1 + 7) / 8, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, conv.p, 2 * lN, lN, K,
                        (const u64*)e->md_phatinv, (const double*)e->md_phatinvf, (const u64*)e->md_phat, (const double*)e->md_phatf, e->Lp1, e->q, e->logN);
+    }
     HIPC(hipGetLastError());
     {
         Span sc = span_s(conv.p, lN, l + 1, l + 1, 0, e->Lp1);
         ntt(e, sc, sc, B * 2 * (l + 1), false);
     }
+    ProfScope psf(e, FAM_KS, 8.0 * N * (double)B * 2 * (l + 1) * 4);
     hipLaunchKernelGGL(k_moddown_finish, dim3(N / 256, l + 1, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, (const u64*)conv.p, 2 * lN, lN, addend, out_of(o), e->q, (const u64*)e->md_pinv, (const double*)e->md_pinvf, e->logN);
     HIPC(hipGetLastError());
 }

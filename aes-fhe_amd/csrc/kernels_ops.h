@@ -75,6 +75,16 @@ __global__ void k_add_pt(Opnd in, const u64* __restrict__ pt, Out o, int np,
     o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)l << logN) + k] = v;
 }
 
+// out = in + (f[2l] for k < N/2, f[2l+1] otherwise) on poly 0 ; grid (N/256, nl, B*np)
+__global__ void k_add_const(Opnd in, Out o, int np, const u64* __restrict__ f,
+                            const u64* __restrict__ qs, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z / np, p = blockIdx.z - bb * np;
+    u64 v = opnd_get(in, bb, p, l, k, logN);
+    if (p == 0) v = add_m(v, f[2 * l + (k >> (logN - 1))], qs[l]);
+    o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)l << logN) + k] = v;
+}
+
 // (d0,d1,d2) (+)= (a0 b0, a0 b1 + a1 b0, a1 b1) ; grid (N/256, nl, B)
 __global__ void k_tensor(Opnd a, Opnd b, Out o, const u64* __restrict__ qs,
                          const double* __restrict__ qinv, int acc, int logN) {

@@ -166,6 +166,9 @@ int aesfhe_negate(aesfhe_engine *eng, const aesfhe_ct *a, aesfhe_ct **out);
 /* pt must be encoded at the canonical scale of ct's level and created at that level */
 int aesfhe_add_pt(aesfhe_engine *eng, const aesfhe_ct *ct, const aesfhe_pt *pt,
                   aesfhe_ct **out);
+/* ct + (re + i*im) at ct's level (constant encoded at the canonical scale, no level used) */
+int aesfhe_add_const(aesfhe_engine *eng, const aesfhe_ct *ct, double re, double im,
+                     aesfhe_ct **out);
 /* pt encoded at aesfhe_engine_mul_scale(level); output rescaled to level-1 */
 int aesfhe_mul_pt(aesfhe_engine *eng, const aesfhe_ct *ct, const aesfhe_pt *pt,
                   aesfhe_ct **out);

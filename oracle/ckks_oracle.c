@@ -1133,6 +1133,26 @@ int aesfhe_add_pt(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_pt *pt, aes
     return 0;
 }
 
+int aesfhe_add_const(aesfhe_engine *e, const aesfhe_ct *c, double re, double im, aesfhe_ct **out) {
+    double s = e->scales[c->level];
+    i64 A = llround(re * s), Bc = llround(im * s);
+    aesfhe_ct *r;
+    aesfhe_ct_copy(e, c, &r);
+    r->is_zero = c->is_zero && A == 0 && Bc == 0;
+    for (int i = 0; i <= c->level; i++) {
+        const u64 q = e->q[i];
+        u64 a = smod(A, q), bi = mul_mod_slow(smod(Bc, q), e->iroot[i], q);
+        u64 f0 = add_mod(a, bi, q), f1 = sub_mod(a, bi, q);
+        for (int b = 0; b < c->B; b++) {
+            u64 *x = limb(e, r, b, 0, i);
+            for (int j = 0; j < e->N / 2; j++) x[j] = add_mod(x[j], f0, q);
+            for (int j = e->N / 2; j < e->N; j++) x[j] = add_mod(x[j], f1, q);
+        }
+    }
+    *out = r;
+    return 0;
+}
+
 int aesfhe_mul_pt(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_pt *pt, aesfhe_ct **out) {
     if (c->level < 1) return fail(AESFHE_ELEVEL, "no level left for a plaintext multiplication");
     if (pt->level < c->level) return fail(AESFHE_EARG, "plaintext level %d below ciphertext level %d", pt->level, c->level);
