@@ -58,6 +58,7 @@ SIGNATURES = [
      [C.c_int32, _P(C.c_double), _P(C.c_double), C.c_int64, C.c_double, _P(C.c_int64)]),
     ("aesfhe_decode", C.c_int,
      [C.c_int32, _P(C.c_int64), C.c_double, _P(C.c_double), _P(C.c_double)]),
+    ("aesfhe_chain", C.c_int, [_P(Params), _P(C.c_uint64), _P(C.c_double)]),
     ("aesfhe_key_secret", C.c_int, [c_eng_p, C.c_uint64, _P(c_key_p)]),
     ("aesfhe_key_public", C.c_int, [c_eng_p, c_key_p, _P(c_key_p)]),
     ("aesfhe_key_relin", C.c_int, [c_eng_p, c_key_p, _P(c_key_p)]),

@@ -189,10 +189,14 @@ struct Codec {
         M = 2 * N;
         kre.resize(M + 1);
         kim.resize(M + 1);
+        // libm cos/sin through volatile pointers: never fused into sincos() (its last bit can
+        // differ), so the table matches the oracle's bit for bit
+        double (*volatile fcos)(double) = ::cos;
+        double (*volatile fsin)(double) = ::sin;
         for (long j = 0; j <= M; j++) {
             double ang = 2.0 * M_PI * (double)j / (double)M;
-            kre[j] = std::cos(ang);
-            kim[j] = std::sin(ang);
+            kre[j] = fcos(ang);
+            kim[j] = fsin(ang);
         }
         rot.resize(n);
         long g = 1;

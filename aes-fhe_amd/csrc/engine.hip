@@ -544,6 +544,14 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
     API_END
 }
 
+extern "C" int aesfhe_chain(const aesfhe_params* pp, uint64_t* primes, double* scales) {
+    API_BEGIN
+    Chain c = make_chain(pp->log_n, pp->max_level, pp->special_primes, pp->base_bits, pp->special_bits, pp->scale_bits);
+    std::copy(c.q.begin(), c.q.end(), primes);
+    std::copy(c.scale.begin(), c.scale.end(), scales);
+    API_END
+}
+
 extern "C" void aesfhe_engine_destroy(aesfhe_engine* e) {
     if (!e) return;
     hipSetDevice(e->device);

@@ -116,6 +116,10 @@ int aesfhe_encode(int32_t log_n, const double *re, const double *im, int64_t n_s
 int aesfhe_decode(int32_t log_n, const int64_t *coeffs, double scale, double *re_out,
                   double *im_out);
 
+/* Prime chain + canonical scales the engine would generate for these parameters (host only):
+ * primes_out L+1+K words, scales_out L+1 doubles. */
+int aesfhe_chain(const aesfhe_params *params, uint64_t *primes_out, double *scales_out);
+
 /* ---- keys ------------------------------------------------------------------------------- */
 int aesfhe_key_secret(aesfhe_engine *eng, uint64_t seed, aesfhe_key **out);
 int aesfhe_key_public(aesfhe_engine *eng, const aesfhe_key *sk, aesfhe_key **out);

@@ -426,6 +426,22 @@ int aesfhe_engine_create(const aesfhe_params *pp, aesfhe_engine **out) {
     return 0;
 }
 
+int aesfhe_chain(const aesfhe_params *pp, uint64_t *primes, double *scales) {
+    aesfhe_engine tmp;
+    memset(&tmp, 0, sizeof tmp);
+    tmp.logN = pp->log_n;
+    tmp.N = 1 << pp->log_n;
+    tmp.L = pp->max_level;
+    tmp.K = pp->special_primes;
+    tmp.np = tmp.L + 1 + tmp.K;
+    if (tmp.np > MAXP) return fail(AESFHE_EARG, "too many primes");
+    int rc = gen_primes(&tmp, pp->base_bits, pp->special_bits, pp->scale_bits);
+    if (rc) return rc;
+    memcpy(primes, tmp.q, sizeof(u64) * tmp.np);
+    memcpy(scales, tmp.scales, sizeof(double) * (tmp.L + 1));
+    return 0;
+}
+
 void aesfhe_engine_destroy(aesfhe_engine *e) {
     if (!e) return;
     for (int p = 0; p < e->np; p++) {
@@ -498,10 +514,14 @@ static void codec_init(codec_t *c, int logN) {
     c->M = 2 * N;
     c->kre = malloc(sizeof(double) * (c->M + 1));
     c->kim = malloc(sizeof(double) * (c->M + 1));
+    /* called through volatile pointers so no compiler fuses them into sincos(), whose last
+       bit can differ: the HIP engine's host codec must produce the same table */
+    double (*volatile fcos)(double) = cos;
+    double (*volatile fsin)(double) = sin;
     for (long j = 0; j <= c->M; j++) {
         double ang = 2.0 * M_PI * (double)j / (double)c->M;
-        c->kre[j] = cos(ang);
-        c->kim[j] = sin(ang);
+        c->kre[j] = fcos(ang);
+        c->kim[j] = fsin(ang);
     }
     c->rot = malloc(sizeof(long) * c->n);
     long g = 1;

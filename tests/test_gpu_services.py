@@ -1,0 +1,83 @@
+"""The reference services on the HIP engine at BASELINE.json's parameters (N = 2^16, L = 30),
+checked against the reference's own decoded outputs (tests/golden/, 32768 slots) and FIPS-197.
+Size-independent properties cover what the golden run cannot: the batched AES round
+decrypts to the plaintext round for every block of every ciphertext."""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from aes_xor_fhe import aes_tables as T
+from aes_xor_fhe.engine_context import EngineContext
+from aes_xor_fhe.xor_service import EngineWrapper, XORConfig, XORService, ZetaEncoder
+
+pytestmark = pytest.mark.gpu
+GOLD = np.load(Path(__file__).resolve().parent / "golden" / "golden.npz")
+
+
+@pytest.fixture(scope="module")
+def wrap(product_lib, gpu_available):
+    ctx = EngineContext(signature=1, seed=2024)
+    assert ctx.engine._lib.backend == "hip-gfx950"
+    assert ctx.engine.slot_count == 32768 and ctx.engine.max_level == 30
+    return EngineWrapper(XORConfig(), ctx=ctx)
+
+
+def test_xor_random_32768(wrap):                     # test/test_xor_service.py:38-43
+    svc = XORService(wrap)
+    out = svc.xor(GOLD["xor_a"], GOLD["xor_b"])
+    assert np.array_equal(out, GOLD["xor_a"] ^ GOLD["xor_b"])
+    assert np.array_equal(out, GOLD["xor_out"])
+
+
+def test_xor_simple(wrap):                           # test/test_xor_service.py:31-35
+    a = np.array([0, 1, 2, 3], dtype=np.uint8)
+    b = np.array([3, 2, 1, 0], dtype=np.uint8)
+    assert np.array_equal(XORService(wrap).xor(a, b)[:4], a ^ b)
+
+
+def test_full_round_ark_32768(wrap):                 # new.py:231-262
+    from aes_xor_fhe.new import AESFHERound
+    out = AESFHERound(wrap, XORService(wrap)).full_round(GOLD["ark_state"], GOLD["ark_key"])
+    assert np.array_equal(out, GOLD["ark_out"])
+    assert np.array_equal(out, GOLD["ark_state"] ^ GOLD["ark_key"])
+
+
+def test_sub_bytes_array_32768(wrap):                # test/test_sbox_service.py:55-65
+    from aes_xor_fhe.sbox.sbox_service import SBoxService
+    from aes_xor_fhe.utils import zeta_decode, zeta_encode
+    sb = SBoxService(wrap.ctx)
+    enc = wrap.engine.encrypt(zeta_encode(GOLD["sbox_in"], modulus=256), wrap.public_key)
+    out = sb.sub_bytes_array(enc)
+    got = zeta_decode(wrap.engine.decrypt(out, wrap.secret_key), modulus=256)
+    assert np.array_equal(got, GOLD["sbox_out"])
+    assert 30 - out.level == int(GOLD["sbox_level_drop"][0])
+
+
+def test_gf_and_shiftrows(wrap):
+    from aes_xor_fhe.gf_service import GFService
+    from aes_xor_fhe.shiftrows_service import AESFHEShiftRows
+    from aes_xor_fhe.utils import zeta_decode, zeta_encode
+    n = wrap.engine.slot_count
+    x = np.resize(np.arange(256), n)
+    ct = wrap.engine.encrypt(zeta_encode(x, modulus=256), wrap.public_key)
+    svc = XORService(wrap)
+    gf = GFService(wrap, svc)
+    hi, lo = gf.mul3(ct)
+    assert np.array_equal(zeta_decode(wrap.decrypt(svc.recombine_nibbles(hi, lo)), 256), T.GF3[x])
+    sr = AESFHEShiftRows(wrap)
+    state = np.resize(np.arange(16), n).astype(float)
+    out = np.real(wrap.decrypt(sr.shift_rows(wrap.encrypt(state)))).round().astype(int)
+    assert np.array_equal(out, T.shift_rows(state.reshape(-1, 16).astype(int)).ravel())
+
+
+def test_aes_round_engine_batched(wrap):
+    from aes_xor_fhe.aes_round import AESRoundEngine
+    e = wrap.engine
+    R = AESRoundEngine(e, wrap.secret_key, wrap.public_key, wrap.relin_key, wrap.conj_key)
+    rng = np.random.default_rng(11)
+    blocks = rng.integers(0, 256, (2, R.n_blk, 16), dtype=np.uint8)
+    rk = T.expand_key(rng.integers(0, 256, 16, dtype=np.uint8))[3]
+    h, l = R.encrypt_blocks(blocks)
+    oh, ol = R.round(h, l, R.encrypt_round_key(rk))
+    assert np.array_equal(R.decrypt_blocks(oh, ol), T.aes_round(blocks, rk))

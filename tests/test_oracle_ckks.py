@@ -1,0 +1,131 @@
+"""The CPU oracle pinned before it is trusted: the reference's engine-contract tests
+(test/test_engine_rot.py:21-61) restated on it, NTT known answers against big-integer
+schoolbook negacyclic convolution, canonical-embedding encode against direct evaluation."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from aes_xor_fhe.fhe import Engine
+
+KW = dict(log_n=10, max_level=6, special_primes=2, seed=5)
+
+
+@pytest.fixture(scope="module")
+def env(oracle_lib):
+    e = Engine(_lib=oracle_lib, **KW)
+    sk = e.create_secret_key()
+    return e, sk, e.create_public_key(sk), e.create_relinearization_key(sk), e.create_rotation_key(sk)
+
+
+def test_encrypt_decrypt_identity(env):            # test_engine_rot.py:21-29
+    e, sk, pk, *_ = env
+    vec = np.linspace(0.0, 1.0, num=e.slot_count)
+    np.testing.assert_allclose(e.decrypt(e.encrypt(vec, pk), sk), vec, atol=1e-6)
+
+
+@pytest.mark.parametrize("k", [5, -4, 1, 300, -511])
+def test_rotate_is_np_roll(env, k):                # test_engine_rot.py:32-40
+    e, sk, pk, _, rot = env
+    base = np.arange(e.slot_count, dtype=np.float64)
+    np.testing.assert_allclose(e.decrypt(e.rotate(e.encrypt(base, pk), rot, k), sk),
+                               np.roll(base, k), atol=1e-6)
+
+
+def test_relinearize_noop_and_error(env):          # test_engine_rot.py:43-50
+    e, sk, pk, rlk, _ = env
+    from aes_xor_fhe.xor_service import EngineWrapper
+    vec = np.random.RandomState(0).rand(e.slot_count)
+    ct = e.encrypt(vec, pk)
+    with pytest.raises(RuntimeError, match="should have 3 polynomials"):
+        e.relinearize(ct, rlk)
+
+    class Ctx:  # EngineWrapper over an existing engine (xor_service.py:107-118 swallow path)
+        engine, secret_key, public_key, relinearization_key = e, sk, pk, rlk
+        conjugation_key = rotation_key = bootstrap_key = None
+    ew = EngineWrapper(None, ctx=Ctx)
+    np.testing.assert_allclose(e.decrypt(ew.relinearize(ct), sk), vec, atol=1e-6)
+
+
+def test_square_after_relin(env):                  # test_engine_rot.py:53-61
+    e, sk, pk, rlk, _ = env
+    vec = np.random.RandomState(1).rand(e.slot_count)
+    ct = e.encrypt(vec, pk)
+    sq = e.multiply(ct, ct, rlk)
+    assert sq.level == ct.level - 1
+    np.testing.assert_allclose(e.decrypt(sq, sk), vec * vec, atol=1e-5)
+    # unrelinearised product + explicit relinearize
+    t3 = e.multiply(ct, ct)
+    assert t3.npoly == 3
+    np.testing.assert_allclose(e.decrypt(e.relinearize(t3, rlk), sk), vec * vec, atol=1e-5)
+
+
+@pytest.mark.parametrize("log_n", [4, 6, 8])
+def test_ntt_known_answer_schoolbook(oracle_lib, log_n):
+    e = Engine(_lib=oracle_lib, log_n=log_n, max_level=2, special_primes=1, seed=1)
+    N = 1 << log_n
+    rng = np.random.default_rng(log_n)
+    for pid, q in enumerate(e.primes):
+        a = rng.integers(0, q, N, dtype=np.uint64)
+        b = rng.integers(0, q, N, dtype=np.uint64)
+        # schoolbook negacyclic product in Python integers
+        ref = [0] * N
+        for i in range(N):
+            for j in range(N):
+                k, v = i + j, int(a[i]) * int(b[j])
+                if k >= N:
+                    ref[k - N] -= v
+                else:
+                    ref[k] += v
+        ref = np.array([x % q for x in ref], dtype=np.uint64)
+        bufs = np.stack([a, b]).copy()
+        pids = np.array([pid, pid], dtype=np.int32)
+        e._check(oracle_lib.ntt_host(e._h, bufs.ctypes.data_as(C.POINTER(C.c_uint64)), 2,
+                                     pids.ctypes.data_as(C.POINTER(C.c_int32)), 0))
+        prod = np.array([(int(x) * int(y)) % q for x, y in zip(bufs[0], bufs[1])], dtype=np.uint64)
+        prod = prod.reshape(1, N).copy()
+        e._check(oracle_lib.ntt_host(e._h, prod.ctypes.data_as(C.POINTER(C.c_uint64)), 1,
+                                     pids[:1].ctypes.data_as(C.POINTER(C.c_int32)), 1))
+        np.testing.assert_array_equal(prod[0], ref)
+
+
+@pytest.mark.parametrize("log_n", [6, 10])
+def test_encode_is_canonical_embedding(oracle_lib, log_n):
+    N, n = 1 << log_n, 1 << (log_n - 1)
+    rng = np.random.default_rng(0)
+    z = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    co = np.empty(N, np.int64)
+    re_, im_ = np.ascontiguousarray(z.real), np.ascontiguousarray(z.imag)
+    oracle_lib.check(oracle_lib.encode(log_n, re_.ctypes.data_as(C.POINTER(C.c_double)),
+                                       im_.ctypes.data_as(C.POINTER(C.c_double)), n, 2.0 ** 30,
+                                       co.ctypes.data_as(C.POINTER(C.c_int64))))
+    M = 2 * N
+    roots = np.exp(2j * np.pi * np.array([pow(5, j, M) for j in range(n)]) / M)
+    vals = np.polyval(co[::-1].astype(np.float64), roots) / 2.0 ** 30
+    np.testing.assert_allclose(vals, z, atol=1e-6)
+
+
+def test_deterministic_keys_and_encryption(oracle_lib):
+    outs = []
+    for _ in range(2):
+        e = Engine(_lib=oracle_lib, **KW)
+        sk = e.create_secret_key(3)
+        ct = e.encrypt(np.ones(4), e.create_public_key(sk))
+        outs.append(e.export_residues(ct))
+    np.testing.assert_array_equal(*outs)
+
+
+def test_levels_and_scales(env):
+    e, sk, pk, rlk, _ = env
+    z = np.exp(-2j * np.pi * np.arange(e.slot_count) / 16)
+    ct = e.encrypt(z, pk)
+    pb = e.make_power_basis(ct, 8, rlk)
+    assert [c.level for c in pb] == [6, 5, 4, 4, 3, 3, 3, 3]
+    for k, c in enumerate(pb, 1):
+        np.testing.assert_allclose(e.decrypt(c, sk), z ** k, atol=1e-6)
+    lo = e.level_down(ct, 2)
+    assert lo.level == 2
+    np.testing.assert_allclose(e.decrypt(lo, sk), z, atol=1e-6)
+    s = e.add(pb[7], ct)                                   # mixed levels align
+    np.testing.assert_allclose(e.decrypt(s, sk), z ** 8 + z, atol=1e-6)
+    np.testing.assert_allclose(e.decrypt(e.add(ct, 0.5 - 0.25j), sk), z + 0.5 - 0.25j, atol=1e-6)
