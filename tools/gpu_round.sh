@@ -1,0 +1,18 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, bench (with CPU baseline), rocprof kernel stats.
+# Every GPU step has its own time limit; steps are chained so a failure stops the script.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r01}
+timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 \
+ && echo "gpu tests ok" \
+ && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+ && echo "smoke ok" \
+ && timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err \
+ && echo "bench ok" \
+ && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o bench -- python bench.py --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/prof_${TAG}.log 2>&1 \
+ && echo "rocprof ok"
+rc=$?
+tail -3 gpurun_out/pytest_gpu.log; cat gpurun_out/smoke.log 2>/dev/null | tail -2; cat gpurun_out/bench_${TAG}.json 2>/dev/null
+exit $rc
