@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -19,6 +20,7 @@
 
 #include "../../include/aesfhe.h"
 #include "kernels_ops.h"
+#include "ntt256.h"
 
 using namespace aesfhe;
 
@@ -131,6 +133,7 @@ struct aesfhe_engine {
     // device tables
     u64 *q, *psi, *ipsi, *ninv;
     double *qinv, *psif, *ipsif, *ninvf;
+    Tw *tw, *itw;
     u64* iroot;  // host copy only needed
     std::vector<u64> h_iroot;
     // base conversion tables
@@ -158,6 +161,8 @@ struct aesfhe_engine {
         t.ipsif = ipsif;
         t.ninv = ninv;
         t.ninvf = ninvf;
+        t.tw = tw;
+        t.itw = itw;
         t.logN = logN;
         t.Lp1 = Lp1;
         return t;
@@ -353,8 +358,36 @@ static void ntt_inv_t(aesfhe_engine* e, Span src, Span dst, int total) {
     }
 }
 
+// N = 2^16: register-resident radix-16x16 passes (ntt256.h)
+static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
+    Tabs T = e->tabs();
+    const double by = 8.0 * e->N * (double)total;
+    if (!inverse) {
+        {
+            ProfScope ps(e, FAM_NTT, by);
+            hipLaunchKernelGGL(k_ntt256_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
+        }
+        ProfScope ps(e, FAM_NTT, by);
+        hipLaunchKernelGGL(k_ntt256_fwd_rows, dim3(16, total), dim3(256), 0, e->stream, dst, T);
+    } else {
+        {
+            ProfScope ps(e, FAM_NTT, by);
+            hipLaunchKernelGGL(k_ntt256_inv_rows, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
+        }
+        ProfScope ps(e, FAM_NTT, by);
+        hipLaunchKernelGGL(k_ntt256_inv_cols, dim3(16, total), dim3(256), 0, e->stream, dst, T);
+    }
+}
+
+static bool g_ntt_generic = getenv("AESFHE_NTT_GENERIC") != nullptr;
+
 static void ntt(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
     if (total <= 0) return;
+    if (e->logN == 16 && !g_ntt_generic) {
+        ntt256(e, src, dst, total, inverse);
+        HIPC(hipGetLastError());
+        return;
+    }
     switch (e->logN) {
 #define CASE(LG, R)                                                        \
     case LG:                                                               \
@@ -430,6 +463,15 @@ static void build_tables(aesfhe_engine* e) {
     up(hipsif, &e->ipsif);
     up(hninv, &e->ninv);
     up(hninvf, &e->ninvf);
+    {
+        std::vector<Tw> htw((size_t)np * N), hitw((size_t)np * N);
+        for (size_t i = 0; i < htw.size(); i++) {
+            htw[i] = Tw{hpsi[i], hpsif[i]};
+            hitw[i] = Tw{hipsi[i], hipsif[i]};
+        }
+        up(htw, &e->tw);
+        up(hitw, &e->itw);
+    }
 
     // ModUp tables per (digit j, alpha a): hatinv[i], hat[i][pid]
     const size_t mu_sets = (size_t)e->dnum * K;
@@ -565,7 +607,7 @@ extern "C" void aesfhe_engine_destroy(aesfhe_engine* e) {
     void* ptrs[] = {e->q, e->psi, e->ipsi, e->ninv, e->qinv, e->psif, e->ipsif, e->ninvf,
                     e->mu_hatinv, e->mu_hat, e->md_phatinv, e->md_phat, e->md_pinv, e->rs_inv,
                     e->rs_mod, e->pmod, e->mu_hatinvf, e->mu_hatf, e->md_phatinvf, e->md_phatf,
-                    e->md_pinvf, e->rs_invf, e->ring_d};
+                    e->md_pinvf, e->rs_invf, e->ring_d, e->tw, e->itw};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (e->ring_h) hipHostFree(e->ring_h);
@@ -1330,6 +1372,7 @@ extern "C" int aesfhe_power_basis(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
 extern "C" int aesfhe_lincomb(aesfhe_engine* e, const aesfhe_ct* const* cts, int32_t n, const double* re, const double* im, aesfhe_ct** out) {
     API_BEGIN
     if (n < 1) throw_err(AESFHE_EARG, "empty linear combination");
+    if (n > 4096) throw_err(AESFHE_EARG, "linear combination too long");
     int l = cts[0]->level, B = 1, np = 2;
     for (int i = 0; i < n; i++) {
         l = std::min(l, cts[i]->level);
@@ -1339,24 +1382,46 @@ extern "C" int aesfhe_lincomb(aesfhe_engine* e, const aesfhe_ct* const* cts, int
     for (int i = 0; i < n; i++)
         if (cts[i]->B != B && cts[i]->B != 1) throw_err(AESFHE_EARG, "batch mismatch");
     if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a linear combination");
-    double s = aesfhe_engine_mul_scale(e, l);
-    aesfhe_ct* acc = ct_new(e, B, np, l);
-    bool any = false;
+    const int nl = l + 1;
+    const double s = aesfhe_engine_mul_scale(e, l);
+    // gather the contributing inputs, each aligned to level l
+    std::vector<std::unique_ptr<Aligned>> al;
+    std::vector<const u64*> ptrs;
+    std::vector<long> bstr;
+    std::vector<int> npi;
+    std::vector<u64> f;
+    std::vector<double> ff;
     for (int i = 0; i < n; i++) {
         int64_t A = llround(re[i] * s), Bc = llround(im[i] * s);
         if (cts[i]->is_zero || (A == 0 && Bc == 0)) continue;
-        Aligned a;
-        align_to(e, cts[i], l, a);
-        // the first contributing input writes every polynomial it has; a missing third
-        // polynomial (2-poly input into a 3-poly sum) is zero-filled first
-        if (!any && a.v.np < np) HIPC(hipMemsetAsync(acc->d, 0, acc->bytes, e->stream));
-        mul_const_into(e, a.v, A, Bc, acc, (any || a.v.np < np) ? 1 : 0);
-        any = true;
+        al.emplace_back(new Aligned());
+        align_to(e, cts[i], l, *al.back());
+        const View& v = al.back()->v;
+        ptrs.push_back(v.d);
+        bstr.push_back(v.B == 1 && B > 1 ? 0 : v.bs);
+        npi.push_back(v.np);
+        std::vector<u64> fi;
+        std::vector<double> ffi;
+        const_factors(e, A, Bc, nl, fi, ffi);
+        f.insert(f.end(), fi.begin(), fi.end());
+        ff.insert(ff.end(), ffi.begin(), ffi.end());
     }
-    if (!any) {
-        aesfhe_ct_free(acc);
+    if (ptrs.empty()) {
         *out = ct_zero_new(e, B, np, l - 1);
     } else {
+        const int m = (int)ptrs.size();
+        const long ps = (long)nl * e->N;
+        aesfhe_ct* acc = ct_new(e, B, np, l);
+        auto dp = upload_small(e, ptrs.data(), ptrs.size());
+        auto db = upload_small(e, bstr.data(), bstr.size());
+        auto dn = upload_small(e, npi.data(), npi.size());
+        auto df = upload_small(e, f.data(), f.size());
+        auto dff = upload_small(e, ff.data(), ff.size());
+        {
+            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (m + 1));
+            hipLaunchKernelGGL(k_lincomb, ew_grid(e, nl, B * np), dim3(256), 0, e->stream, (const u64* const*)dp, (const long*)db, (const int*)dn, m, ps, (const u64*)df, (const double*)dff, out_of(acc), np, nl, e->q, e->qinv, e->logN);
+        }
+        HIPC(hipGetLastError());
         *out = rescale_view(e, view_of(acc));
         aesfhe_ct_free(acc);
     }
@@ -1376,21 +1441,37 @@ extern "C" int aesfhe_dot(aesfhe_engine* e, const aesfhe_ct* const* a, const aes
     for (int i = 0; i < n; i++)
         if ((a[i]->B != B && a[i]->B != 1) || (b[i]->B != B && b[i]->B != 1)) throw_err(AESFHE_EARG, "batch mismatch");
     if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a dot product");
-    aesfhe_ct* acc = ct_new(e, B, 3, l);
-    bool any = false;
+    const int nl = l + 1;
+    std::vector<std::unique_ptr<Aligned>> al;
+    std::vector<const u64*> pa, pb;
+    std::vector<long> sa, sb;
     for (int i = 0; i < n; i++) {
         if (a[i]->is_zero || b[i]->is_zero) continue;
-        Aligned x, y;
-        align_to(e, a[i], l, x);
-        align_to(e, b[i], l, y);
-        hipLaunchKernelGGL(k_tensor, ew_grid(e, l + 1, B), dim3(256), 0, e->stream, opnd(x.v, B), opnd(y.v, B), out_of(acc), e->q, e->qinv, any ? 1 : 0, e->logN);
-        HIPC(hipGetLastError());
-        any = true;
+        al.emplace_back(new Aligned());
+        align_to(e, a[i], l, *al.back());
+        const View va = al.back()->v;
+        al.emplace_back(new Aligned());
+        align_to(e, b[i], l, *al.back());
+        const View vb = al.back()->v;
+        pa.push_back(va.d);
+        pb.push_back(vb.d);
+        sa.push_back(va.B == 1 && B > 1 ? 0 : va.bs);
+        sb.push_back(vb.B == 1 && B > 1 ? 0 : vb.bs);
     }
-    if (!any) {
-        aesfhe_ct_free(acc);
+    if (pa.empty()) {
         *out = ct_zero_new(e, B, 2, l - 1);
     } else {
+        const int m = (int)pa.size();
+        aesfhe_ct* acc = ct_new(e, B, 3, l);
+        auto dpa = upload_small(e, pa.data(), pa.size());
+        auto dpb = upload_small(e, pb.data(), pb.size());
+        auto dsa = upload_small(e, sa.data(), sa.size());
+        auto dsb = upload_small(e, sb.data(), sb.size());
+        {
+            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * (4.0 * m + 3));
+            hipLaunchKernelGGL(k_dot, ew_grid(e, nl, B), dim3(256), 0, e->stream, (const u64* const*)dpa, (const long*)dsa, (const u64* const*)dpb, (const long*)dsb, m, (long)nl * e->N, out_of(acc), e->q, e->qinv, e->logN);
+        }
+        HIPC(hipGetLastError());
         aesfhe_ct* rl = relin_ct(e, acc, rlk);
         aesfhe_ct_free(acc);
         *out = rescale_view(e, view_of(rl));

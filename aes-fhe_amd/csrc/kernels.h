@@ -30,15 +30,27 @@ __device__ __forceinline__ u64 fix_m(u64 r, u64 q) {  // r = true value in [-q, 
     return (u64)s;
 }
 
-// a * b mod q, a,b < 2^51
+// fp64 view of an integer a < 2^52 (exact): the 2^52 magic-number trick, two instructions
+__device__ __forceinline__ double u2d(u64 a) {
+    return __longlong_as_double((long long)(a | 0x4330000000000000ULL)) - 4503599627370496.0;
+}
+// nearest integer of a non-negative x < 2^52 (one fma against 2^52, then the mantissa bits)
+__device__ __forceinline__ u64 rint_u(double x_times, double scale) {
+    return (u64)__double_as_longlong(__builtin_fma(x_times, scale, 4503599627370496.0)) & 0xFFFFFFFFFFFFFULL;
+}
+
+// a * b mod q, a,b < q < 2^51: quotient a*b/q rounded to nearest in fp64 (|error| <= 1), exact
+// remainder from two wrapping 64-bit products, one two-sided correction.
 __device__ __forceinline__ u64 mul_m(u64 a, u64 b, u64 q, double qinv) {
-    u64 qh = (u64)(((double)a * (double)b) * qinv);
+    const u64 qh = rint_u(u2d(a) * u2d(b), qinv);
     return fix_m(a * b - qh * q, q);
 }
-// a * w mod q with wq = w / q precomputed
+// a * w mod q for a < 2^52, w < q < 2^51, wq = w / q: remainder in (-q, q), one correction
 __device__ __forceinline__ u64 mul_w(u64 a, u64 w, double wq, u64 q) {
-    u64 qh = (u64)((double)a * wq);
-    return fix_m(a * w - qh * q, q);
+    const u64 qh = rint_u(u2d(a), wq);
+    int64_t r = (int64_t)(a * w - qh * q);
+    r += (r >> 63) & (int64_t)q;
+    return (u64)r;
 }
 
 // A set of limbs: poly p (0..npoly-1), limb l (0..nl-1) at base + p*pstride + l*N.
@@ -68,8 +80,15 @@ struct Tabs {
     const double* ipsif;
     const u64* ninv;
     const double* ninvf;
+    const struct Tw* tw;   // [np][N] {psi^{brv(k)}, psi^{brv(k)}/q} interleaved (16 B)
+    const struct Tw* itw;  // [np][N] inverse
     int logN;
     int Lp1;
+};
+
+struct alignas(16) Tw {
+    u64 w;
+    double wq;
 };
 
 // ---------------------------------------------------------------------------------------------

@@ -3,10 +3,12 @@
 // oracle, oracle/ckks_oracle.c, which these kernels must match residue for residue).
 #pragma once
 #include "kernels.h"
+#include "ntt256.h"
 
 namespace aesfhe {
 
 // fp64-quotient reduction of x < 2^52
+// reduction of x < 2^63 (lazy sums): fp64 quotient estimate, two-sided correction
 __device__ __forceinline__ u64 red_m(u64 x, u64 q, double qinv) {
     u64 qh = (u64)((double)x * qinv);
     return fix_m(x - qh * q, q);
@@ -107,6 +109,61 @@ __global__ void k_tensor(Opnd a, Opnd b, Out o, const u64* __restrict__ qs,
         base[o.ps] = d1;
         base[2 * o.ps] = d2;
     }
+}
+
+// Fused linear combination: out[b][p][l] = sum_i in_i[b][p][l] * f_i(l, half) (one pass, lazy
+// sum in u64: n <= 64 terms of < 2^51 each).  ptrs/bstr: [n]; f/ff: [n][nl][2].  Inputs with
+// fewer polynomials than np contribute zero to the missing ones (npi[i]).
+// grid (N/256, nl, B*np)
+__global__ void k_lincomb(const u64* const* __restrict__ ptrs, const long* __restrict__ bstr,
+                          const int* __restrict__ npi, int n, long ps, const u64* __restrict__ f,
+                          const double* __restrict__ ff, Out o, int np, int nl,
+                          const u64* __restrict__ qs, const double* __restrict__ qinv, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z / np, p = blockIdx.z - bb * np;
+    const u64 q = qs[l];
+    const int h = k >> (logN - 1);
+    const long off = (long)p * ps + ((long)l << logN) + k;
+    u64 acc = 0;
+    for (int i = 0; i < n; i++) {
+        if (p >= npi[i]) continue;
+        const u64 v = ptrs[i][(long)bb * bstr[i] + off];
+        const int fi = (i * nl + l) * 2 + h;
+        acc += mulw(v, f[fi], ff[fi], q);
+    }
+    o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)l << logN) + k] = red_m(acc, q, qinv[l]);
+}
+
+// Fused dot product: (d0,d1,d2) = sum_i a_i (x) b_i (one pass).  a/b pointer + batch-stride
+// arrays [n]; inputs compact 2-poly ciphertexts at the same level (poly stride ps).
+// grid (N/256, nl, B)
+__global__ void k_dot(const u64* const* __restrict__ ap, const long* __restrict__ abs_,
+                      const u64* const* __restrict__ bp, const long* __restrict__ bbs, int n,
+                      long ps, Out o, const u64* __restrict__ qs, const double* __restrict__ qinv,
+                      int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z;
+    const u64 q = qs[l];
+    const double qi = qinv[l];
+    const long off = ((long)l << logN) + k;
+    u64 d0 = 0, d1 = 0, d2 = 0;
+    for (int i = 0; i < n; i++) {
+        const u64* a = ap[i] + (long)bb * abs_[i] + off;
+        const u64* b = bp[i] + (long)bb * bbs[i] + off;
+        const u64 a0 = a[0], a1 = a[ps], b0 = b[0], b1 = b[ps];
+        d0 += mul_m(a0, b0, q, qi);
+        d1 += mul_m(a0, b1, q, qi) + mul_m(a1, b0, q, qi);
+        d2 += mul_m(a1, b1, q, qi);
+        if ((i & 15) == 15) {  // keep the lazy sums below 2^52 for red_m
+            d0 = red_m(d0, q, qi);
+            d1 = red_m(d1, q, qi);
+            d2 = red_m(d2, q, qi);
+        }
+    }
+    u64* base = o.ptr + (long)bb * o.bs + off;
+    base[0] = red_m(d0, q, qi);
+    base[o.ps] = red_m(d1, q, qi);
+    base[2 * o.ps] = red_m(d2, q, qi);
 }
 
 // ---------------------------------------------------------------------------------------------
