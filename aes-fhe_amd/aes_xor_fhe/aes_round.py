@@ -146,15 +146,16 @@ class AESRoundEngine:
 
     # ---- LUT evaluation -------------------------------------------------------------------------
     def _inner(self, ybasis: Dict[int, Ciphertext], C: np.ndarray, rows: Sequence[int]):
-        """L_i(y) = sum_{j>=1} C[i, j] y^j for the requested rows (rows whose y-part is empty
-        are omitted; the y^0 column C[i, 0] is handled by _outer)."""
-        e = self.e
-        out = {}
-        for i in rows:
-            js = [j for j in range(1, 16) if _nz(C[i, j]) and j in ybasis]
-            if js:
-                out[i] = e.lincomb([ybasis[j] for j in js], [C[i, j] for j in js])
-        return out
+        """L_i(y) = sum_{j>=1} C[i, j] y^j for the requested rows, all rows in one fused pass over
+        the basis (engine.lincomb_many); rows whose y-part is empty are omitted (the y^0 column
+        C[i, 0] is handled by _outer)."""
+        js = sorted(j for j in ybasis if j >= 1)
+        rows = [i for i in rows if any(_nz(C[i, j]) for j in js)]
+        if not rows:
+            return {}
+        M = np.array([[C[i, j] for j in js] for i in rows], dtype=np.complex128)
+        outs = self.e.lincomb_many([ybasis[j] for j in js], M)
+        return dict(zip(rows, outs))
 
     def _xor_inner(self, ybasis):
         rows = [i for i in range(1, 16, 2)]

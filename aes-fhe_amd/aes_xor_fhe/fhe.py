@@ -441,6 +441,19 @@ class Engine:
         return self._call_ct(self._lib.lincomb, arr, n, _as_ptr(re, C.c_double),
                              _as_ptr(im, C.c_double))
 
+    def lincomb_many(self, cts: Sequence[Ciphertext], coeffs) -> list:
+        """Rows of a (m, n) coefficient matrix applied to the same n ciphertexts in one pass."""
+        n = len(cts)
+        M = np.ascontiguousarray(np.asarray(coeffs, dtype=np.complex128).reshape(-1, n))
+        m = M.shape[0]
+        arr = (c_ct_p * n)(*[c._h for c in cts])
+        re = np.ascontiguousarray(M.real)
+        im = np.ascontiguousarray(M.imag)
+        outs = (c_ct_p * m)()
+        self._check(self._lib.lincomb_many(self._h, arr, n, _as_ptr(re, C.c_double),
+                                           _as_ptr(im, C.c_double), m, outs))
+        return [self._ct(outs[i]) for i in range(m)]
+
     def dot(self, a: Sequence[Ciphertext], b: Sequence[Ciphertext],
             relinearization_key: RelinearizationKey) -> Ciphertext:
         n = len(a)

@@ -2,7 +2,7 @@
 // deterministic prime chain, root selection, the counter-based PRNG (also used on device)
 // and the canonical-embedding codec.  Every integer / floating-point choice here follows the
 // specification in DESIGN.md section 3, which the CPU oracle (oracle/ckks_oracle.c) restates
-// independently; tests/test_codec_primes.py checks the two agree bit for bit.
+// independently; tests/test_abi.py checks the two agree bit for bit.
 #pragma once
 
 #include <cmath>

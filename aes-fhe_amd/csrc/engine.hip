@@ -991,6 +991,28 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in) {
     return r;
 }
 
+// rescale of a compact buffer holding G groups of Bg batch elements (np polys, level l) into G
+// new ciphertexts at level l-1 (one rescale pass for all groups)
+static std::vector<aesfhe_ct*> rescale_groups(aesfhe_engine* e, const u64* d, int G, int Bg, int np, int l) {
+    const int N = e->N, P = G * Bg * np;
+    std::vector<aesfhe_ct*> outs(G);
+    for (int g = 0; g < G; g++) outs[g] = ct_new(e, Bg, np, l - 1);
+    Tmp x(e, (size_t)P * N), t(e, (size_t)P * l * N);
+    const long cps = (long)(l + 1) * N;
+    Span src = span_s((u64*)d + (long)l * N, cps, 1, 1, l, e->Lp1);
+    Span dx = span_s(x.p, N, 1, 1, l, e->Lp1);
+    ntt(e, src, dx, P, true);
+    hipLaunchKernelGGL(k_rescale_spread, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN);
+    Span st = span_s(t.p, (long)l * N, l, l, 0, e->Lp1);
+    ntt(e, st, st, P * l, false);
+    std::vector<u64*> op(G);
+    for (int g = 0; g < G; g++) op[g] = outs[g]->d;
+    auto dop = upload_small(e, op.data(), op.size());
+    hipLaunchKernelGGL(k_rescale_finish_g, dim3(N / 256, l, P), dim3(256), 0, e->stream, d, cps, (const u64*)t.p, (u64* const*)dop, (long)l * N, np, Bg, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN);
+    HIPC(hipGetLastError());
+    return outs;
+}
+
 // constant factor tables for A + B X^{N/2} over limbs 0..nl-1
 static void const_factors(aesfhe_engine* e, int64_t A, int64_t Bc, int nl, std::vector<u64>& f, std::vector<double>& ff) {
     f.resize(2 * nl);
@@ -1181,42 +1203,41 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
                       Opnd addend, aesfhe_ct* o) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long lN = (long)(l + 1) * N, neN = (long)ne * N;
-    Tmp dc(e, (size_t)B * lN), ext(e, (size_t)B * neN), acc(e, (size_t)B * 2 * neN);
+    const int beta = (l + 1 + K - 1) / K;
+    if (beta > 12) throw_err(AESFHE_EUNSUPPORTED, "more than 12 key-switch digits");
+    Tmp dc(e, (size_t)B * lN), ext(e, (size_t)beta * B * neN), acc(e, (size_t)B * 2 * neN);
     // 1. INTT copy of the input
     Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1), sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
     ntt(e, sd, sdc, B * (l + 1), true);
-    const int beta = (l + 1 + K - 1) / K;
     for (int j = 0; j < beta; j++) {
         const int lo = j * K, hi = std::min(lo + K, l + 1), alpha = hi - lo;
         const size_t set = (size_t)j * K + (alpha - 1);
-        // 2. ModUp base conversion to every other limb, then NTT those limbs
+        u64* exj = ext.p + (size_t)j * B * neN;
+        // 2. ModUp base conversion of digit j to every other limb, then NTT those limbs
         {
-        ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
-        hipLaunchKernelGGL(k_modup, dim3(N / 256, (ne + 7) / 8, B), dim3(256), 0, e->stream, (const u64*)dc.p, lN, ext.p, neN, lo, alpha, l, ne,
-                           (const u64*)(e->mu_hatinv + set * K), (const double*)(e->mu_hatinvf + set * K),
-                           (const u64*)(e->mu_hat + set * K * e->np), (const double*)(e->mu_hatf + set * K * e->np),
-                           e->np, e->q, e->Lp1, e->logN);
+            ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
+            hipLaunchKernelGGL(k_modup, dim3(N / 256, (ne + 7) / 8, B), dim3(256), 0, e->stream, (const u64*)dc.p, lN, exj, neN, lo, alpha, l, ne,
+                               (const u64*)(e->mu_hatinv + set * K), (const double*)(e->mu_hatinvf + set * K),
+                               (const u64*)(e->mu_hat + set * K * e->np), (const double*)(e->mu_hatf + set * K * e->np),
+                               e->np, e->q, e->Lp1, e->logN);
         }
         HIPC(hipGetLastError());
-        // NTT of targets: limbs [0, lo) and [hi, ne) of every batch element
         if (lo > 0) {
-            Span s1 = span_s(ext.p, neN, lo, lo, 0, e->Lp1);
+            Span s1 = span_s(exj, neN, lo, lo, 0, e->Lp1);
             ntt(e, s1, s1, B * lo, false);
         }
         {
             int nrest = ne - hi, nq_rest = (l + 1) - hi;
-            Span s2 = span_s(ext.p + (long)hi * N, neN, nrest, nq_rest, hi, e->Lp1);
+            Span s2 = span_s(exj + (long)hi * N, neN, nrest, nq_rest, hi, e->Lp1);
             ntt(e, s2, s2, B * nrest, false);
         }
-        // 3. inner product with the key digit
-        const u64* kb = k->d + ((size_t)j * 2 + 0) * e->np * N;
-        const u64* ka = k->d + ((size_t)j * 2 + 1) * e->np * N;
-        {
-        ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (B + 2 + (j == 0 ? 2 : 4) * B));
-        hipLaunchKernelGGL(k_ks_inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, (const u64*)ext.p, neN, kb, ka, acc.p, 2 * neN, neN, B, lo, hi, l, e->q, e->qinv, e->Lp1, j == 0 ? 1 : 0, e->logN);
-        }
-        HIPC(hipGetLastError());
     }
+    // 3. inner product with every key digit in one pass
+    {
+        ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B));
+        hipLaunchKernelGGL(k_ks_inner_all, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, (const u64*)ext.p, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, e->logN);
+    }
+    HIPC(hipGetLastError());
     // 4. ModDown: INTT special limbs of both accumulators
     {
         Span ssp = span_s(acc.p + lN, neN, K, 0, 0, e->Lp1);
@@ -1224,9 +1245,9 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
     }
     Tmp conv(e, (size_t)B * 2 * lN);
     {
-    ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + l + 1));
-    hipLaunchKernelGGL(k_moddown, dim3(N / 256, (l + 1 + 7) / 8, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, conv.p, 2 * lN, lN, K,
-                       (const u64*)e->md_phatinv, (const double*)e->md_phatinvf, (const u64*)e->md_phat, (const double*)e->md_phatf, e->Lp1, e->q, e->logN);
+        ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + l + 1));
+        hipLaunchKernelGGL(k_moddown, dim3(N / 256, (l + 1 + 7) / 8, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, conv.p, 2 * lN, lN, K,
+                           (const u64*)e->md_phatinv, (const double*)e->md_phatinvf, (const u64*)e->md_phat, (const double*)e->md_phatf, e->Lp1, e->q, e->logN);
     }
     HIPC(hipGetLastError());
     {
@@ -1425,6 +1446,89 @@ extern "C" int aesfhe_lincomb(aesfhe_engine* e, const aesfhe_ct* const* cts, int
         *out = rescale_view(e, view_of(acc));
         aesfhe_ct_free(acc);
     }
+    API_END
+}
+
+extern "C" int aesfhe_lincomb_many(aesfhe_engine* e, const aesfhe_ct* const* cts, int32_t n, const double* re, const double* im, int32_t m, aesfhe_ct** outs) {
+    if (n > kManyMax || m < 1) {
+        for (int r = 0; r < m; r++) {
+            int rc = aesfhe_lincomb(e, cts, n, re + (size_t)r * n, im + (size_t)r * n, &outs[r]);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    API_BEGIN
+    if (n < 1) throw_err(AESFHE_EARG, "empty linear combination");
+    int l = cts[0]->level, B = 1, np = 2;
+    for (int i = 0; i < n; i++) {
+        l = std::min(l, cts[i]->level);
+        B = std::max(B, cts[i]->B);
+        np = std::max(np, cts[i]->np);
+    }
+    for (int i = 0; i < n; i++)
+        if (cts[i]->B != B && cts[i]->B != 1) throw_err(AESFHE_EARG, "batch mismatch");
+    if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a linear combination");
+    const int nl = l + 1;
+    const double s = aesfhe_engine_mul_scale(e, l);
+    // rows whose constants all round to zero (or whose inputs are all zero) are zero outputs
+    std::vector<int> live;
+    std::vector<char> used(n, 0);
+    for (int r = 0; r < m; r++) {
+        bool any = false;
+        for (int i = 0; i < n; i++) {
+            int64_t A = llround(re[(size_t)r * n + i] * s), Bc = llround(im[(size_t)r * n + i] * s);
+            if (!cts[i]->is_zero && (A || Bc)) any = true, used[i] = 1;
+        }
+        if (any) live.push_back(r);
+        else outs[r] = nullptr;
+    }
+    std::vector<int> cols;
+    for (int i = 0; i < n; i++)
+        if (used[i]) cols.push_back(i);
+    std::vector<std::unique_ptr<Aligned>> al;
+    std::vector<const u64*> ptrs;
+    std::vector<long> bstr;
+    std::vector<int> npi;
+    for (int i : cols) {
+        al.emplace_back(new Aligned());
+        align_to(e, cts[i], l, *al.back());
+        const View& v = al.back()->v;
+        ptrs.push_back(v.d);
+        bstr.push_back(v.B == 1 && B > 1 ? 0 : v.bs);
+        npi.push_back(v.np);
+    }
+    const int nc = (int)cols.size(), ml = (int)live.size();
+    if (ml > 0) {
+        std::vector<u64> F((size_t)ml * nc * nl * 2);
+        std::vector<double> FF(F.size());
+        for (int r = 0; r < ml; r++)
+            for (int c = 0; c < nc; c++) {
+                const size_t idx = (size_t)live[r] * n + cols[c];
+                int64_t A = llround(re[idx] * s), Bc = llround(im[idx] * s);
+                if (cts[cols[c]]->is_zero) A = Bc = 0;
+                std::vector<u64> fi;
+                std::vector<double> ffi;
+                const_factors(e, A, Bc, nl, fi, ffi);
+                std::copy(fi.begin(), fi.end(), F.begin() + ((size_t)r * nc + c) * nl * 2);
+                std::copy(ffi.begin(), ffi.end(), FF.begin() + ((size_t)r * nc + c) * nl * 2);
+            }
+        const long ps = (long)nl * e->N, obs = (long)np * ps, orow = (long)B * obs;
+        Tmp acc(e, (size_t)ml * orow);
+        auto dp = upload_small(e, ptrs.data(), ptrs.size());
+        auto db = upload_small(e, bstr.data(), bstr.size());
+        auto dn = upload_small(e, npi.data(), npi.size());
+        auto dF = upload_small(e, F.data(), F.size());
+        auto dFF = upload_small(e, FF.data(), FF.size());
+        {
+            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (nc + ml));
+            hipLaunchKernelGGL(k_lincomb_many, ew_grid(e, nl, B * np), dim3(256), 0, e->stream, (const u64* const*)dp, (const long*)db, (const int*)dn, nc, ps, (const u64*)dF, (const double*)dFF, ml, acc.p, orow, obs, np, nl, e->q, e->qinv, e->logN);
+        }
+        HIPC(hipGetLastError());
+        std::vector<aesfhe_ct*> res = rescale_groups(e, acc.p, ml, B, np, l);
+        for (int r = 0; r < ml; r++) outs[live[r]] = res[r];
+    }
+    for (int r = 0; r < m; r++)
+        if (!outs[r]) outs[r] = ct_zero_new(e, B, np, l - 1);
     API_END
 }
 

@@ -134,6 +134,38 @@ __global__ void k_lincomb(const u64* const* __restrict__ ptrs, const long* __res
     o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)l << logN) + k] = red_m(acc, q, qinv[l]);
 }
 
+// m linear combinations of the same n <= 16 aligned inputs in one pass.  F/FF: [m][n][nl][2]
+// (row-uniform factors -> scalar loads).  out: [m][B][np][nl][N].  grid (N/256, nl, B*np)
+constexpr int kManyMax = 16;
+__global__ void k_lincomb_many(const u64* const* __restrict__ ptrs, const long* __restrict__ bstr,
+                               const int* __restrict__ npi, int n, long ps,
+                               const u64* __restrict__ F, const double* __restrict__ FF, int m,
+                               u64* __restrict__ out, long orow, long obs, int np, int nl,
+                               const u64* __restrict__ qs, const double* __restrict__ qinv,
+                               int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z / np, p = blockIdx.z - bb * np;
+    const u64 q = qs[l];
+    const int h = k >> (logN - 1);
+    const long off = (long)p * ps + ((long)l << logN) + k;
+    u64 v[kManyMax];
+#pragma unroll
+    for (int j = 0; j < kManyMax; j++)
+        v[j] = (j < n && p < npi[j]) ? ptrs[j][(long)bb * bstr[j] + off] : 0;
+    u64* o = out + (long)bb * obs + off;
+    for (int i = 0; i < m; i++) {
+        u64 acc = 0;
+#pragma unroll
+        for (int j = 0; j < kManyMax; j++) {
+            if (j < n) {
+                const int fi = ((i * n + j) * nl + l) * 2 + h;
+                acc += mulw(v[j], F[fi], FF[fi], q);
+            }
+        }
+        o[(long)i * orow] = red_m(acc, q, qinv[l]);
+    }
+}
+
 // Fused dot product: (d0,d1,d2) = sum_i a_i (x) b_i (one pass).  a/b pointer + batch-stride
 // arrays [n]; inputs compact 2-poly ciphertexts at the same level (poly stride ps).
 // grid (N/256, nl, B)
@@ -191,6 +223,20 @@ __global__ void k_rescale_finish(Opnd c, const u64* __restrict__ t, Out o, int n
     u64 cv = opnd_get(c, bb, p, i, k, logN);
     u64 tv = t[(((long)P * l + i) << logN) + k];
     o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)i << logN) + k] = mul_w(sub_m(cv, tv, q), inv[i], invf[i], q);
+}
+
+// rescale finish writing to per-group output ciphertexts: P = (g*Bg + b)*np + p
+__global__ void k_rescale_finish_g(const u64* __restrict__ c, long cps, const u64* __restrict__ t,
+                                   u64* const* __restrict__ outs, long ops, int np, int Bg, int l,
+                                   const u64* __restrict__ qs, const u64* __restrict__ inv,
+                                   const double* __restrict__ invf, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y, P = blockIdx.z;
+    const int g = P / (Bg * np), rem = P - g * Bg * np;
+    const u64 q = qs[i];
+    u64 cv = c[(long)P * cps + ((long)i << logN) + k];
+    u64 tv = t[(((long)P * l + i) << logN) + k];
+    outs[g][(long)rem * ops + ((long)i << logN) + k] = mul_w(sub_m(cv, tv, q), inv[i], invf[i], q);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -252,6 +298,46 @@ __global__ void k_ks_inner(const u64* __restrict__ d, long dbs, const u64* __res
             *a0 = add_m(*a0, m0, q);
             *a1 = add_m(*a1, m1, q);
         }
+    }
+}
+
+// All digits at once: acc[b][c][t] = sum_j e_j[b][t] * key_j,c[pid(t)], e_j = d (limbs of digit
+// j, NTT) or ext_j (other limbs).  key layout [dnum][2][np][N]; ext layout [beta][B][ne][N].
+// grid (N/256, ne, 1); loops over the batch so each key word is read once per batch.
+__global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* __restrict__ ext,
+                               long exs, long exj, const u64* __restrict__ key, long kdig,
+                               long kcomp, u64* __restrict__ acc, long abs_, long acs, int B,
+                               int beta, int K, int l, const u64* __restrict__ qall,
+                               const double* __restrict__ qinvall, int Lp1, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.y;
+    const int pid = t <= l ? t : Lp1 + (t - l - 1);
+    const u64 q = qall[pid];
+    const double qi = qinvall[pid];
+    const int own = t <= l ? t / K : -1;  // the digit whose limbs include t (Q limbs only)
+    u64 kb[12], ka[12];
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        if (j < beta) {
+            const long ko = (long)j * kdig + ((long)pid << logN) + k;
+            kb[j] = key[ko];
+            ka[j] = key[ko + kcomp];
+        }
+    }
+    for (int bb = 0; bb < B; bb++) {
+        u64 s0 = 0, s1 = 0;
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+            if (j < beta) {
+                const u64 e = (j == own) ? d[(long)bb * dbs + ((long)t << logN) + k]
+                                         : ext[(long)j * exj + (long)bb * exs + ((long)t << logN) + k];
+                s0 += mul_m(e, kb[j], q, qi);
+                s1 += mul_m(e, ka[j], q, qi);
+            }
+        }
+        u64* a0 = acc + (long)bb * abs_ + ((long)t << logN) + k;
+        a0[0] = red_m(s0, q, qi);
+        a0[acs] = red_m(s1, q, qi);
     }
 }
 

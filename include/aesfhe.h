@@ -201,6 +201,10 @@ int aesfhe_power_basis(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t d,
 /* sum_i (re_i + i*im_i) * cts[i], aligned to the lowest input level, output at that - 1 */
 int aesfhe_lincomb(aesfhe_engine *eng, const aesfhe_ct *const *cts, int32_t n,
                    const double *re, const double *im, aesfhe_ct **out);
+/* m linear combinations of the same n inputs in one pass: outs[r] = lincomb(cts, re/im row r)
+ * (re, im row-major [m][n]); bit-identical to m separate aesfhe_lincomb calls. */
+int aesfhe_lincomb_many(aesfhe_engine *eng, const aesfhe_ct *const *cts, int32_t n,
+                        const double *re, const double *im, int32_t m, aesfhe_ct **outs);
 /* sum_i a_i (*) b_i, one relinearisation + one rescale for the whole sum */
 int aesfhe_dot(aesfhe_engine *eng, const aesfhe_ct *const *a, const aesfhe_ct *const *b,
                int32_t n, const aesfhe_key *rlk, aesfhe_ct **out);

@@ -1490,6 +1490,15 @@ int aesfhe_lincomb(aesfhe_engine *e, const aesfhe_ct *const *cts, int32_t n, con
     return 0;
 }
 
+int aesfhe_lincomb_many(aesfhe_engine *e, const aesfhe_ct *const *cts, int32_t n, const double *re,
+                        const double *im, int32_t m, aesfhe_ct **outs) {
+    for (int r = 0; r < m; r++) {
+        int rc = aesfhe_lincomb(e, cts, n, re + (size_t)r * n, im + (size_t)r * n, &outs[r]);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
 int aesfhe_dot(aesfhe_engine *e, const aesfhe_ct *const *a, const aesfhe_ct *const *b, int32_t n,
                const aesfhe_key *rlk, aesfhe_ct **out) {
     if (n < 1) return fail(AESFHE_EARG, "empty dot product");

@@ -94,6 +94,9 @@ def test_ops_bit_exact(product_lib, oracle_lib, gpu_available):
         _same(g, o, a, b)
     coeffs = [0.5, 0.25j, -1.0, 2.0 + 1j]
     _same(g, o, g.lincomb(pg[:4], coeffs), o.lincomb(po[:4], coeffs))
+    M = np.array([coeffs, [0, 0, 0, 0], [1j, -0.5, 0.125, 0.3 - 0.7j]])
+    for a, b in zip(g.lincomb_many(pg[:4], M), o.lincomb_many(po[:4], M)):
+        _same(g, o, a, b)
     _same(g, o, g.dot(pg[:3], pg[1:4], kg["rlk"]), o.dot(po[:3], po[1:4], ko["rlk"]))
     # mixed levels: add aligns by exact-scale level-down
     _same(g, o, g.add(pg[7], cg), o.add(po[7], co))
