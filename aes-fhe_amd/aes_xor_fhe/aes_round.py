@@ -249,9 +249,25 @@ class AESRoundEngine:
         return (self._outer(self.odd_basis(h), key.inner_hi),
                 self._outer(self.odd_basis(l), key.inner_lo))
 
-    def round(self, h: Ciphertext, l: Ciphertext, key: RoundKey):
-        """SubBytes -> ShiftRows -> MixColumns -> AddRoundKey (a middle AES-128 round)."""
+    def round(self, h: Ciphertext, l: Ciphertext, key: RoundKey, timings: dict | None = None):
+        """SubBytes -> ShiftRows -> MixColumns -> AddRoundKey (a middle AES-128 round).
+        With `timings`, the engine is synchronised after each step and wall times recorded."""
+        import time
+
+        def mark(name, t0):
+            if timings is not None:
+                self.e.synchronize()
+                t1 = time.perf_counter()
+                timings[name] = timings.get(name, 0.0) + (t1 - t0)
+                return t1
+            return t0
+        t = mark("start", 0.0) if timings is not None else 0.0
         sh, sl = self.sub_bytes(h, l)
+        t = mark("sub_bytes", t)
         th, tl = self.shift_mix_terms(sh), self.shift_mix_terms(sl)
+        t = mark("shift_rows_terms", t)
         mh, ml = self.mix_columns(th, tl)
-        return self.add_round_key(mh, ml, key)
+        t = mark("mix_columns", t)
+        out = self.add_round_key(mh, ml, key)
+        mark("add_round_key", t)
+        return out

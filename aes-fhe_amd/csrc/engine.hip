@@ -557,8 +557,8 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
     if (pp->max_level < 1 || pp->special_primes < 1 || pp->special_primes > 16 ||
         pp->max_level + 1 + pp->special_primes > kMaxPrimes)
         throw_err(AESFHE_EARG, "bad level / special prime count");
-    if (pp->scale_bits < 20 || pp->scale_bits > 50 || pp->base_bits > 51 || pp->special_bits > 51)
-        throw_err(AESFHE_EARG, "bit sizes must keep every prime below 2^51");
+    if (pp->scale_bits < 20 || pp->scale_bits > 50 || pp->base_bits > 50 || pp->special_bits > 50)
+        throw_err(AESFHE_EARG, "bit sizes must keep every prime below 2^50");
     std::unique_ptr<aesfhe_engine> e(new aesfhe_engine());
     e->logN = pp->log_n;
     e->N = 1 << pp->log_n;
@@ -575,8 +575,8 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
     } else {
         e->chain = make_chain(e->logN, e->L, e->K, pp->base_bits, pp->special_bits, pp->scale_bits);
     }
-    for (u64 x : e->chain.q)
-        if (x >> 51) throw_err(AESFHE_EARG, "prime %llu exceeds 2^51", (unsigned long long)x);
+    for (u64 x : e->chain.q)  // lazy NTT keeps values < 4q, which must stay below 2^52
+        if (x >> 50) throw_err(AESFHE_EARG, "prime %llu exceeds 2^50", (unsigned long long)x);
     HIPC(hipSetDevice(e->device));
     HIPC(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     build_tables(e.get());

@@ -30,6 +30,41 @@ __device__ __forceinline__ void gs_bfly(u64& x, u64& y, u64 w, double wq, u64 q)
     y = mulw(d, w, wq, q);
 }
 
+// Lazy (Harvey) butterflies: every prime < 2^50 so values up to 4q stay below 2^52, the exact
+// range of the fp64 quotient trick.  CT: inputs [0, 4q) -> outputs [0, 4q); GS: [0, 2q) ->
+// [0, 2q).  Passes reduce to canonical [0, q) only where a transform ends.
+__device__ __forceinline__ void ct_lazy(u64& x, u64& y, u64 w, double wq, u64 q, u64 q2) {
+#ifdef NTT_NOCOMPUTE  // timing-only build (tools/ntt_bench.hip): keep the data flow, drop the math
+    x ^= w;
+    y ^= x;
+    return;
+#endif
+    const u64 qh = rint_u(u2d(y), wq);
+    const u64 v = y * w - qh * q + q;  // (0, 2q)
+    const u64 xr = x >= q2 ? x - q2 : x;  // [0, 2q)
+    x = xr + v;
+    y = xr - v + q2;
+}
+
+__device__ __forceinline__ void gs_lazy(u64& x, u64& y, u64 w, double wq, u64 q, u64 q2) {
+#ifdef NTT_NOCOMPUTE
+    x ^= w;
+    y ^= x;
+    return;
+#endif
+    u64 s = x + y;
+    s = s >= q2 ? s - q2 : s;         // [0, 2q)
+    const u64 d = x - y + q2;         // (0, 4q)
+    const u64 qh = rint_u(u2d(d), wq);
+    y = d * w - qh * q + q;           // (0, 2q)
+    x = s;
+}
+
+__device__ __forceinline__ u64 canon4(u64 x, u64 q, u64 q2) {  // [0, 4q) -> [0, q)
+    x = x >= q2 ? x - q2 : x;
+    return x >= q ? x - q : x;
+}
+
 constexpr int kPad = 17;  // LDS row stride (u64) of the 16 x 16 transpose tiles: kills conflicts
 
 // Forward, column pass: stages m = 1..128 on columns of stride 256.
@@ -42,7 +77,7 @@ __global__ __launch_bounds__(256) void k_ntt256_fwd_cols(Span src, Span dst, Tab
     u64* out = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
     const int tid = threadIdx.x, cl = tid & 15, b = tid >> 4;
     const int c = blockIdx.x * 16 + cl;
-    const u64 q = T.q[pid];
+    const u64 q = T.q[pid], q2 = 2 * q;
     const long toff = (long)pid << T.logN;
     const Tw* tg = T.tw + toff;
     tws[tid] = tg[tid];
@@ -58,7 +93,7 @@ __global__ __launch_bounds__(256) void k_ntt256_fwd_cols(Span src, Span dst, Tab
         for (int a = 0; a < 16; a++) {
             if (a & h) continue;
             const Tw t = tg[m + (a >> (4 - st))];  // uniform address: scalar load
-            ct_bfly(x[a], x[a + h], t.w, t.wq, q);
+            ct_lazy(x[a], x[a + h], t.w, t.wq, q, q2);
         }
     }
     // transpose: row r = a*16 + b, column cl
@@ -76,7 +111,7 @@ __global__ __launch_bounds__(256) void k_ntt256_fwd_cols(Span src, Span dst, Tab
         for (int bb = 0; bb < 16; bb++) {
             if (bb & h) continue;
             const Tw t = tws[m + ap * (m >> 4) + (bb >> (8 - st))];
-            ct_bfly(x[bb], x[bb + h], t.w, t.wq, q);
+            ct_lazy(x[bb], x[bb + h], t.w, t.wq, q, q2);
         }
     }
 #pragma unroll
@@ -91,7 +126,7 @@ __global__ __launch_bounds__(256) void k_ntt256_fwd_rows(Span dst, Tabs T) {
     u64* io = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
     const int tid = threadIdx.x, b = tid & 15, rl = tid >> 4;
     const int row = blockIdx.x * 16 + rl;
-    const u64 q = T.q[pid];
+    const u64 q = T.q[pid], q2 = 2 * q;
     const long toff = (long)pid << T.logN;
     const Tw* W = T.tw + toff;
     u64* rp = io + (long)row * 256;
@@ -107,7 +142,7 @@ __global__ __launch_bounds__(256) void k_ntt256_fwd_rows(Span dst, Tabs T) {
         for (int a = 0; a < 16; a++) {
             if (a & h) continue;
             const Tw t = W[base + (a >> (4 - st))];
-            ct_bfly(x[a], x[a + h], t.w, t.wq, q);
+            ct_lazy(x[a], x[a + h], t.w, t.wq, q, q2);
         }
     }
     u64* sr = s + rl * 16 * kPad;
@@ -125,12 +160,12 @@ __global__ __launch_bounds__(256) void k_ntt256_fwd_rows(Span dst, Tabs T) {
         for (int bb = 0; bb < 16; bb++) {
             if (bb & h) continue;
             const Tw t = W[base + (bb >> (8 - st))];
-            ct_bfly(x[bb], x[bb + h], t.w, t.wq, q);
+            ct_lazy(x[bb], x[bb + h], t.w, t.wq, q, q2);
         }
     }
     // coalesced store through LDS: lane writes back its 16 elements, then row-major copy-out
 #pragma unroll
-    for (int bb = 0; bb < 16; bb++) sr[ap * kPad + bb] = x[bb];
+    for (int bb = 0; bb < 16; bb++) sr[ap * kPad + bb] = canon4(x[bb], q, q2);
     __syncthreads();
     u64* base = io + (long)blockIdx.x * 16 * 256;
 #pragma unroll
@@ -148,7 +183,7 @@ __global__ __launch_bounds__(256) void k_ntt256_inv_rows(Span src, Span dst, Tab
     u64* out = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
     const int tid = threadIdx.x, b = tid & 15, rl = tid >> 4;
     const int row = blockIdx.x * 16 + rl;
-    const u64 q = T.q[pid];
+    const u64 q = T.q[pid], q2 = 2 * q;
     const long toff = (long)pid << T.logN;
     const Tw* W = T.itw + toff;
     const int N = 1 << T.logN;
@@ -174,7 +209,7 @@ __global__ __launch_bounds__(256) void k_ntt256_inv_rows(Span src, Span dst, Tab
         for (int bb = 0; bb < 16; bb++) {
             if (bb & t) continue;
             const Tw w = W[base + (bb >> (st + 1))];
-            gs_bfly(x[bb], x[bb + t], w.w, w.wq, q);
+            gs_lazy(x[bb], x[bb + t], w.w, w.wq, q, q2);
         }
     }
 #pragma unroll
@@ -191,7 +226,7 @@ __global__ __launch_bounds__(256) void k_ntt256_inv_rows(Span src, Span dst, Tab
         for (int a = 0; a < 16; a++) {
             if (a & ta) continue;
             const Tw w = W[base + (a >> (st - 3))];
-            gs_bfly(x[a], x[a + ta], w.w, w.wq, q);
+            gs_lazy(x[a], x[a + ta], w.w, w.wq, q, q2);
         }
     }
     u64* op = out + (long)row * 256;
@@ -207,7 +242,7 @@ __global__ __launch_bounds__(256) void k_ntt256_inv_cols(Span dst, Tabs T) {
     u64* io = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
     const int tid = threadIdx.x, cl = tid & 15, b = tid >> 4;
     const int c = blockIdx.x * 16 + cl;
-    const u64 q = T.q[pid];
+    const u64 q = T.q[pid], q2 = 2 * q;
     const long toff = (long)pid << T.logN;
     const Tw* tg = T.itw + toff;
     tws[tid] = tg[tid];
@@ -226,7 +261,7 @@ __global__ __launch_bounds__(256) void k_ntt256_inv_cols(Span dst, Tabs T) {
         for (int bb = 0; bb < 16; bb++) {
             if (bb & tr) continue;
             const Tw w = tws[base + (bb >> (st + 1))];
-            gs_bfly(x[bb], x[bb + tr], w.w, w.wq, q);
+            gs_lazy(x[bb], x[bb + tr], w.w, w.wq, q, q2);
         }
     }
 #pragma unroll
@@ -243,7 +278,7 @@ __global__ __launch_bounds__(256) void k_ntt256_inv_cols(Span dst, Tabs T) {
         for (int a = 0; a < 16; a++) {
             if (a & ta) continue;
             const Tw w = tg[base + (a >> (st - 3))];  // uniform: scalar load
-            gs_bfly(x[a], x[a + ta], w.w, w.wq, q);
+            gs_lazy(x[a], x[a + ta], w.w, w.wq, q, q2);
         }
     }
     const u64 ni = T.ninv[pid];

@@ -3,10 +3,11 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
 
-One *step* = one full middle AES-128 round (SubBytes -> ShiftRows -> MixColumns ->
-AddRoundKey, aes_xor_fhe.aes_round.AESRoundEngine) over a batch of B ciphertext pairs at
-N = 2^16, L = 30; each pair carries 2048 AES blocks, so a step processes B * 2048 blocks per
-GPU.  Inputs (encrypted synthetic random AES states) and the encrypted round key are resident
+One *step* = one full middle AES-128 round (ShiftRows -> SubBytes -> MixColumns ->
+AddRoundKey) at N = 2^16, L = 30 over a batch of B ciphertext sets per GPU.  Default layout
+"rows" (aes_xor_fhe.aes_round_bits.AESRowRound): a set is 4 state rows x (hi, lo) Zeta-16
+nibble ciphertexts carrying 8192 AES blocks; layout "bytes" (aes_xor_fhe.aes_round.
+AESRoundEngine): a set is one byte-major (hi, lo) pair carrying 2048 blocks.  Inputs (encrypted synthetic random AES states) and the encrypted round key are resident
 in HBM before the timed region; the key-side XOR polynomials are precomputed once per key.
 
 Multi-GPU (torchrun, one process per GPU): every rank runs its own shard of ciphertexts --
@@ -43,7 +44,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=8, help="ciphertext pairs per GPU per step")
+    ap.add_argument("--batch", type=int, default=4, help="ciphertext sets per GPU per step")
+    ap.add_argument("--layout", choices=("rows", "bytes"), default="rows")
     ap.add_argument("--log-n", type=int, default=16)
     ap.add_argument("--max-level", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -51,24 +53,56 @@ def parse():
     return ap.parse_args()
 
 
+class RoundDriver:
+    """Uniform face over the two round implementations: encrypt / step / decrypt."""
+
+    def __init__(self, layout, eng, sk, pk, rlk, cjk, rotation_keys=None):
+        if layout == "rows":
+            from aes_xor_fhe.aes_round_bits import AESRowRound
+            self.R = AESRowRound(eng, sk, pk, rlk, cjk, rotation_keys=rotation_keys)
+        else:
+            from aes_xor_fhe.aes_round import AESRoundEngine
+            self.R = AESRoundEngine(eng, sk, pk, rlk, cjk, rotation_keys=rotation_keys)
+        self.layout = layout
+        self.n_blk = self.R.n_blk
+
+    def encrypt(self, blocks):
+        st = self.R.encrypt_blocks(blocks)
+        return st if self.layout == "rows" else tuple(st)
+
+    def key(self, rk):
+        return self.R.encrypt_round_key(rk)
+
+    def round(self, st, key):
+        return self.R.round(st, key) if self.layout == "rows" else self.R.round(st[0], st[1], key)
+
+    def sub_bytes(self, st):
+        """Bounded CPU sample: SubBytes of the first nibble pair only."""
+        if self.layout == "rows":
+            h, l = st[0]
+            return self.R.lut2_bits(self.R.full_basis(h), self.R.full_basis(l))
+        return self.R.sub_bytes(st[0], st[1])
+
+    def decrypt(self, st):
+        return self.R.decrypt_blocks(st) if self.layout == "rows" else self.R.decrypt_blocks(*st)
+
+
 def setup_engine(args, device):
     from aes_xor_fhe.fhe import Engine
-    from aes_xor_fhe.aes_round import AESRoundEngine
     eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=8, device_id=device)
     sk = eng.create_secret_key(1)
     pk = eng.create_public_key(sk)
     rlk = eng.create_relinearization_key(sk)
     cjk = eng.create_conjugation_key(sk)
-    R = AESRoundEngine(eng, sk, pk, rlk, cjk)
-    return eng, R
+    return eng, RoundDriver(args.layout, eng, sk, pk, rlk, cjk)
 
 
 def cpu_baseline(args):
     """Oracle (CPU restatement) on a bounded sample of the same workload, scaled to blocks/s.
 
     The full round at N=2^16 takes minutes on the oracle, so the sample is: SubBytes of one
-    ciphertext pair at N=2^16, L=30 (timed), scaled by the oracle's own full-round/SubBytes
-    time ratio measured at N=2^12, L=30 on the same op sequence."""
+    (hi, lo) nibble pair at N=2^16, L=30 (timed), scaled by the oracle's own full-round/SubBytes
+    time ratio measured at N=2^12, L=30 on the same op sequence (same layout as the GPU run)."""
     sys.path.insert(0, str(ROOT / "tests"))
     import subprocess
     so = ROOT / "oracle" / "_build" / "liboracle_ckks.so"
@@ -76,8 +110,6 @@ def cpu_baseline(args):
         subprocess.run(["make", "-C", str(ROOT / "oracle")], check=True, stdout=subprocess.DEVNULL)
     from aes_xor_fhe._abi import Lib
     from aes_xor_fhe.fhe import Engine
-    from aes_xor_fhe.aes_round import AESRoundEngine
-    from aes_xor_fhe import aes_tables as T
     lib = Lib(so)
     threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
     times = {}
@@ -85,27 +117,26 @@ def cpu_baseline(args):
         eng = Engine(log_n=log_n, max_level=args.max_level, special_primes=8, thread_count=threads, _lib=lib)
         sk = eng.create_secret_key(1)
         pk = eng.create_public_key(sk)
-        R = AESRoundEngine(eng, sk, pk, eng.create_relinearization_key(sk),
-                           eng.create_conjugation_key(sk),
-                           rotation_keys={} if log_n != 12 else None)
+        R = RoundDriver(args.layout, eng, sk, pk, eng.create_relinearization_key(sk),
+                        eng.create_conjugation_key(sk),
+                        rotation_keys={} if log_n != 12 else None)
         rng = np.random.default_rng(log_n)
         blocks = rng.integers(0, 256, (1, R.n_blk, 16), dtype=np.uint8)
-        h, l = R.encrypt_blocks(blocks)
+        st = R.encrypt(blocks)
         t0 = time.perf_counter()
-        sh, sl = R.sub_bytes(h, l)
-        t_sb = time.perf_counter() - t0
-        times[(log_n, "sb")] = t_sb
+        R.sub_bytes(st)
+        times[(log_n, "sb")] = time.perf_counter() - t0
         if log_n == 12:
-            key = R.encrypt_round_key(rng.integers(0, 256, 16, dtype=np.uint8))
+            key = R.key(rng.integers(0, 256, 16, dtype=np.uint8))
             t0 = time.perf_counter()
-            R.round(h, l, key)
+            R.round(st, key)
             times[(log_n, "round")] = time.perf_counter() - t0
     ratio = times[(12, "round")] / times[(12, "sb")]
     est_round = times[(args.log_n, "sb")] * ratio
-    n_blk = (1 << (args.log_n - 1)) // 16
+    n_blk = (1 << (args.log_n - 1)) // (4 if args.layout == "rows" else 16)
     return {
         "value": n_blk / est_round, "unit": "blocks/s", "cores": threads, "kind": "port",
-        "sample": (f"oracle SubBytes of 1 ciphertext pair ({n_blk} blocks) at N=2^{args.log_n} "
+        "sample": (f"oracle SubBytes of 1 nibble pair ({args.layout} layout, {n_blk} blocks/set) at N=2^{args.log_n} "
                    f"L={args.max_level}: {times[(args.log_n, 'sb')]:.2f} s, scaled by the oracle's "
                    f"round/SubBytes ratio {ratio:.2f} measured at N=2^12 -> est. {est_round:.1f} s "
                    f"per round"),
@@ -132,12 +163,12 @@ def main():
     rng = np.random.default_rng(1000 + rank)
     blocks = rng.integers(0, 256, (args.batch, R.n_blk, 16), dtype=np.uint8)
     rk = np.random.default_rng(25073102).integers(0, 256, 16, dtype=np.uint8)
-    h, l = R.encrypt_blocks(blocks)
-    key = R.encrypt_round_key(rk)
+    st = R.encrypt(blocks)
+    key = R.key(rk)
     eng.synchronize()
 
     def step():
-        return R.round(h, l, key)
+        return R.round(st, key)
 
     for _ in range(args.warmup):
         out = step()
@@ -171,7 +202,7 @@ def main():
 
     ok = None
     if args.check:
-        got = R.decrypt_blocks(*out)
+        got = R.decrypt(out)
         ok = bool((got == T.aes_round(blocks, rk)).all())
 
     blocks_per_step = args.batch * R.n_blk * world
@@ -193,10 +224,13 @@ def main():
             "dtype": "u64",
             "data": "synthetic random AES states + random round key, encrypted",
             "config": {
-                "workload": "one full AES-128 middle round (SubBytes+ShiftRows+MixColumns+"
-                            "AddRoundKey), nibble-domain Zeta-16 LUTs, byte-major SIMD packing",
+                "workload": ("one full AES-128 middle round (ShiftRows+SubBytes+MixColumns+"
+                             "AddRoundKey): " + ("row-sliced state, Zeta-16 nibble S-box LUTs to "
+                             "+-1 bits, bit-domain MixColumns/AddRoundKey" if args.layout == "rows"
+                             else "nibble-domain Zeta-16 LUTs, byte-major SIMD packing")),
+                "layout": args.layout,
                 "log_n": args.log_n, "max_level": args.max_level, "special_primes": 8,
-                "ciphertext_pairs_per_gpu": args.batch, "blocks_per_gpu_per_step": args.batch * R.n_blk,
+                "ciphertext_sets_per_gpu": args.batch, "blocks_per_gpu_per_step": args.batch * R.n_blk,
                 "parallelism": f"ciphertext-batch sharding x{world} (no data-path collective)",
                 "verified": ok,
             },
