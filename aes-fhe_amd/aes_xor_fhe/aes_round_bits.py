@@ -10,7 +10,7 @@ xor_service.py:245-286 / sbox_service.py:116-138, slot rotations as in shiftrows
   with SubBytes it is applied to the nibble inputs (6 rotations per 8192 blocks).
 * SubBytes -- from the Zeta-16 nibble pair (h, l) straight to the 8 output bits in the +-1
   encoding B_j = (-1)^{bit_j}: eight 2-D LUT polynomials sharing the power bases of h and l
-  (baby-step giant-step; inner sums fused in one engine.lincomb_many, one engine.dot per bit).
+  (one fused Engine.poly2 call: inner sums never rescaled, one relinearisation per bit).
 * MixColumns -- in the +-1 encoding XOR is multiplication.  With a_r the SubBytes bytes of row
   r: out_r = xtime(a_r ^ a_{r+1}) ^ a_r ^ t, t = a_0 ^ a_1 ^ a_2 ^ a_3.  Per bit j:
   U_rj = A_rj A_{r+1,j}; T_j = U_0j U_2j; xtime(u)_j = u_{j-1} (j = 0: u_7), times u_7 for
@@ -36,9 +36,6 @@ ZETA16 = np.exp(-2j * np.pi / 16)
 XT_OF = {0: (7, False), 1: (0, True), 2: (1, False), 3: (2, True), 4: (3, True), 5: (4, False),
          6: (5, False), 7: (6, False)}  # xtime bit j = u[src] (* u[7] if flagged)
 
-
-def _nz(c: complex) -> bool:
-    return abs(c) > 1e-12
 
 
 class AESRowRound:
@@ -124,37 +121,10 @@ class AESRowRound:
         return self.e.multiply(a, b, self.rlk)
 
     def lut2_bits(self, hb, lb) -> List[Ciphertext]:
-        """The 8 S-box output bits from the bases of h and l: out_j = sum_i h^i L_ij(l) +
-        sum_i C_j[i,0] h^i, inner sums of all bits in one lincomb_many pass."""
-        e = self.e
-        js = sorted(k for k in lb if k >= 1)
-        rows, M = [], []
-        for bit, C in enumerate(self.C_bits):
-            for i in range(16):
-                if any(_nz(C[i, j]) for j in js):
-                    rows.append((bit, i))
-                    M.append([C[i, j] for j in js])
-        inner = e.lincomb_many([lb[j] for j in js], np.array(M, dtype=np.complex128))
-        lv = min(c.level for c in inner)
-        keys = sorted(hb)
-        hal = dict(zip(keys, e.align([hb[k] for k in keys], lv)))
-        outs = []
-        for bit, C in enumerate(self.C_bits):
-            terms = {i: inner[t] for t, (b2, i) in enumerate(rows) if b2 == bit}
-            ks = sorted(k for k in terms if k != 0)
-            parts = [e.dot([hal[k] for k in ks], [terms[k] for k in ks], self.rlk)]
-            if 0 in terms:
-                parts.append(terms[0])
-            cx = [k for k in range(1, 16) if _nz(C[k, 0])]
-            if cx:
-                parts.append(e.lincomb([hal[k] for k in cx], [C[k, 0] for k in cx]))
-            out = parts[0]
-            for p in parts[1:]:
-                out = e.add(out, p)
-            if _nz(C[0, 0]):
-                out = e.add(out, complex(C[0, 0]))
-            outs.append(out)
-        return outs
+        """The 8 S-box output bits from the power bases of h and l in one fused bivariate
+        evaluation (Engine.poly2): out_j = sum_{i,k} C_j[i,k] h^i l^k."""
+        C = np.stack(self.C_bits)
+        return self.e.poly2([hb[k] for k in range(1, 16)], [lb[k] for k in range(1, 16)], C, self.rlk)
 
     # ---- round steps ---------------------------------------------------------------------------
     def shift_rows(self, rows):

@@ -461,6 +461,26 @@ class Engine:
         bb = (c_ct_p * n)(*[c._h for c in b])
         return self._call_ct(self._lib.dot, aa, bb, n, relinearization_key._h)
 
+    def poly2(self, x_basis: Sequence[Ciphertext], y_basis: Sequence[Ciphertext], coeffs,
+              relinearization_key: RelinearizationKey) -> list:
+        """outs[t] = sum_{i,j} C[t, i, j] x^i y^j for C of shape (m, nx, ny), with
+        x_basis = [x^1..x^{nx-1}] and y_basis = [y^1..y^{ny-1}] (aesfhe_poly2: fused inner sums,
+        one relinearisation per output, two levels)."""
+        Cf = np.asarray(coeffs, dtype=np.complex128)
+        if Cf.ndim == 2:
+            Cf = Cf[None]
+        m, nx, ny = Cf.shape
+        if len(x_basis) != nx - 1 or len(y_basis) != ny - 1:
+            raise ValueError("poly2: basis lengths must be nx-1 and ny-1")
+        xa = (c_ct_p * max(nx - 1, 1))(*[c._h for c in x_basis])
+        ya = (c_ct_p * max(ny - 1, 1))(*[c._h for c in y_basis])
+        re = np.ascontiguousarray(Cf.real)
+        im = np.ascontiguousarray(Cf.imag)
+        outs = (c_ct_p * m)()
+        self._check(self._lib.poly2(self._h, xa, nx, ya, ny, _as_ptr(re, C.c_double),
+                                    _as_ptr(im, C.c_double), m, relinearization_key._h, outs))
+        return [self._ct(outs[i]) for i in range(m)]
+
     def align(self, cts: Sequence[Ciphertext], level: int | None = None) -> list:
         """Exact-scale level-down of every ciphertext to `level` (default: the lowest)."""
         level = min(c.level for c in cts) if level is None else level

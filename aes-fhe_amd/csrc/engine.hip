@@ -143,6 +143,8 @@ struct aesfhe_engine {
     char* ring_d = nullptr;
     char* ring_h = nullptr;
     size_t ring_size = 8u << 20, ring_off = 0;
+    // aesfhe_poly2 constant tables, keyed by (level, shape, coefficients)
+    std::map<std::string, Tw*> poly2_tabs;
     // profiling
     bool prof = false;
     std::vector<ProfRec> recs;
@@ -610,6 +612,7 @@ extern "C" void aesfhe_engine_destroy(aesfhe_engine* e) {
                     e->md_pinvf, e->rs_invf, e->ring_d, e->tw, e->itw};
     for (void* p : ptrs)
         if (p) hipFree(p);
+    for (auto& kv : e->poly2_tabs) hipFree(kv.second);
     if (e->ring_h) hipHostFree(e->ring_h);
     hipStreamDestroy(e->stream);
     delete e;
@@ -1581,6 +1584,130 @@ extern "C" int aesfhe_dot(aesfhe_engine* e, const aesfhe_ct* const* a, const aes
         *out = rescale_view(e, view_of(rl));
         aesfhe_ct_free(rl);
     }
+    API_END
+}
+
+// Bivariate polynomial with shared power bases (fused BSGS):
+//   out_t = sum_{i<nx, j<ny} C[t][i][j] x^i y^j,   xb = x^1..x^{nx-1}, yb = y^1..y^{ny-1}.
+// Constants carry the integer scale S1 = Delta_{l-2} q_l q_{l-1} / Delta_l^2 (x^0, y^0 terms
+// also R = round(Delta_l) per missing basis factor), so the inner sums are never rescaled: one
+// tensor pass (k_poly2), one batched relinearisation of all m*B outputs, then two rescales land
+// exactly on the canonical scale Delta_{l-2}.  Constant rules: oracle/ckks_oracle.c aesfhe_poly2.
+static Tw* poly2_table(aesfhe_engine* e, int l, int nx, int ny, int m, const std::vector<int64_t>& A,
+                       const std::vector<int64_t>& Bc, int64_t R) {
+    std::string key((const char*)&l, sizeof l);
+    key.append((const char*)&nx, sizeof nx).append((const char*)&ny, sizeof ny).append((const char*)&m, sizeof m);
+    key.append((const char*)A.data(), A.size() * 8).append((const char*)Bc.data(), Bc.size() * 8);
+    auto it = e->poly2_tabs.find(key);
+    if (it != e->poly2_tabs.end()) return it->second;
+    if (e->poly2_tabs.size() >= 256) {
+        HIPC(hipStreamSynchronize(e->stream));
+        for (auto& kv : e->poly2_tabs) HIPC(hipFree(kv.second));
+        e->poly2_tabs.clear();
+    }
+    const int nl = l + 1;
+    const size_t per = (size_t)m * nx * ny;
+    std::vector<Tw> T((size_t)nl * 2 * per);
+    for (int li = 0; li < nl; li++) {
+        const u64 q = e->chain.q[li];
+        const u64 r1 = h_smod(R, q), r2 = h_mulmod(r1, r1, q), I = e->h_iroot[li];
+        for (size_t c = 0; c < per; c++) {
+            const int j = (int)(c % ny), i = (int)((c / ny) % nx);
+            const u64 t = (i == 0 && j == 0) ? r2 : (i == 0 || j == 0) ? r1 : 1;
+            const u64 a = h_mulmod(h_smod(A[c], q), t, q), b = h_mulmod(h_smod(Bc[c], q), t, q);
+            const u64 bi = h_mulmod(b, I, q);
+            const u64 f0 = h_addmod(a, bi, q), f1 = h_submod(a, bi, q);
+            T[((size_t)li * 2 + 0) * per + c] = Tw{f0, (double)f0 / (double)q};
+            T[((size_t)li * 2 + 1) * per + c] = Tw{f1, (double)f1 / (double)q};
+        }
+    }
+    Tw* d = nullptr;
+    HIPC(hipMalloc(&d, T.size() * sizeof(Tw)));
+    HIPC(hipMemcpy(d, T.data(), T.size() * sizeof(Tw), hipMemcpyHostToDevice));
+    e->poly2_tabs.emplace(key, d);
+    return d;
+}
+
+extern "C" int aesfhe_poly2(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_t nx, const aesfhe_ct* const* yb, int32_t ny, const double* re, const double* im, int32_t m, const aesfhe_key* rlk, aesfhe_ct** outs) {
+    API_BEGIN
+    if (nx < 1 || ny < 1 || nx > kPoly2Max || ny > kPoly2Max || m < 1)
+        throw_err(AESFHE_EARG, "poly2 needs 1 <= nx, ny <= %d and m >= 1", kPoly2Max);
+    if (nx + ny < 3) throw_err(AESFHE_EARG, "poly2 needs at least one basis ciphertext");
+    if (!rlk || rlk->kind != 2) throw_err(AESFHE_EARG, "poly2 needs a relinearization key");
+    std::vector<const aesfhe_ct*> all;
+    for (int i = 0; i < nx - 1; i++) all.push_back(xb[i]);
+    for (int j = 0; j < ny - 1; j++) all.push_back(yb[j]);
+    int l = all[0]->level, B = 1;
+    for (auto* c : all) {
+        if (c->np != 2) throw_err(AESFHE_EDEGREE, "poly2 inputs should have 2 polynomials");
+        if (c->is_zero) throw_err(AESFHE_EARG, "poly2 basis ciphertext is zero");
+        l = std::min(l, c->level);
+        B = std::max(B, c->B);
+    }
+    for (auto* c : all)
+        if (c->B != B && c->B != 1) throw_err(AESFHE_EARG, "batch mismatch");
+    if (l < 2) throw_err(AESFHE_ELEVEL, "no level left for a bivariate polynomial");
+    const int nl = l + 1, N = e->N;
+    const double* D = e->chain.scale.data();
+    const double S1 = D[l - 2] / D[l] * ((double)e->chain.q[l] / D[l]) * (double)e->chain.q[l - 1];
+    const int64_t R = llround(D[l]);
+    const size_t per = (size_t)nx * ny;
+    std::vector<int> live;
+    std::vector<int64_t> A, Bc;
+    for (int t = 0; t < m; t++) {
+        bool any = false;
+        for (size_t c = 0; c < per; c++)
+            if (llround(re[t * per + c] * S1) || llround(im[t * per + c] * S1)) any = true;
+        if (!any) {
+            outs[t] = nullptr;
+            continue;
+        }
+        live.push_back(t);
+        for (size_t c = 0; c < per; c++) {
+            A.push_back(llround(re[t * per + c] * S1));
+            Bc.push_back(llround(im[t * per + c] * S1));
+        }
+    }
+    const int ml = (int)live.size();
+    if (ml > 0) {
+        std::vector<std::unique_ptr<Aligned>> al;
+        std::vector<const u64*> px, py;
+        std::vector<long> sx, sy;
+        for (size_t a = 0; a < all.size(); a++) {
+            al.emplace_back(new Aligned());
+            align_to(e, all[a], l, *al.back());
+            const View& v = al.back()->v;
+            if (v.ps != (long)nl * N) throw_err(AESFHE_EARG, "poly2: non-compact basis view");
+            const long bs = v.B == 1 && B > 1 ? 0 : v.bs;
+            if ((int)a < nx - 1) px.push_back(v.d), sx.push_back(bs);
+            else py.push_back(v.d), sy.push_back(bs);
+        }
+        if (px.empty()) px.push_back(nullptr), sx.push_back(0);
+        if (py.empty()) py.push_back(nullptr), sy.push_back(0);
+        const Tw* tab = poly2_table(e, l, nx, ny, ml, A, Bc, R);
+        auto dpx = upload_small(e, px.data(), px.size());
+        auto dpy = upload_small(e, py.data(), py.size());
+        auto dsx = upload_small(e, sx.data(), sx.size());
+        auto dsy = upload_small(e, sy.data(), sy.size());
+        const int Bt = ml * B;
+        const long obs = 3L * nl * N;
+        aesfhe_ct* d3 = ct_new(e, Bt, 3, l);
+        {
+            ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml));
+            for (int t0 = 0; t0 < ml; t0 += kPoly2Out)
+                hipLaunchKernelGGL(k_poly2, ew_grid(e, nl, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, nx, (const u64* const*)dpy, (const long*)dsy, ny, (long)nl * N, tab, ml, t0, std::min(kPoly2Out, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, e->logN);
+        }
+        HIPC(hipGetLastError());
+        aesfhe_ct* rl = relin_ct(e, d3, rlk);
+        aesfhe_ct_free(d3);
+        aesfhe_ct* r1 = rescale_view(e, view_of(rl));
+        aesfhe_ct_free(rl);
+        std::vector<aesfhe_ct*> res = rescale_groups(e, r1->d, ml, B, 2, l - 1);
+        aesfhe_ct_free(r1);
+        for (int t = 0; t < ml; t++) outs[live[t]] = res[t];
+    }
+    for (int t = 0; t < m; t++)
+        if (!outs[t]) outs[t] = ct_zero_new(e, B, 2, l - 2);
     API_END
 }
 

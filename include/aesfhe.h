@@ -208,6 +208,18 @@ int aesfhe_lincomb_many(aesfhe_engine *eng, const aesfhe_ct *const *cts, int32_t
 /* sum_i a_i (*) b_i, one relinearisation + one rescale for the whole sum */
 int aesfhe_dot(aesfhe_engine *eng, const aesfhe_ct *const *a, const aesfhe_ct *const *b,
                int32_t n, const aesfhe_key *rlk, aesfhe_ct **out);
+/* m bivariate polynomials over shared power bases (the 2-D LUT evaluation of the reference's
+ * nibble services, xor_service.py:245-286 / sbox_service.py:116-138, fused):
+ *   outs[t] = sum_{i<nx, j<ny} C[t][i][j] x^i y^j,  C = re + i*im row-major [m][nx][ny],
+ * xb = x^1..x^{nx-1}, yb = y^1..y^{ny-1} (2 polynomials, aligned to the lowest level l >= 2).
+ * Constants are scaled by S1 = D_{l-2} q_l q_{l-1} / D_l^2 (D = canonical scales) and
+ * rounded: A = llround(re*S1), B = llround(im*S1); an x^0 or y^0 factor multiplies the
+ * constant by R = llround(D_l) mod q (both: R^2).  Inner sums stay unrescaled; one
+ * relinearisation and two rescales put every output at level l-2, scale D_{l-2}.
+ * 1 <= nx, ny <= 16. */
+int aesfhe_poly2(aesfhe_engine *eng, const aesfhe_ct *const *xb, int32_t nx,
+                 const aesfhe_ct *const *yb, int32_t ny, const double *re, const double *im,
+                 int32_t m, const aesfhe_key *rlk, aesfhe_ct **outs);
 
 /* ---- raw kernels (known-answer tests and roofline measurement) ------------------------- */
 /* In-place forward (inverse=0) / inverse NTT of nlimb host limbs; limb i uses prime pids[i]

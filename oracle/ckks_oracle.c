@@ -1539,6 +1539,114 @@ int aesfhe_dot(aesfhe_engine *e, const aesfhe_ct *const *a, const aesfhe_ct *con
     return 0;
 }
 
+/* Bivariate polynomial over shared power bases (include/aesfhe.h aesfhe_poly2), evaluated
+ * term by term: per output, inner sums a_i = F_i0 + sum_{j>=1} F_ij y^j (F = llround(c*S1),
+ * times R = llround(D_l) for an x^0 or y^0 factor, R^2 for both), tensor d = sum_{i>=1}
+ * x^i (x) a_i + (a_0, a_0', 0), then relinearisation and two rescales. */
+int aesfhe_poly2(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, const aesfhe_ct *const *yb,
+                 int32_t ny, const double *re, const double *im, int32_t m, const aesfhe_key *rlk,
+                 aesfhe_ct **outs) {
+    if (nx < 1 || ny < 1 || nx > 16 || ny > 16 || m < 1)
+        return fail(AESFHE_EARG, "poly2 needs 1 <= nx, ny <= %d and m >= 1", 16);
+    if (nx + ny < 3) return fail(AESFHE_EARG, "poly2 needs at least one basis ciphertext");
+    if (!rlk || rlk->kind != 2) return fail(AESFHE_EARG, "poly2 needs a relinearization key");
+    const aesfhe_ct *all[32] = {0};
+    int na = 0;
+    for (int i = 0; i < nx - 1; i++) all[na++] = xb[i];
+    for (int j = 0; j < ny - 1; j++) all[na++] = yb[j];
+    int l = all[0]->level, B = 1;
+    for (int a = 0; a < na; a++) {
+        if (all[a]->npoly != 2) return fail(AESFHE_EDEGREE, "poly2 inputs should have 2 polynomials");
+        if (all[a]->is_zero) return fail(AESFHE_EARG, "poly2 basis ciphertext is zero");
+        if (all[a]->level < l) l = all[a]->level;
+        if (all[a]->B > B) B = all[a]->B;
+    }
+    for (int a = 0; a < na; a++)
+        if (all[a]->B != B && all[a]->B != 1) return fail(AESFHE_EARG, "batch mismatch");
+    if (l < 2) return fail(AESFHE_ELEVEL, "no level left for a bivariate polynomial");
+    const double *D = e->scales;
+    const double S1 = D[l - 2] / D[l] * ((double)e->q[l] / D[l]) * (double)e->q[l - 1];
+    const i64 R = llround(D[l]);
+    const int per = nx * ny, N = e->N;
+    aesfhe_ct *al[32];
+    for (int a = 0; a < na; a++) al[a] = level_down_raw(e, all[a], l);
+    aesfhe_ct **X = al, **Y = al + (nx - 1);
+    i64 *A = malloc(sizeof(i64) * per), *Bc = malloc(sizeof(i64) * per);
+    for (int t = 0; t < m; t++) {
+        int any = 0;
+        for (int c = 0; c < per; c++) {
+            A[c] = llround(re[(size_t)t * per + c] * S1);
+            Bc[c] = llround(im[(size_t)t * per + c] * S1);
+            if (A[c] || Bc[c]) any = 1;
+        }
+        if (!any) {
+            outs[t] = ct_new(e, B, 2, l - 2);
+            outs[t]->is_zero = 1;
+            continue;
+        }
+        aesfhe_ct *acc = ct_new(e, B, 3, l);
+#pragma omp parallel for schedule(static)
+        for (int li = 0; li <= l; li++) {
+            const u64 q = e->q[li];
+            const mont_t *mt = &e->mont[li];
+            const u64 r1 = smod(R, q), r2 = mul_mod_slow(r1, r1, q), I = e->iroot[li];
+            u64 f[2][256], fp[2][256];
+            for (int c = 0; c < per; c++) {
+                const int j = c % ny, i = c / ny;
+                const u64 sc = (i == 0 && j == 0) ? r2 : (i == 0 || j == 0) ? r1 : 1;
+                const u64 a = mul_mod_slow(smod(A[c], q), sc, q), b = mul_mod_slow(smod(Bc[c], q), sc, q);
+                const u64 bi = mul_mod_slow(b, I, q);
+                f[0][c] = add_mod(a, bi, q);
+                f[1][c] = sub_mod(a, bi, q);
+                fp[0][c] = shoup_pre(f[0][c], q);
+                fp[1][c] = shoup_pre(f[1][c], q);
+            }
+            for (int b = 0; b < B; b++) {
+                u64 *d0 = limb(e, acc, b, 0, li), *d1 = limb(e, acc, b, 1, li), *d2 = limb(e, acc, b, 2, li);
+                for (int k = 0; k < N; k++) {
+                    const int hh = k >= N / 2;
+                    u64 s0 = 0, s1 = 0, s2 = 0;
+                    for (int i = 0; i < nx; i++) {
+                        u64 a0 = f[hh][i * ny], a1 = 0;
+                        for (int j = 1; j < ny; j++) {
+                            const aesfhe_ct *y = Y[j - 1];
+                            const int yb_ = y->B == 1 ? 0 : b;
+                            const int c = i * ny + j;
+                            a0 = add_mod(a0, mul_shoup(limb(e, y, yb_, 0, li)[k], f[hh][c], fp[hh][c], q), q);
+                            a1 = add_mod(a1, mul_shoup(limb(e, y, yb_, 1, li)[k], f[hh][c], fp[hh][c], q), q);
+                        }
+                        if (i == 0) {
+                            s0 = add_mod(s0, a0, q);
+                            s1 = add_mod(s1, a1, q);
+                        } else {
+                            const aesfhe_ct *x = X[i - 1];
+                            const int xb_ = x->B == 1 ? 0 : b;
+                            const u64 x0 = limb(e, x, xb_, 0, li)[k], x1 = limb(e, x, xb_, 1, li)[k];
+                            s0 = add_mod(s0, mul_mod(x0, a0, mt), q);
+                            s1 = add_mod(s1, add_mod(mul_mod(x0, a1, mt), mul_mod(x1, a0, mt), q), q);
+                            s2 = add_mod(s2, mul_mod(x1, a1, mt), q);
+                        }
+                    }
+                    d0[k] = s0;
+                    d1[k] = s1;
+                    d2[k] = s2;
+                }
+            }
+        }
+        aesfhe_ct *rl, *r1;
+        relin_raw(e, acc, rlk, &rl);
+        aesfhe_ct_free(acc);
+        r1 = rescale_raw(e, rl);
+        aesfhe_ct_free(rl);
+        outs[t] = rescale_raw(e, r1);
+        aesfhe_ct_free(r1);
+    }
+    free(A);
+    free(Bc);
+    for (int a = 0; a < na; a++) aesfhe_ct_free(al[a]);
+    return 0;
+}
+
 int aesfhe_ntt_host(aesfhe_engine *e, uint64_t *limbs, int32_t nlimb, const int32_t *pids, int32_t inv) {
     for (int i = 0; i < nlimb; i++)
         if (pids[i] < 0 || pids[i] >= e->np) return fail(AESFHE_EARG, "bad prime index");

@@ -134,3 +134,25 @@ def test_full_params_mul_bit_exact(product_lib, oracle_lib, gpu_available):
     _same(g, o, mg, mo)
     np.testing.assert_allclose(g.decrypt(mg, kg["sk"]), z * z, atol=1e-5)
     _same(g, o, g.rotate(mg, kg["rot"], -2048), o.rotate(mo, ko["rot"], -2048))
+
+
+def test_poly2_bit_exact(product_lib, oracle_lib, gpu_available):
+    """Fused bivariate evaluation: m = 10 outputs (two kernel chunks), one all-zero output,
+    nx != ny, a broadcast (B = 1) basis element, constant row/column terms."""
+    g, o = _pair(product_lib, oracle_lib, **SMALL)
+    kg, ko = _keys(g), _keys(o)
+    rng = np.random.default_rng(7)
+    zx = np.exp(-2j * np.pi * rng.integers(0, 16, (2, g.slot_count)) / 16)
+    zy = np.exp(-2j * np.pi * rng.integers(0, 16, g.slot_count) / 16)
+    C = (rng.standard_normal((10, 4, 3)) + 1j * rng.standard_normal((10, 4, 3))) * 0.2
+    C[3] = 0
+    res = []
+    for eng, k in ((g, kg), (o, ko)):
+        xb = eng.make_power_basis(eng.encrypt(zx, k["pk"]), 3, k["rlk"])
+        yb = eng.make_power_basis(eng.encrypt(zy, k["pk"]), 2, k["rlk"])
+        res.append(eng.poly2(xb, yb, C, k["rlk"]))
+    for a, b in zip(*res):
+        _same(g, o, a, b)
+    dec = g.decrypt(res[0][0], kg["sk"])
+    want = sum(C[0, i, j] * zx ** i * zy ** j for i in range(4) for j in range(3))
+    np.testing.assert_allclose(dec, want, atol=1e-4)

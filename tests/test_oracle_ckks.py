@@ -129,3 +129,24 @@ def test_levels_and_scales(env):
     s = e.add(pb[7], ct)                                   # mixed levels align
     np.testing.assert_allclose(e.decrypt(s, sk), z ** 8 + z, atol=1e-6)
     np.testing.assert_allclose(e.decrypt(e.add(ct, 0.5 - 0.25j), sk), z + 0.5 - 0.25j, atol=1e-6)
+
+
+def test_poly2_semantics(env):
+    """aesfhe_poly2 = sum C[t,i,j] x^i y^j at level l-2 (include/aesfhe.h)."""
+    e, sk, pk, rlk, _ = env
+    rng = np.random.default_rng(9)
+    zx = np.exp(-2j * np.pi * rng.integers(0, 16, e.slot_count) / 16)
+    zy = np.exp(-2j * np.pi * rng.integers(0, 16, e.slot_count) / 16)
+    xb = e.make_power_basis(e.encrypt(zx, pk), 3, rlk)
+    yb = e.make_power_basis(e.encrypt(zy, pk), 3, rlk)
+    C = rng.standard_normal((2, 4, 4)) + 1j * rng.standard_normal((2, 4, 4))
+    outs = e.poly2(xb, yb, C, rlk)
+    lv = min(c.level for c in xb + yb)
+    for t in range(2):
+        assert outs[t].level == lv - 2
+        want = sum(C[t, i, j] * zx ** i * zy ** j for i in range(4) for j in range(4))
+        np.testing.assert_allclose(e.decrypt(outs[t], sk), want, atol=1e-4)
+    with pytest.raises(ValueError):
+        e.poly2(xb[:2], yb, C, rlk)
+    with pytest.raises(RuntimeError, match="at least one basis"):
+        e._check(e._lib.poly2(e._h, None, 1, None, 1, None, None, 1, None, None))
