@@ -144,7 +144,7 @@ struct aesfhe_engine {
     char* ring_h = nullptr;
     size_t ring_size = 8u << 20, ring_off = 0;
     // aesfhe_poly2 constant tables, keyed by (level, shape, coefficients)
-    std::map<std::string, Tw*> poly2_tabs;
+    std::map<std::string, TwD*> poly2_tabs;
     // profiling
     bool prof = false;
     std::vector<ProfRec> recs;
@@ -1593,7 +1593,7 @@ extern "C" int aesfhe_dot(aesfhe_engine* e, const aesfhe_ct* const* a, const aes
 // also R = round(Delta_l) per missing basis factor), so the inner sums are never rescaled: one
 // tensor pass (k_poly2), one batched relinearisation of all m*B outputs, then two rescales land
 // exactly on the canonical scale Delta_{l-2}.  Constant rules: oracle/ckks_oracle.c aesfhe_poly2.
-static Tw* poly2_table(aesfhe_engine* e, int l, int nx, int ny, int m, const std::vector<int64_t>& A,
+static TwD* poly2_table(aesfhe_engine* e, int l, int nx, int ny, int m, const std::vector<int64_t>& A,
                        const std::vector<int64_t>& Bc, int64_t R) {
     std::string key((const char*)&l, sizeof l);
     key.append((const char*)&nx, sizeof nx).append((const char*)&ny, sizeof ny).append((const char*)&m, sizeof m);
@@ -1607,7 +1607,7 @@ static Tw* poly2_table(aesfhe_engine* e, int l, int nx, int ny, int m, const std
     }
     const int nl = l + 1;
     const size_t per = (size_t)m * nx * ny;
-    std::vector<Tw> T((size_t)nl * 2 * per);
+    std::vector<TwD> T((size_t)nl * 2 * per);
     for (int li = 0; li < nl; li++) {
         const u64 q = e->chain.q[li];
         const u64 r1 = h_smod(R, q), r2 = h_mulmod(r1, r1, q), I = e->h_iroot[li];
@@ -1617,13 +1617,13 @@ static Tw* poly2_table(aesfhe_engine* e, int l, int nx, int ny, int m, const std
             const u64 a = h_mulmod(h_smod(A[c], q), t, q), b = h_mulmod(h_smod(Bc[c], q), t, q);
             const u64 bi = h_mulmod(b, I, q);
             const u64 f0 = h_addmod(a, bi, q), f1 = h_submod(a, bi, q);
-            T[((size_t)li * 2 + 0) * per + c] = Tw{f0, (double)f0 / (double)q};
-            T[((size_t)li * 2 + 1) * per + c] = Tw{f1, (double)f1 / (double)q};
+            T[((size_t)li * 2 + 0) * per + c] = TwD{(double)f0, (double)f0 / (double)q};
+            T[((size_t)li * 2 + 1) * per + c] = TwD{(double)f1, (double)f1 / (double)q};
         }
     }
-    Tw* d = nullptr;
-    HIPC(hipMalloc(&d, T.size() * sizeof(Tw)));
-    HIPC(hipMemcpy(d, T.data(), T.size() * sizeof(Tw), hipMemcpyHostToDevice));
+    TwD* d = nullptr;
+    HIPC(hipMalloc(&d, T.size() * sizeof(TwD)));
+    HIPC(hipMemcpy(d, T.data(), T.size() * sizeof(TwD), hipMemcpyHostToDevice));
     e->poly2_tabs.emplace(key, d);
     return d;
 }
@@ -1684,7 +1684,7 @@ extern "C" int aesfhe_poly2(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_
         }
         if (px.empty()) px.push_back(nullptr), sx.push_back(0);
         if (py.empty()) py.push_back(nullptr), sy.push_back(0);
-        const Tw* tab = poly2_table(e, l, nx, ny, ml, A, Bc, R);
+        const TwD* tab = poly2_table(e, l, nx, ny, ml, A, Bc, R);
         auto dpx = upload_small(e, px.data(), px.size());
         auto dpy = upload_small(e, py.data(), py.size());
         auto dsx = upload_small(e, sx.data(), sx.size());

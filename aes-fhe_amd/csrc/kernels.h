@@ -53,6 +53,38 @@ __device__ __forceinline__ u64 mul_w(u64 a, u64 w, double wq, u64 q) {
     return (u64)r;
 }
 
+// ---- all-fp64 modular arithmetic on exact integers carried in doubles (|x| < 2^52) ----------
+// a*w - rint(a*w/q)*q computed exactly: p + pl = a*w (fma split), t + tl = qh*q, and
+// (p - t) + (pl - tl) has no rounding (Sterbenz once qh != 0; integers < 2^53 otherwise).
+// Result in (-q, q) when wq = w/q rounded (|quotient error| < 1); signed inputs are fine.
+// tools/mulmod_bench.hip: 2.65 T/s vs 2.17 T/s for mul_w on gfx950.
+// rint(v) = (v + 1.5*2^52) - 1.5*2^52 for |v| < 2^51 (signed: the sum stays in [2^52, 2^53))
+constexpr double kMagic52 = 6755399441055744.0;
+__device__ __forceinline__ double fmul_rem(double a, double w, double wq, double q) {
+    const double p = a * w;
+    const double pl = __builtin_fma(a, w, -p);
+    const double qh = __builtin_fma(a, wq, kMagic52) - kMagic52;
+    const double t = qh * q;
+    const double tl = __builtin_fma(qh, q, -t);
+    return (p - t) + (pl - tl);
+}
+// x - rint(x/q)*q for |x| < 2^53: result in [-q/2 - 1, q/2 + 1] (exact: qh*q < 2^53)
+__device__ __forceinline__ double fred(double x, double q, double qinv) {
+    const double qh = __builtin_fma(x, qinv, kMagic52) - kMagic52;
+    return __builtin_fma(-qh, q, x);
+}
+// canonical residue in [0, q) of |x| < 2^53, as u64
+__device__ __forceinline__ u64 fcanon(double x, double q, double qinv) {
+    double r = fred(x, q, qinv);
+    r = r < 0.0 ? r + q : r;
+    r = r >= q ? r - q : r;
+    return (u64)r;
+}
+struct alignas(16) TwD {
+    double w;   // constant as an exact double (< 2^52)
+    double wq;  // w / q
+};
+
 // A set of limbs: poly p (0..npoly-1), limb l (0..nl-1) at base + p*pstride + l*N.
 // Prime of limb l: l < nq ? qpid0 + l : spid0 + (l - nq)  (Q limbs then special limbs).
 struct Span {

@@ -513,69 +513,78 @@ __global__ void k_square(const u64* __restrict__ s, u64* __restrict__ o,
 // t0 <= t < t0 + mc (mc <= 8) and element (batch bb, limb l, coefficient k):
 //   a_{t,i} = F[t,i,0] + sum_{j>=1} F[t,i,j] * y^j       (inner sums, never rescaled)
 //   d_t     = (a_{t,0}, a'_{t,0}, 0) + sum_{i>=1} x^i (x) a_{t,i}
-// F: Tw table [nl][half][mtot][nx][ny]; the j = 0 entries are additive constants (w only), the
-// i = 0 row already carries the factor R = round(Delta_l) of the implicit x^0 ciphertext.
-// The y basis lives in registers, x^i is loaded once per i (outer loop), the mc output
-// accumulators stay in registers.  Lazy u64 sums: <= 16 terms < 2^50 (inner), <= 31 (d1).
-// x/y: pointer + batch-stride arrays of compact 2-poly views at level nl-1 (poly stride ps).
-// out: [mtot][B][3][nl][N] (output t at out + t*oos).  grid (N/256, nl, B)
+// F: TwD table [nl][half][mtot][nx][ny]; the j = 0 entries are additive constants, the i = 0
+// row already carries the factor R = round(Delta_l) of the implicit x^0 ciphertext.
+// All arithmetic is exact integer arithmetic in fp64 (fmul_rem / fred): signed residues in
+// (-q, q), sums folded back below 2^53 every 5 terms.  The y basis lives in registers (as
+// doubles), x^i is loaded once per i (outer loop), the mc output accumulators stay in
+// registers.  x/y: pointer + batch-stride arrays of compact 2-poly views at level nl-1 (poly
+// stride ps).  out: [mtot][B][3][nl][N] (output t at out + t*oos).  grid (N/256, nl, B)
 constexpr int kPoly2Max = 16, kPoly2Out = 8;
 __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp, const long* __restrict__ xbs, int nx,
                         const u64* const* __restrict__ yp, const long* __restrict__ ybs, int ny,
-                        long ps, const Tw* __restrict__ F, int mtot, int t0, int mc,
+                        long ps, const TwD* __restrict__ F, int mtot, int t0, int mc,
                         u64* __restrict__ out, long oos, long obs, const u64* __restrict__ qs,
                         const double* __restrict__ qinv, int logN) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int l = blockIdx.y, bb = blockIdx.z, nl = gridDim.y;
     const int h = (int)((blockIdx.x * blockDim.x) >> (logN - 1));  // block-uniform half
-    const u64 q = qs[l];
+    const double q = (double)qs[l];
     const double qi = qinv[l];
     const long off = ((long)l << logN) + k;
-    u64 y0[kPoly2Max - 1], y1[kPoly2Max - 1];
+    double y0[kPoly2Max - 1], y1[kPoly2Max - 1];
 #pragma unroll
     for (int j = 0; j < kPoly2Max - 1; j++) {
-        y0[j] = y1[j] = 0;
+        y0[j] = y1[j] = 0.0;
         if (j < ny - 1) {
             const u64* p = yp[j] + (long)bb * ybs[j] + off;
-            y0[j] = p[0];
-            y1[j] = p[ps];
+            y0[j] = u2d(p[0]);
+            y1[j] = u2d(p[ps]);
         }
     }
-    u64 d0[kPoly2Out], d1[kPoly2Out], d2[kPoly2Out];
+    double d0[kPoly2Out], d1[kPoly2Out], d2[kPoly2Out];
 #pragma unroll
-    for (int t = 0; t < kPoly2Out; t++) d0[t] = d1[t] = d2[t] = 0;
-    const Tw* Fl = F + ((size_t)(l * 2 + h) * mtot + t0) * nx * ny;
+    for (int t = 0; t < kPoly2Out; t++) d0[t] = d1[t] = d2[t] = 0.0;
+    const TwD* Fl = F + ((size_t)(l * 2 + h) * mtot + t0) * nx * ny;
 #pragma unroll 1
     for (int i = 0; i < nx; i++) {
-        u64 xa = 0, xb = 0;
+        double xa = 0.0, xb = 0.0;
         if (i > 0) {
             const u64* p = xp[i - 1] + (long)bb * xbs[i - 1] + off;
-            xa = p[0];
-            xb = p[ps];
+            xa = u2d(p[0]);
+            xb = u2d(p[ps]);
         }
 #pragma unroll
         for (int t = 0; t < kPoly2Out; t++) {
             if (t < mc) {
-                const Tw* Fi = Fl + ((size_t)t * nx + i) * ny;
-                u64 a0 = Fi[0].w, a1 = 0;
+                const TwD* Fi = Fl + ((size_t)t * nx + i) * ny;
+                double a0 = Fi[0].w, a1 = 0.0;
 #pragma unroll
                 for (int j = 1; j < kPoly2Max; j++) {
                     if (j < ny) {
-                        const Tw f = Fi[j];
-                        a0 += mul_w(y0[j - 1], f.w, f.wq, q);
-                        a1 += mul_w(y1[j - 1], f.w, f.wq, q);
+                        const TwD f = Fi[j];
+                        a0 += fmul_rem(y0[j - 1], f.w, f.wq, q);
+                        a1 += fmul_rem(y1[j - 1], f.w, f.wq, q);
+                        if (j == 5 || j == 10) {  // keep |sum| <= q/2 + 5q < 2^53
+                            a0 = fred(a0, q, qi);
+                            a1 = fred(a1, q, qi);
+                        }
                     }
                 }
-                a0 = red_m(a0, q, qi);
-                a1 = red_m(a1, q, qi);
+                a0 = fred(a0, q, qi);
+                a1 = fred(a1, q, qi);
                 if (i == 0) {
                     d0[t] += a0;
                     d1[t] += a1;
                 } else {
-                    d0[t] += mul_m(xa, a0, q, qi);
-                    d1[t] += mul_m(xa, a1, q, qi) + mul_m(xb, a0, q, qi);
-                    d2[t] += mul_m(xb, a1, q, qi);
+                    const double a0q = a0 * qi, a1q = a1 * qi;
+                    d0[t] += fmul_rem(xa, a0, a0q, q);
+                    d1[t] += fmul_rem(xa, a1, a1q, q) + fmul_rem(xb, a0, a0q, q);
+                    d2[t] += fmul_rem(xb, a1, a1q, q);
                 }
+                d0[t] = fred(d0[t], q, qi);
+                d1[t] = fred(d1[t], q, qi);
+                d2[t] = fred(d2[t], q, qi);
             }
         }
     }
@@ -585,9 +594,9 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
     for (int t = 0; t < kPoly2Out; t++) {
         if (t < mc) {
             u64* ot = o + (long)(t0 + t) * oos;
-            ot[0] = red_m(d0[t], q, qi);
-            ot[pstr] = red_m(d1[t], q, qi);
-            ot[2 * pstr] = red_m(d2[t], q, qi);
+            ot[0] = fcanon(d0[t], q, qi);
+            ot[pstr] = fcanon(d1[t], q, qi);
+            ot[2 * pstr] = fcanon(d2[t], q, qi);
         }
     }
 }
