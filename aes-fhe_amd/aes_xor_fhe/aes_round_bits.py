@@ -1,55 +1,59 @@
 """Row-sliced, bit-domain homomorphic AES-128 round (the fast path of the bench).
 
-Same primitive kinds as the reference's services (Zeta-16 nibble LUT polynomials as in
-xor_service.py:245-286 / sbox_service.py:116-138, slot rotations as in shiftrows_service.py:
-33-51), arranged so that the expensive operations disappear:
+Same primitive kinds as the reference's services (LUT polynomials as in xor_service.py:245-286
+/ sbox_service.py:116-138, slot rotations as in shiftrows_service.py:33-51), arranged so that
+the expensive operations disappear.  The state is carried as +-1 bits B = (-1)^bit:
 
-* layout -- one ciphertext per state row r and nibble: slot = c * n_blk + block with
-  n_blk = slot_count / 4 (8192 blocks at N = 2^16).  ShiftRows (out(r,c) = in(r, c+r)) is then a
-  single whole-ciphertext rotation of row r by -r*n_blk slots, with no masks; as it commutes
-  with SubBytes it is applied to the nibble inputs (6 rotations per 8192 blocks).
-* SubBytes -- from the Zeta-16 nibble pair (h, l) straight to the 8 output bits in the +-1
-  encoding B_j = (-1)^{bit_j}: eight 2-D LUT polynomials sharing the power bases of h and l
-  (one fused Engine.poly2 call: inner sums never rescaled, one relinearisation per bit).
-* MixColumns -- in the +-1 encoding XOR is multiplication.  With a_r the SubBytes bytes of row
-  r: out_r = xtime(a_r ^ a_{r+1}) ^ a_r ^ t, t = a_0 ^ a_1 ^ a_2 ^ a_3.  Per bit j:
+* layout -- one ciphertext per state row r and bit j: slot = c * n_blk + block with
+  n_blk = slot_count / 4 (8192 blocks at N = 2^16).  ShiftRows (out(r,c) = in(r, c+r)) is a
+  single whole-ciphertext rotation of row r by -r*n_blk slots, no masks (24 per 8192 blocks).
+* SubBytes -- every Boolean function of a byte is a multilinear polynomial in its +-1 bits
+  whose coefficients are its Walsh spectrum.  With M^hi_S / M^lo_T the 15 non-empty monomials
+  of the high / low nibble bits (11 products each, depth 2), the 8 output bits are
+  out_t = sum_{S,T} W_t[S,T] M^hi_S M^lo_T: one fused Engine.poly2 call per row (inner sums
+  never rescaled, one relinearisation per output bit), depth 2.
+* MixColumns -- XOR is multiplication.  With a_r the SubBytes bytes of row r:
+  out_r = xtime(a_r ^ a_{r+1}) ^ a_r ^ t, t = a_0 ^ a_1 ^ a_2 ^ a_3.  Per bit j:
   U_rj = A_rj A_{r+1,j}; T_j = U_0j U_2j; xtime(u)_j = u_{j-1} (j = 0: u_7), times u_7 for
   j in {1, 3, 4}; OUT_rj = (A_rj T_j) XT_rj.  116 products, depth 4.
 * AddRoundKey -- 32 products with the encrypted key bits (B = 1, broadcast), depth 1.
-* back to nibbles -- Zeta16^h = prod_k (alpha_k + beta_k B_{4+k}) with alpha = (1 + zeta^{2^k})/2,
-  beta = (1 - zeta^{2^k})/2: one product per bit pair, one linear combination, one product,
-  depth 3 (same for the low nibble).
-Round depth 5 + 4 + 1 + 3 = 13 (two rounds per 30-level budget); about 322 key switches per
-8192 blocks against ~960 for the byte-major nibble-domain round (aes_round.py).
+Round depth 4 + 4 + 1 = 9 (three rounds per 30-level budget); 24 + 88 + 4 + 116 + 32 = 264 key
+switches per 8192 blocks against ~960 for the byte-major nibble-domain round (aes_round.py).
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Sequence
 
 import numpy as np
 
 from . import aes_tables as T
-from .coeffs_gen import lut_2d
 from .fhe import Ciphertext, Engine
 
-ZETA16 = np.exp(-2j * np.pi / 16)
 XT_OF = {0: (7, False), 1: (0, True), 2: (1, False), 3: (2, True), 4: (3, True), 5: (4, False),
          6: (5, False), 7: (6, False)}  # xtime bit j = u[src] (* u[7] if flagged)
 
 
+def walsh_sbox() -> np.ndarray:
+    """W[t, S, T]: +-1 S-box output bit t as sum_{S,T} W M^hi_S M^lo_T (S, T = 4-bit masks of
+    the high / low nibble bits; mask 0 = the constant monomial)."""
+    x = np.arange(256)
+    f = np.stack([1.0 - 2.0 * ((T.SBOX[x].astype(np.int64) >> t) & 1) for t in range(8)])
+    mono = np.array([[np.prod([1 - 2 * ((v >> k) & 1) for k in range(4) if (m >> k) & 1])
+                      for v in range(16)] for m in range(16)], dtype=np.float64)  # [mask, nibble]
+    hi, lo = x >> 4, x & 15
+    return np.einsum("tx,sx,ux->tsu", f, mono[:, hi], mono[:, lo]) / 256.0
+
 
 class AESRowRound:
-    def __init__(self, engine: Engine, sk, pk, rlk, cjk, rotation_keys=None):
+    """State: 4 rows x 8 +-1 bit ciphertexts (row r, bit j), each batched over NB sets of
+    n_blk blocks."""
+
+    def __init__(self, engine: Engine, sk, pk, rlk, cjk=None, rotation_keys=None):
         self.e = engine
         self.sk, self.pk, self.rlk, self.cjk = sk, pk, rlk, cjk
         self.sc = engine.slot_count
         self.n_blk = self.sc // 4
-        # SubBytes output bits as +-1 values: (-1)^{bit_j(S(16h + l))} = zeta_2^{bit}
-        self.C_bits = [lut_2d(lambda h, l, j=j: (int(T.SBOX[16 * h + l]) >> j) & 1, 16, out_mod=2)
-                       for j in range(8)]
-        # bits -> Zeta-16 nibble: factor k maps B = (-1)^x to zeta^{2^k x}
-        self.alpha = [(1 + ZETA16 ** (1 << k)) / 2 for k in range(4)]
-        self.beta = [(1 - ZETA16 ** (1 << k)) / 2 for k in range(4)]
+        self.W = walsh_sbox()
         if rotation_keys is None:
             rotation_keys = {r: engine.create_fixed_rotation_key(sk, -r * self.n_blk) for r in (1, 2, 3)}
         self.rot_keys = rotation_keys
@@ -71,23 +75,14 @@ class AESRowRound:
                 out[:, :, r + 4 * c] = v[:, c, :]
         return out
 
-    def encrypt_blocks(self, blocks: np.ndarray) -> List[Tuple[Ciphertext, Ciphertext]]:
-        out = []
-        for row in self.pack(blocks):
-            s = row.astype(np.int64)
-            out.append((self.e.encrypt(ZETA16 ** (s >> 4), self.pk),
-                        self.e.encrypt(ZETA16 ** (s & 15), self.pk)))
-        return out
+    def encrypt_bytes_rows(self, rows: Sequence[np.ndarray], level: int | None = None):
+        return [[self.e.encrypt(1.0 - 2.0 * ((row.astype(np.int64) >> j) & 1), self.pk, level=level)
+                 for j in range(8)] for row in rows]
 
-    def _dec16(self, ct):
-        z = np.atleast_2d(self.e.decrypt(ct, self.sk))
-        return np.mod(np.rint(-np.angle(z) * 16 / (2 * np.pi)), 16).astype(np.uint8)
+    def encrypt_blocks(self, blocks: np.ndarray) -> List[List[Ciphertext]]:
+        return self.encrypt_bytes_rows(self.pack(blocks))
 
-    def decrypt_blocks(self, rows: Sequence[Tuple[Ciphertext, Ciphertext]]) -> np.ndarray:
-        return self.unpack([(self._dec16(h) << 4) | self._dec16(l) for h, l in rows])
-
-    def decrypt_bits(self, bits: Sequence[Sequence[Ciphertext]]) -> np.ndarray:
-        """4 rows x 8 bit ciphertexts (+-1) -> blocks (debug / tests)."""
+    def decrypt_blocks(self, bits: Sequence[Sequence[Ciphertext]]) -> np.ndarray:
         rows = []
         for r in range(4):
             acc = 0
@@ -97,47 +92,46 @@ class AESRowRound:
             rows.append(acc)
         return self.unpack(rows)
 
+    decrypt_bits = decrypt_blocks
+
     def encrypt_round_key(self, rk: np.ndarray, level: int | None = None) -> List[List[Ciphertext]]:
         """Key bits as +-1 per row (B = 1, broadcast over the batch)."""
         rk = np.asarray(rk, dtype=np.int64)
-        keys = []
-        for r in range(4):
-            row = np.repeat(rk[[r + 4 * c for c in range(4)]], self.n_blk)
-            keys.append([self.e.encrypt(1.0 - 2.0 * ((row >> j) & 1), self.pk, level=level)
-                         for j in range(8)])
-        return keys
+        rows = [np.repeat(rk[[r + 4 * c for c in range(4)]], self.n_blk)[None] for r in range(4)]
+        return self.encrypt_bytes_rows(rows, level=level)
 
     # ---- building blocks ---------------------------------------------------------------------
-    def full_basis(self, x: Ciphertext) -> Dict[int, Ciphertext]:
-        e = self.e
-        pw = e.make_power_basis(x, 8, self.rlk)
-        b = {k + 1: c for k, c in enumerate(pw)}
-        for k in range(9, 16):
-            b[k] = e.conjugate(b[16 - k], self.cjk)
-        keys = sorted(b)
-        return dict(zip(keys, e.align([b[k] for k in keys])))
-
     def mul(self, a: Ciphertext, b: Ciphertext) -> Ciphertext:
         return self.e.multiply(a, b, self.rlk)
 
-    def lut2_bits(self, hb, lb) -> List[Ciphertext]:
-        """The 8 S-box output bits from the power bases of h and l in one fused bivariate
-        evaluation (Engine.poly2): out_j = sum_{i,k} C_j[i,k] h^i l^k."""
-        C = np.stack(self.C_bits)
-        return self.e.poly2([hb[k] for k in range(1, 16)], [lb[k] for k in range(1, 16)], C, self.rlk)
+    def monomials(self, b4: Sequence[Ciphertext]) -> Dict[int, Ciphertext]:
+        """All 15 non-empty products of 4 +-1 bit ciphertexts, keyed by bit mask (depth <= 2:
+        pairs from singles, triples = pair * single, the quadruple = pair * pair)."""
+        m = {1 << k: b4[k] for k in range(4)}
+        for a in range(4):
+            for b in range(a + 1, 4):
+                m[(1 << a) | (1 << b)] = self.mul(b4[a], b4[b])
+        m[0b0111] = self.mul(m[0b0011], b4[2])
+        m[0b1011] = self.mul(m[0b0011], b4[3])
+        m[0b1101] = self.mul(m[0b0101], b4[3])
+        m[0b1110] = self.mul(m[0b0110], b4[3])
+        m[0b1111] = self.mul(m[0b0011], m[0b1100])
+        return m
 
     # ---- round steps ---------------------------------------------------------------------------
-    def shift_rows(self, rows):
-        out = [rows[0]]
-        for r in (1, 2, 3):
-            h, l = rows[r]
-            out.append((self.e.rotate(h, self.rot_keys[r]), self.e.rotate(l, self.rot_keys[r])))
+    def shift_rows(self, bits):
+        return [bits[0]] + [[self.e.rotate(c, self.rot_keys[r]) for c in bits[r]] for r in (1, 2, 3)]
+
+    def sub_bytes(self, bits) -> List[List[Ciphertext]]:
+        out = []
+        for row in bits:
+            mh = self.monomials(row[4:8])
+            ml = self.monomials(row[0:4])
+            out.append(self.e.poly2([mh[i] for i in range(1, 16)], [ml[j] for j in range(1, 16)],
+                                    self.W, self.rlk))
         return out
 
-    def sub_bytes_bits(self, rows) -> List[List[Ciphertext]]:
-        return [self.lut2_bits(self.full_basis(h), self.full_basis(l)) for h, l in rows]
-
-    def mix_columns_bits(self, A: List[List[Ciphertext]]) -> List[List[Ciphertext]]:
+    def mix_columns(self, A: List[List[Ciphertext]]) -> List[List[Ciphertext]]:
         U = [[self.mul(A[r][j], A[(r + 1) % 4][j]) for j in range(8)] for r in range(4)]
         Tt = [self.mul(U[0][j], U[2][j]) for j in range(8)]
         out = []
@@ -150,27 +144,11 @@ class AESRowRound:
             out.append(row)
         return out
 
-    def add_round_key_bits(self, S: List[List[Ciphertext]], key) -> List[List[Ciphertext]]:
+    def add_round_key(self, S: List[List[Ciphertext]], key) -> List[List[Ciphertext]]:
         return [[self.mul(S[r][j], key[r][j]) for j in range(8)] for r in range(4)]
 
-    def to_nibbles(self, bits: Sequence[Ciphertext]) -> Tuple[Ciphertext, Ciphertext]:
-        """8 +-1 bit ciphertexts of one row -> (Zeta16^hi, Zeta16^lo)."""
-        e = self.e
-        outs = []
-        for base in (4, 0):
-            pairs = []
-            for k0 in (0, 2):
-                b0, b1 = bits[base + k0], bits[base + k0 + 1]
-                a0, be0 = self.alpha[k0], self.beta[k0]
-                a1, be1 = self.alpha[k0 + 1], self.beta[k0 + 1]
-                p = e.lincomb([b0, b1, self.mul(b0, b1)], [be0 * a1, a0 * be1, be0 * be1])
-                pairs.append(e.add(p, complex(a0 * a1)))
-            outs.append(self.mul(pairs[0], pairs[1]))
-        return outs[0], outs[1]
-
-    def round(self, rows, key, timings: dict | None = None):
-        """ShiftRows -> SubBytes -> MixColumns -> AddRoundKey on the row-sliced state;
-        input and output are 4 (hi, lo) Zeta-16 nibble ciphertext pairs."""
+    def round(self, bits, key, timings: dict | None = None):
+        """ShiftRows -> SubBytes -> MixColumns -> AddRoundKey on the row-sliced +-1 bit state."""
         import time
 
         def mark(name, t0):
@@ -181,14 +159,12 @@ class AESRowRound:
             timings[name] = timings.get(name, 0.0) + (t1 - t0)
             return t1
         t = mark("start", 0.0) if timings is not None else 0.0
-        rows = self.shift_rows(rows)
+        bits = self.shift_rows(bits)
         t = mark("shift_rows", t)
-        A = self.sub_bytes_bits(rows)
+        A = self.sub_bytes(bits)
         t = mark("sub_bytes", t)
-        M = self.mix_columns_bits(A)
+        M = self.mix_columns(A)
         t = mark("mix_columns", t)
-        K = self.add_round_key_bits(M, key)
-        t = mark("add_round_key", t)
-        out = [self.to_nibbles(K[r]) for r in range(4)]
-        mark("to_nibbles", t)
+        out = self.add_round_key(M, key)
+        mark("add_round_key", t)
         return out

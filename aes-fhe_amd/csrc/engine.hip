@@ -1592,7 +1592,9 @@ extern "C" int aesfhe_dot(aesfhe_engine* e, const aesfhe_ct* const* a, const aes
 // Constants carry the integer scale S1 = Delta_{l-2} q_l q_{l-1} / Delta_l^2 (x^0, y^0 terms
 // also R = round(Delta_l) per missing basis factor), so the inner sums are never rescaled: one
 // tensor pass (k_poly2), one batched relinearisation of all m*B outputs, then two rescales land
-// exactly on the canonical scale Delta_{l-2}.  Constant rules: oracle/ckks_oracle.c aesfhe_poly2.
+// exactly on the canonical scale Delta_{l-2}.  Inputs above level l are truncated (limbs 0..l
+// read in place, no rescale); their scale Delta_lev is compensated in the constants by the
+// factor Delta_l / Delta_lev.  Constant rules: oracle/ckks_oracle.c aesfhe_poly2.
 static TwD* poly2_table(aesfhe_engine* e, int l, int nx, int ny, int m, const std::vector<int64_t>& A,
                        const std::vector<int64_t>& Bc, int64_t R) {
     std::string key((const char*)&l, sizeof l);
@@ -1652,50 +1654,55 @@ extern "C" int aesfhe_poly2(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_
     const double S1 = D[l - 2] / D[l] * ((double)e->chain.q[l] / D[l]) * (double)e->chain.q[l - 1];
     const int64_t R = llround(D[l]);
     const size_t per = (size_t)nx * ny;
+    std::vector<double> rx(nx, 1.0), ry(ny, 1.0);
+    for (int i = 1; i < nx; i++) rx[i] = D[l] / D[xb[i - 1]->level];
+    for (int j = 1; j < ny; j++) ry[j] = D[l] / D[yb[j - 1]->level];
+    auto coef = [&](const double* v, int t, size_t c) {
+        return llround(v[t * per + c] * S1 * rx[c / ny] * ry[c % ny]);
+    };
     std::vector<int> live;
     std::vector<int64_t> A, Bc;
     for (int t = 0; t < m; t++) {
         bool any = false;
         for (size_t c = 0; c < per; c++)
-            if (llround(re[t * per + c] * S1) || llround(im[t * per + c] * S1)) any = true;
+            if (coef(re, t, c) || coef(im, t, c)) any = true;
         if (!any) {
             outs[t] = nullptr;
             continue;
         }
         live.push_back(t);
         for (size_t c = 0; c < per; c++) {
-            A.push_back(llround(re[t * per + c] * S1));
-            Bc.push_back(llround(im[t * per + c] * S1));
+            A.push_back(coef(re, t, c));
+            Bc.push_back(coef(im, t, c));
         }
     }
     const int ml = (int)live.size();
     if (ml > 0) {
-        std::vector<std::unique_ptr<Aligned>> al;
         std::vector<const u64*> px, py;
-        std::vector<long> sx, sy;
+        std::vector<long> sx, sy, qx, qy;
         for (size_t a = 0; a < all.size(); a++) {
-            al.emplace_back(new Aligned());
-            align_to(e, all[a], l, *al.back());
-            const View& v = al.back()->v;
-            if (v.ps != (long)nl * N) throw_err(AESFHE_EARG, "poly2: non-compact basis view");
+            const View v = view_of(all[a]);  // truncation: limbs 0..l read in place
+            if (v.B > 1 && v.bs != (long)v.np * v.ps) throw_err(AESFHE_EARG, "poly2: non-compact basis view");
             const long bs = v.B == 1 && B > 1 ? 0 : v.bs;
-            if ((int)a < nx - 1) px.push_back(v.d), sx.push_back(bs);
-            else py.push_back(v.d), sy.push_back(bs);
+            if ((int)a < nx - 1) px.push_back(v.d), sx.push_back(bs), qx.push_back(v.ps);
+            else py.push_back(v.d), sy.push_back(bs), qy.push_back(v.ps);
         }
-        if (px.empty()) px.push_back(nullptr), sx.push_back(0);
-        if (py.empty()) py.push_back(nullptr), sy.push_back(0);
+        if (px.empty()) px.push_back(nullptr), sx.push_back(0), qx.push_back(0);
+        if (py.empty()) py.push_back(nullptr), sy.push_back(0), qy.push_back(0);
         const TwD* tab = poly2_table(e, l, nx, ny, ml, A, Bc, R);
         auto dpx = upload_small(e, px.data(), px.size());
         auto dpy = upload_small(e, py.data(), py.size());
         auto dsx = upload_small(e, sx.data(), sx.size());
         auto dsy = upload_small(e, sy.data(), sy.size());
+        auto dqx = upload_small(e, qx.data(), qx.size());
+        auto dqy = upload_small(e, qy.data(), qy.size());
         const int Bt = ml * B;
         const long obs = 3L * nl * N;
         aesfhe_ct* d3 = ct_new(e, Bt, 3, l);
         {
             ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml));
             for (int t0 = 0; t0 < ml; t0 += kPoly2Out)
-                hipLaunchKernelGGL(k_poly2, ew_grid(e, nl, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, nx, (const u64* const*)dpy, (const long*)dsy, ny, (long)nl * N, tab, ml, t0, std::min(kPoly2Out, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, e->logN);
+                hipLaunchKernelGGL(k_poly2, ew_grid(e, nl, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny, tab, ml, t0, std::min(kPoly2Out, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, e->logN);
         }
         HIPC(hipGetLastError());
         aesfhe_ct* rl = relin_ct(e, d3, rlk);

@@ -518,12 +518,14 @@ __global__ void k_square(const u64* __restrict__ s, u64* __restrict__ o,
 // All arithmetic is exact integer arithmetic in fp64 (fmul_rem / fred): signed residues in
 // (-q, q), sums folded back below 2^53 every 5 terms.  The y basis lives in registers (as
 // doubles), x^i is loaded once per i (outer loop), the mc output accumulators stay in
-// registers.  x/y: pointer + batch-stride arrays of compact 2-poly views at level nl-1 (poly
-// stride ps).  out: [mtot][B][3][nl][N] (output t at out + t*oos).  grid (N/256, nl, B)
+// registers.  x/y: pointer, batch-stride and poly-stride arrays of 2-poly ciphertexts at level
+// >= nl-1 (only limbs 0..nl-1 are read: truncation).  out: [mtot][B][3][nl][N] (output t at
+// out + t*oos).  grid (N/256, nl, B)
 constexpr int kPoly2Max = 16, kPoly2Out = 8;
-__global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp, const long* __restrict__ xbs, int nx,
-                        const u64* const* __restrict__ yp, const long* __restrict__ ybs, int ny,
-                        long ps, const TwD* __restrict__ F, int mtot, int t0, int mc,
+__global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
+                        const long* __restrict__ xps, int nx, const u64* const* __restrict__ yp,
+                        const long* __restrict__ ybs, const long* __restrict__ yps, int ny,
+                        const TwD* __restrict__ F, int mtot, int t0, int mc,
                         u64* __restrict__ out, long oos, long obs, const u64* __restrict__ qs,
                         const double* __restrict__ qinv, int logN) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -539,7 +541,7 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
         if (j < ny - 1) {
             const u64* p = yp[j] + (long)bb * ybs[j] + off;
             y0[j] = u2d(p[0]);
-            y1[j] = u2d(p[ps]);
+            y1[j] = u2d(p[yps[j]]);
         }
     }
     double d0[kPoly2Out], d1[kPoly2Out], d2[kPoly2Out];
@@ -552,7 +554,7 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
         if (i > 0) {
             const u64* p = xp[i - 1] + (long)bb * xbs[i - 1] + off;
             xa = u2d(p[0]);
-            xb = u2d(p[ps]);
+            xb = u2d(p[xps[i - 1]]);
         }
 #pragma unroll
         for (int t = 0; t < kPoly2Out; t++) {

@@ -5,10 +5,10 @@
 
 One *step* = one full middle AES-128 round (ShiftRows -> SubBytes -> MixColumns ->
 AddRoundKey) at N = 2^16, L = 30 over a batch of B ciphertext sets per GPU.  Default layout
-"rows" (aes_xor_fhe.aes_round_bits.AESRowRound): a set is 4 state rows x (hi, lo) Zeta-16
-nibble ciphertexts carrying 8192 AES blocks; layout "bytes" (aes_xor_fhe.aes_round.
-AESRoundEngine): a set is one byte-major (hi, lo) pair carrying 2048 blocks.  Inputs (encrypted synthetic random AES states) and the encrypted round key are resident
-in HBM before the timed region; the key-side XOR polynomials are precomputed once per key.
+"rows" (aes_xor_fhe.aes_round_bits.AESRowRound): a set is 4 state rows x 8 +-1 bit ciphertexts
+carrying 8192 AES blocks; layout "bytes" (aes_xor_fhe.aes_round.AESRoundEngine): a set is one
+byte-major (hi, lo) Zeta-16 nibble pair carrying 2048 blocks.  Inputs (encrypted synthetic
+random AES states) and the encrypted round key are resident in HBM before the timed region.
 
 Multi-GPU (torchrun, one process per GPU): every rank runs its own shard of ciphertexts --
 the path is embarrassingly parallel (no data-path collective), so the scaling is weak.  The
@@ -77,10 +77,9 @@ class RoundDriver:
         return self.R.round(st, key) if self.layout == "rows" else self.R.round(st[0], st[1], key)
 
     def sub_bytes(self, st):
-        """Bounded CPU sample: SubBytes of the first nibble pair only."""
+        """Bounded CPU sample: SubBytes of the first state row (rows) / the nibble pair (bytes)."""
         if self.layout == "rows":
-            h, l = st[0]
-            return self.R.lut2_bits(self.R.full_basis(h), self.R.full_basis(l))
+            return self.R.sub_bytes(st[:1])
         return self.R.sub_bytes(st[0], st[1])
 
     def decrypt(self, st):
@@ -101,7 +100,7 @@ def cpu_baseline(args):
     """Oracle (CPU restatement) on a bounded sample of the same workload, scaled to blocks/s.
 
     The full round at N=2^16 takes minutes on the oracle, so the sample is: SubBytes of one
-    (hi, lo) nibble pair at N=2^16, L=30 (timed), scaled by the oracle's own full-round/SubBytes
+    state row (rows layout) / nibble pair (bytes layout) at N=2^16, L=30 (timed), scaled by the oracle's own full-round/SubBytes
     time ratio measured at N=2^12, L=30 on the same op sequence (same layout as the GPU run)."""
     sys.path.insert(0, str(ROOT / "tests"))
     import subprocess
@@ -136,7 +135,7 @@ def cpu_baseline(args):
     n_blk = (1 << (args.log_n - 1)) // (4 if args.layout == "rows" else 16)
     return {
         "value": n_blk / est_round, "unit": "blocks/s", "cores": threads, "kind": "port",
-        "sample": (f"oracle SubBytes of 1 nibble pair ({args.layout} layout, {n_blk} blocks/set) at N=2^{args.log_n} "
+        "sample": (f"oracle SubBytes of 1 row/pair ({args.layout} layout, {n_blk} blocks/set) at N=2^{args.log_n} "
                    f"L={args.max_level}: {times[(args.log_n, 'sb')]:.2f} s, scaled by the oracle's "
                    f"round/SubBytes ratio {ratio:.2f} measured at N=2^12 -> est. {est_round:.1f} s "
                    f"per round"),
@@ -225,8 +224,8 @@ def main():
             "data": "synthetic random AES states + random round key, encrypted",
             "config": {
                 "workload": ("one full AES-128 middle round (ShiftRows+SubBytes+MixColumns+"
-                             "AddRoundKey): " + ("row-sliced state, Zeta-16 nibble S-box LUTs to "
-                             "+-1 bits, bit-domain MixColumns/AddRoundKey" if args.layout == "rows"
+                             "AddRoundKey): " + ("row-sliced +-1 bit state, S-box as Walsh "
+                             "polynomial over nibble-bit monomials, bit-domain MixColumns/AddRoundKey" if args.layout == "rows"
                              else "nibble-domain Zeta-16 LUTs, byte-major SIMD packing")),
                 "layout": args.layout,
                 "log_n": args.log_n, "max_level": args.max_level, "special_primes": 8,

@@ -1540,9 +1540,10 @@ int aesfhe_dot(aesfhe_engine *e, const aesfhe_ct *const *a, const aesfhe_ct *con
 }
 
 /* Bivariate polynomial over shared power bases (include/aesfhe.h aesfhe_poly2), evaluated
- * term by term: per output, inner sums a_i = F_i0 + sum_{j>=1} F_ij y^j (F = llround(c*S1),
- * times R = llround(D_l) for an x^0 or y^0 factor, R^2 for both), tensor d = sum_{i>=1}
- * x^i (x) a_i + (a_0, a_0', 0), then relinearisation and two rescales. */
+ * term by term: per output, inner sums a_i = F_i0 + sum_{j>=1} F_ij y^j (F = llround(c*S1*
+ * rx_i*ry_j), times R = llround(D_l) for an x^0 or y^0 factor, R^2 for both), tensor
+ * d = sum_{i>=1} x^i (x) a_i + (a_0, a_0', 0), then relinearisation and two rescales.  Inputs
+ * above level l are truncated to l; rx_i = D_l / D_level(x_i) (1 for x^0), ry_j likewise. */
 int aesfhe_poly2(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, const aesfhe_ct *const *yb,
                  int32_t ny, const double *re, const double *im, int32_t m, const aesfhe_key *rlk,
                  aesfhe_ct **outs) {
@@ -1568,15 +1569,19 @@ int aesfhe_poly2(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, const
     const double S1 = D[l - 2] / D[l] * ((double)e->q[l] / D[l]) * (double)e->q[l - 1];
     const i64 R = llround(D[l]);
     const int per = nx * ny, N = e->N;
+    double rx[16], ry[16];
+    rx[0] = ry[0] = 1.0;
+    for (int i = 1; i < nx; i++) rx[i] = D[l] / D[xb[i - 1]->level];
+    for (int j = 1; j < ny; j++) ry[j] = D[l] / D[yb[j - 1]->level];
     aesfhe_ct *al[32];
-    for (int a = 0; a < na; a++) al[a] = level_down_raw(e, all[a], l);
+    for (int a = 0; a < na; a++) al[a] = truncate_ct(e, all[a], l);
     aesfhe_ct **X = al, **Y = al + (nx - 1);
     i64 *A = malloc(sizeof(i64) * per), *Bc = malloc(sizeof(i64) * per);
     for (int t = 0; t < m; t++) {
         int any = 0;
         for (int c = 0; c < per; c++) {
-            A[c] = llround(re[(size_t)t * per + c] * S1);
-            Bc[c] = llround(im[(size_t)t * per + c] * S1);
+            A[c] = llround(re[(size_t)t * per + c] * S1 * rx[c / ny] * ry[c % ny]);
+            Bc[c] = llround(im[(size_t)t * per + c] * S1 * rx[c / ny] * ry[c % ny]);
             if (A[c] || Bc[c]) any = 1;
         }
         if (!any) {
