@@ -21,6 +21,7 @@
 #include "../../include/aesfhe.h"
 #include "kernels_ops.h"
 #include "ntt256.h"
+#include "ntt256f.h"
 
 using namespace aesfhe;
 
@@ -361,9 +362,24 @@ static void ntt_inv_t(aesfhe_engine* e, Span src, Span dst, int total) {
 }
 
 // N = 2^16: register-resident radix-16x16 passes (ntt256.h)
+static bool g_ntt_int = getenv("AESFHE_NTT_INT") != nullptr;  // integer-arithmetic passes (A/B)
+
 static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
     Tabs T = e->tabs();
+    // algorithmic bytes per pass: 8 B * N * limbs = half of the transform's read-once +
+    // write-once 16 B per coefficient (the two-pass split itself is charged as overhead)
     const double by = 8.0 * e->N * (double)total;
+    if (!g_ntt_int) {  // fp64-arithmetic passes (ntt256f.h)
+        {
+            ProfScope ps(e, FAM_NTT, by);
+            if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
+            else hipLaunchKernelGGL(k_nttf_inv_rows, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
+        }
+        ProfScope ps(e, FAM_NTT, by);
+        if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_rows, dim3(16, total), dim3(256), 0, e->stream, dst, T);
+        else hipLaunchKernelGGL(k_nttf_inv_cols, dim3(16, total), dim3(256), 0, e->stream, dst, T);
+        return;
+    }
     if (!inverse) {
         {
             ProfScope ps(e, FAM_NTT, by);

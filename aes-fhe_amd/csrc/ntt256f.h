@@ -1,0 +1,286 @@
+// ntt256f.h -- fp64-arithmetic NTT passes for N = 2^16 (= 256 x 256), the BASELINE.json ring.
+//
+// Same data movement as ntt256.h (register-resident 256-point sub-transforms, 16 lanes x 16
+// registers, one LDS transpose per pass), but every residue is carried as an exact integer in
+// a double and every butterfly is full-rate fp64 (fmul_rem, kernels.h): ~11 VALU ops instead of
+// ~30 mixed integer ops with six quarter-rate 32-bit multiplies.  Twiddles are read as w/q only
+// (8 B, Tabs::psif / ipsif) and w = rint(wq * q) is recovered exactly (|wq*q - w| < 2^-4).
+//
+// Ranges (fmul_rem needs |input| < 2^51, fred needs |x| < 2^53):
+//   forward CT   x' = x + v, y' = x - v with v in (-q, q): +q per stage.  Primes < 2^42 grow
+//                to at most 17q over both passes; larger primes are folded (fred, |x| <= q/2+1)
+//                before every second stage (fmul_rem inputs <= 2q).
+//   inverse GS   x' = x + y doubles per stage, y' = (x - y) w in (-q, q): primes < 2^42 reach
+//                at most 2^8 q per pass (the column pass starts folded); for larger primes the
+//                sum output is folded in every butterfly (inputs <= q, differences <= 2q).
+// The branch on the prime size is block-uniform (one prime per block).  Between the two passes
+// of a transform the intermediate is stored as raw doubles; final outputs are canonical u64
+// residues in [0, q), so results are identical to ntt256.h and to the oracle residue for residue.
+#pragma once
+#include <type_traits>
+
+#include "kernels.h"
+
+namespace aesfhe {
+
+constexpr double kBigPrime = 4398046511104.0;  // 2^42
+
+__device__ __forceinline__ double tw_w(double wq, double q) {
+    return __builtin_fma(wq, q, kMagic52) - kMagic52;
+}
+__device__ __forceinline__ void ct_f(double& x, double& y, double wq, double q) {
+    const double v = fmul_rem(y, tw_w(wq, q), wq, q);
+    const double t = x;
+    x = t + v;
+    y = t - v;
+}
+template <bool FOLD>
+__device__ __forceinline__ void gs_f(double& x, double& y, double wq, double q, double qi) {
+    const double s = x + y, d = x - y;
+    x = FOLD ? fred(s, q, qi) : s;
+    y = fmul_rem(d, tw_w(wq, q), wq, q);
+}
+__device__ __forceinline__ double ld_d(const u64* p) { return __longlong_as_double((long long)*p); }
+__device__ __forceinline__ void st_d(u64* p, double v) { *p = (u64)__double_as_longlong(v); }
+
+constexpr int kPadF = 17;  // LDS row stride (8 B words) of the 16 x 16 transpose tiles
+
+// Forward, column pass: stages m = 1..128 on columns of stride 256; canonical u64 in, raw
+// doubles out.  Workgroup = 16 columns [c0, c0+16); lane (cl, b) = (tid & 15, tid >> 4).
+__global__ __launch_bounds__(256) void k_nttf_fwd_cols(Span src, Span dst, Tabs T) {
+    __shared__ double s[256 * kPadF];
+    __shared__ double twq[256];
+    int pid;
+    const u64* in = span_ptr(src, blockIdx.y, T.logN, T.Lp1, pid);
+    u64* out = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
+    const int tid = threadIdx.x, cl = tid & 15, b = tid >> 4;
+    const int c = blockIdx.x * 16 + cl;
+    const double q = (double)T.q[pid], qi = T.qinv[pid];
+    const bool big = q >= kBigPrime;
+    const double* tg = T.psif + ((long)pid << T.logN);
+    twq[tid] = tg[tid];
+    double x[16];
+#pragma unroll
+    for (int a = 0; a < 16; a++) x[a] = u2d(in[(a * 16 + b) * 256 + c]);
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < 4; st++) {
+        const int m = 1 << st, h = 8 >> st;
+        if (big && st == 2) {
+#pragma unroll
+            for (int a = 0; a < 16; a++) x[a] = fred(x[a], q, qi);
+        }
+#pragma unroll
+        for (int a = 0; a < 16; a++) {
+            if (a & h) continue;
+            ct_f(x[a], x[a + h], tg[m + (a >> (4 - st))], q);  // uniform: scalar load
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 16; a++) s[(a * 16 + b) * kPadF + cl] = x[a];
+    __syncthreads();
+    const int ap = b;
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) x[bb] = s[(ap * 16 + bb) * kPadF + cl];
+#pragma unroll
+    for (int st = 4; st < 8; st++) {
+        const int m = 1 << st, h = 128 >> st;
+        if (big && (st & 1) == 0) {
+#pragma unroll
+            for (int bb = 0; bb < 16; bb++) x[bb] = fred(x[bb], q, qi);
+        }
+#pragma unroll
+        for (int bb = 0; bb < 16; bb++) {
+            if (bb & h) continue;
+            ct_f(x[bb], x[bb + h], twq[m + ap * (m >> 4) + (bb >> (8 - st))], q);
+        }
+    }
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) st_d(&out[(ap * 16 + bb) * 256 + c], x[bb]);
+}
+
+// Forward, row pass: stages m = 256..32768 within rows of 256 contiguous elements; raw doubles
+// in, canonical u64 out.  Workgroup = 16 rows [r0, r0+16); lane (b, rl) = (tid & 15, tid >> 4).
+__global__ __launch_bounds__(256) void k_nttf_fwd_rows(Span dst, Tabs T) {
+    __shared__ double s[16 * 16 * kPadF];
+    int pid;
+    u64* io = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
+    const int tid = threadIdx.x, b = tid & 15, rl = tid >> 4;
+    const int row = blockIdx.x * 16 + rl;
+    const double q = (double)T.q[pid], qi = T.qinv[pid];
+    const bool big = q >= kBigPrime;
+    const double* W = T.psif + ((long)pid << T.logN);
+    u64* rp = io + (long)row * 256;
+    double x[16];
+#pragma unroll
+    for (int a = 0; a < 16; a++) x[a] = ld_d(&rp[a * 16 + b]);
+#pragma unroll
+    for (int st = 0; st < 4; st++) {
+        const int ml = 1 << st, h = 8 >> st;
+        const int base = ml * (256 + row);
+        if (big && (st & 1) == 0) {
+#pragma unroll
+            for (int a = 0; a < 16; a++) x[a] = fred(x[a], q, qi);
+        }
+#pragma unroll
+        for (int a = 0; a < 16; a++) {
+            if (a & h) continue;
+            ct_f(x[a], x[a + h], W[base + (a >> (4 - st))], q);
+        }
+    }
+    double* sr = s + rl * 16 * kPadF;
+#pragma unroll
+    for (int a = 0; a < 16; a++) sr[a * kPadF + b] = x[a];
+    __syncthreads();
+    const int ap = b;
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) x[bb] = sr[ap * kPadF + bb];
+#pragma unroll
+    for (int st = 4; st < 8; st++) {
+        const int ml = 1 << st, h = 128 >> st;
+        const int base = ml * (256 + row) + ap * (ml >> 4);
+        if (big && (st & 1) == 0) {
+#pragma unroll
+            for (int bb = 0; bb < 16; bb++) x[bb] = fred(x[bb], q, qi);
+        }
+#pragma unroll
+        for (int bb = 0; bb < 16; bb++) {
+            if (bb & h) continue;
+            ct_f(x[bb], x[bb + h], W[base + (bb >> (8 - st))], q);
+        }
+    }
+    // coalesced store through LDS: canonical residues, then row-major copy-out
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) sr[ap * kPadF + bb] = __longlong_as_double((long long)fcanon(x[bb], q, qi));
+    __syncthreads();
+    u64* base = io + (long)blockIdx.x * 16 * 256;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
+        base[e] = (u64)__double_as_longlong(s[r * 16 * kPadF + (cc >> 4) * kPadF + (cc & 15)]);
+    }
+}
+
+// Inverse, row pass (Gentleman-Sande, distances 1..128 within rows): canonical u64 in (src),
+// raw doubles out (dst).
+__global__ __launch_bounds__(256) void k_nttf_inv_rows(Span src, Span dst, Tabs T) {
+    __shared__ double s[16 * 16 * kPadF];
+    int pid;
+    const u64* in = span_ptr(src, blockIdx.y, T.logN, T.Lp1, pid);
+    u64* out = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
+    const int tid = threadIdx.x, b = tid & 15, rl = tid >> 4;
+    const int row = blockIdx.x * 16 + rl;
+    const double q = (double)T.q[pid], qi = T.qinv[pid];
+    const bool big = q >= kBigPrime;
+    const double* W = T.ipsif + ((long)pid << T.logN);
+    const int N = 1 << T.logN;
+    const u64* gb = in + (long)blockIdx.x * 16 * 256;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
+        s[r * 16 * kPadF + (cc >> 4) * kPadF + (cc & 15)] = u2d(gb[e]);
+    }
+    __syncthreads();
+    double* sr = s + rl * 16 * kPadF;
+    const int ap = b;
+    double x[16];
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) x[bb] = sr[ap * kPadF + bb];
+    auto stages_lo = [&](auto fold) {
+#pragma unroll
+        for (int st = 0; st < 4; st++) {
+            const int t = 1 << st;
+            const int base = N / (2 * t) + row * (128 / t) + ap * (8 / t);
+#pragma unroll
+            for (int bb = 0; bb < 16; bb++) {
+                if (bb & t) continue;
+                gs_f<decltype(fold)::value>(x[bb], x[bb + t], W[base + (bb >> (st + 1))], q, qi);
+            }
+        }
+    };
+    if (big) stages_lo(std::true_type{});
+    else stages_lo(std::false_type{});
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) sr[ap * kPadF + bb] = x[bb];
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 16; a++) x[a] = sr[a * kPadF + b];
+    auto stages_hi = [&](auto fold) {
+#pragma unroll
+        for (int st = 4; st < 8; st++) {
+            const int t = 1 << st, ta = t >> 4;
+            const int base = N / (2 * t) + row * (128 / t);
+#pragma unroll
+            for (int a = 0; a < 16; a++) {
+                if (a & ta) continue;
+                gs_f<decltype(fold)::value>(x[a], x[a + ta], W[base + (a >> (st - 3))], q, qi);
+            }
+        }
+    };
+    if (big) stages_hi(std::true_type{});
+    else stages_hi(std::false_type{});
+    u64* op = out + (long)row * 256;
+#pragma unroll
+    for (int a = 0; a < 16; a++) st_d(&op[a * 16 + b], x[a]);
+}
+
+// Inverse, column pass (distances 256..32768 = rows 1..128) and the N^{-1} scaling: raw
+// doubles in, canonical u64 out.
+__global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T) {
+    __shared__ double s[256 * kPadF];
+    __shared__ double twq[256];
+    int pid;
+    u64* io = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
+    const int tid = threadIdx.x, cl = tid & 15, b = tid >> 4;
+    const int c = blockIdx.x * 16 + cl;
+    const double q = (double)T.q[pid], qi = T.qinv[pid];
+    const bool big = q >= kBigPrime;
+    const double* tg = T.ipsif + ((long)pid << T.logN);
+    twq[tid] = tg[tid];
+    const int ap = b;
+    double x[16];
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) x[bb] = fred(ld_d(&io[(ap * 16 + bb) * 256 + c]), q, qi);
+    __syncthreads();
+    auto stages_lo = [&](auto fold) {
+#pragma unroll
+        for (int st = 0; st < 4; st++) {
+            const int tr = 1 << st;
+            const int base = 128 / tr + ap * (8 / tr);
+#pragma unroll
+            for (int bb = 0; bb < 16; bb++) {
+                if (bb & tr) continue;
+                gs_f<decltype(fold)::value>(x[bb], x[bb + tr], twq[base + (bb >> (st + 1))], q, qi);
+            }
+        }
+    };
+    if (big) stages_lo(std::true_type{});
+    else stages_lo(std::false_type{});
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) s[(ap * 16 + bb) * kPadF + cl] = x[bb];
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 16; a++) x[a] = s[(a * 16 + b) * kPadF + cl];
+    auto stages_hi = [&](auto fold) {
+#pragma unroll
+        for (int st = 4; st < 8; st++) {
+            const int tr = 1 << st, ta = tr >> 4;
+            const int base = 128 / tr;
+#pragma unroll
+            for (int a = 0; a < 16; a++) {
+                if (a & ta) continue;
+                gs_f<decltype(fold)::value>(x[a], x[a + ta], tg[base + (a >> (st - 3))], q, qi);  // uniform
+            }
+        }
+    };
+    if (big) stages_hi(std::true_type{});
+    else stages_hi(std::false_type{});
+    const double ni = (double)T.ninv[pid], nif = T.ninvf[pid];
+#pragma unroll
+    for (int a = 0; a < 16; a++) {
+        const double r = fred(x[a], q, qi);
+        io[(a * 16 + b) * 256 + c] = fcanon(fmul_rem(r, ni, nif, q), q, qi);
+    }
+}
+
+}  // namespace aesfhe
