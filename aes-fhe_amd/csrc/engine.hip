@@ -1235,10 +1235,9 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
         // 2. ModUp base conversion of digit j to every other limb, then NTT those limbs
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
-            hipLaunchKernelGGL(k_modup, dim3(N / 256, (ne + 7) / 8, B), dim3(256), 0, e->stream, (const u64*)dc.p, lN, exj, neN, lo, alpha, l, ne,
-                               (const u64*)(e->mu_hatinv + set * K), (const double*)(e->mu_hatinvf + set * K),
-                               (const u64*)(e->mu_hat + set * K * e->np), (const double*)(e->mu_hatf + set * K * e->np),
-                               e->np, e->q, e->Lp1, e->logN);
+            hipLaunchKernelGGL(k_modup, dim3(N / 256, (ne + 15) / 16, B), dim3(256), 0, e->stream, (const u64*)dc.p, lN, exj, neN, lo, alpha, l, ne,
+                               (const double*)(e->mu_hatinvf + set * K), (const double*)(e->mu_hatf + set * K * e->np),
+                               e->np, e->q, e->qinv, e->Lp1, e->logN);
         }
         HIPC(hipGetLastError());
         if (lo > 0) {
@@ -1265,8 +1264,8 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
     Tmp conv(e, (size_t)B * 2 * lN);
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + l + 1));
-        hipLaunchKernelGGL(k_moddown, dim3(N / 256, (l + 1 + 7) / 8, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, conv.p, 2 * lN, lN, K,
-                           (const u64*)e->md_phatinv, (const double*)e->md_phatinvf, (const u64*)e->md_phat, (const double*)e->md_phatf, e->Lp1, e->q, e->logN);
+        hipLaunchKernelGGL(k_moddown, dim3(N / 256, (l + 1 + 15) / 16, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, conv.p, 2 * lN, lN, K,
+                           (const double*)e->md_phatinvf, (const double*)e->md_phatf, e->Lp1, e->q, e->qinv, e->logN);
     }
     HIPC(hipGetLastError());
     {

@@ -80,6 +80,10 @@ __device__ __forceinline__ u64 fcanon(double x, double q, double qinv) {
     r = r >= q ? r - q : r;
     return (u64)r;
 }
+// w from its table entry wq = w/q (w < q < 2^52): rint(wq * q) is exact, |wq*q - w| < 2^-4
+__device__ __forceinline__ double tw_w(double wq, double q) {
+    return __builtin_fma(wq, q, kMagic52) - kMagic52;
+}
 struct alignas(16) TwD {
     double w;   // constant as an exact double (< 2^52)
     double wq;  // w / q

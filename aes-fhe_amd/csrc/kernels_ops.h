@@ -239,36 +239,45 @@ __global__ void k_rescale_finish_g(const u64* __restrict__ c, long cps, const u6
     outs[g][(long)rem * ops + ((long)i << logN) + k] = mul_w(sub_m(cv, tv, q), inv[i], invf[i], q);
 }
 
-// ---------------------------------------------------------------------------------------------
-// hybrid key switching
-// ModUp fast base conversion of one digit: dc[b][i][k] (coef, i in [lo, lo+alpha)) to every
-// extended limb t in [0, ne) outside the digit.  ext[b][t][k].  grid (N/256, ceil(ne/8), B)
-// hatinv/hatinvf: [alpha]; hat/hatf: [alpha][np] (row stride np)
+// ModUp base conversion of digit [lo, lo+alpha) (INTT'ed limbs of dc) to the other limbs t of
+// the extended basis (Q_l then P), exact fp64 arithmetic (kernels.h fmul_rem):
+//   y_i = [x_i * qhat_i^{-1}]_{q_i} in [0, q_i) (canonical, so the multiple of Q that the fast
+//   conversion adds is the oracle's), ext[t] = sum_i y_i * (qhat_i mod p_t) mod p_t.
+// Constants come from their w/q tables (w = rint(wq * q) is exact).  grid (N/256,
+// ceil(ne/16), B): each thread converts one coefficient into up to 16 target limbs.
 __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ ext, long exs,
-                        int lo, int alpha, int l, int ne, const u64* __restrict__ hatinv,
-                        const double* __restrict__ hatinvf, const u64* __restrict__ hat,
+                        int lo, int alpha, int l, int ne, const double* __restrict__ hatinvf,
                         const double* __restrict__ hatf, int np, const u64* __restrict__ qall,
-                        int Lp1, int logN) {
+                        const double* __restrict__ qinvall, int Lp1, int logN) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int bb = blockIdx.z;
-    u64 y[16];
+    double y[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) {
+        y[i] = 0.0;
         if (i < alpha) {
             const int pi = lo + i;
-            y[i] = mul_w(dc[(long)bb * dcs + ((long)pi << logN) + k], hatinv[i], hatinvf[i], qall[pi]);
+            const double qp = (double)qall[pi];
+            const double f = hatinvf[i];
+            double r = fmul_rem(u2d(dc[(long)bb * dcs + ((long)pi << logN) + k]), tw_w(f, qp), f, qp);
+            y[i] = r < 0.0 ? r + qp : r;
         }
     }
-    const int t0 = blockIdx.y * 8;
-    for (int t = t0; t < t0 + 8 && t < ne; t++) {
+    const int t0 = blockIdx.y * 16;
+    for (int t = t0; t < t0 + 16 && t < ne; t++) {
         if (t >= lo && t < lo + alpha) continue;
         const int pid = t <= l ? t : Lp1 + (t - l - 1);
-        const u64 qt = qall[pid];
-        u64 s = 0;
+        const double qt = (double)qall[pid], qti = qinvall[pid];
+        double acc = 0.0;
 #pragma unroll
-        for (int i = 0; i < 16; i++)
-            if (i < alpha) s = add_m(s, mul_w(y[i], hat[i * np + pid], hatf[i * np + pid], qt), qt);
-        ext[(long)bb * exs + ((long)t << logN) + k] = s;
+        for (int i = 0; i < 16; i++) {
+            if (i < alpha) {
+                const double f = hatf[i * np + pid];
+                acc += fmul_rem(y[i], tw_w(f, qt), f, qt);
+                if ((i & 3) == 3) acc = fred(acc, qt, qti);
+            }
+        }
+        ext[(long)bb * exs + ((long)t << logN) + k] = fcanon(acc, qt, qti);
     }
 }
 
@@ -312,58 +321,77 @@ __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* _
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int t = blockIdx.y;
     const int pid = t <= l ? t : Lp1 + (t - l - 1);
-    const u64 q = qall[pid];
+    const double q = (double)qall[pid];
     const double qi = qinvall[pid];
     const int own = t <= l ? t / K : -1;  // the digit whose limbs include t (Q limbs only)
-    u64 kb[12], ka[12];
+    double kb[12], ka[12], kbq[12], kaq[12];
 #pragma unroll
     for (int j = 0; j < 12; j++) {
+        kb[j] = ka[j] = kbq[j] = kaq[j] = 0.0;
         if (j < beta) {
             const long ko = (long)j * kdig + ((long)pid << logN) + k;
-            kb[j] = key[ko];
-            ka[j] = key[ko + kcomp];
+            kb[j] = u2d(key[ko]);
+            ka[j] = u2d(key[ko + kcomp]);
+            kbq[j] = kb[j] * qi;
+            kaq[j] = ka[j] * qi;
         }
     }
     for (int bb = 0; bb < B; bb++) {
-        u64 s0 = 0, s1 = 0;
+        double s0 = 0.0, s1 = 0.0;
 #pragma unroll
         for (int j = 0; j < 12; j++) {
             if (j < beta) {
-                const u64 e = (j == own) ? d[(long)bb * dbs + ((long)t << logN) + k]
-                                         : ext[(long)j * exj + (long)bb * exs + ((long)t << logN) + k];
-                s0 += mul_m(e, kb[j], q, qi);
-                s1 += mul_m(e, ka[j], q, qi);
+                const double e = u2d((j == own) ? d[(long)bb * dbs + ((long)t << logN) + k]
+                                                : ext[(long)j * exj + (long)bb * exs + ((long)t << logN) + k]);
+                s0 += fmul_rem(e, kb[j], kbq[j], q);
+                s1 += fmul_rem(e, ka[j], kaq[j], q);
+                if ((j & 3) == 3) {
+                    s0 = fred(s0, q, qi);
+                    s1 = fred(s1, q, qi);
+                }
             }
         }
         u64* a0 = acc + (long)bb * abs_ + ((long)t << logN) + k;
-        a0[0] = red_m(s0, q, qi);
-        a0[acs] = red_m(s1, q, qi);
+        a0[0] = fcanon(s0, q, qi);
+        a0[acs] = fcanon(s1, q, qi);
     }
 }
 
 // ModDown base conversion P -> Q_l: acc special limbs already in coefficient form.
 // conv[b][c][i][k] = sum_k' (z_k' * Phatinv_k' mod p_k') * Phat[k'][i] mod q_i
-// grid (N/256, ceil((l+1)/8), B*2)
+// grid (N/256, ceil((l+1)/16), B*2)
 __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int l,
                           u64* __restrict__ conv, long cbs, long ccs, int K,
-                          const u64* __restrict__ phatinv, const double* __restrict__ phatinvf,
-                          const u64* __restrict__ phat, const double* __restrict__ phatf,
-                          int Lp1, const u64* __restrict__ qall, int logN) {
+                          const double* __restrict__ phatinvf, const double* __restrict__ phatf,
+                          int Lp1, const u64* __restrict__ qall, const double* __restrict__ qinvall,
+                          int logN) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int bb = blockIdx.z >> 1, c = blockIdx.z & 1;
     const u64* src = acc + (long)bb * abs_ + (long)c * acs;
-    u64 y[16];
+    double y[16];
 #pragma unroll
-    for (int j = 0; j < 16; j++)
-        if (j < K) y[j] = mul_w(src[((long)(l + 1 + j) << logN) + k], phatinv[j], phatinvf[j], qall[Lp1 + j]);
-    const int i0 = blockIdx.y * 8;
-    for (int i = i0; i < i0 + 8 && i <= l; i++) {
-        const u64 q = qall[i];
-        u64 s = 0;
+    for (int j = 0; j < 16; j++) {
+        y[j] = 0.0;
+        if (j < K) {
+            const double pp = (double)qall[Lp1 + j];
+            const double f = phatinvf[j];
+            const double r = fmul_rem(u2d(src[((long)(l + 1 + j) << logN) + k]), tw_w(f, pp), f, pp);
+            y[j] = r < 0.0 ? r + pp : r;  // canonical: the oracle's conversion
+        }
+    }
+    const int i0 = blockIdx.y * 16;
+    for (int i = i0; i < i0 + 16 && i <= l; i++) {
+        const double q = (double)qall[i], qi = qinvall[i];
+        double s = 0.0;
 #pragma unroll
-        for (int j = 0; j < 16; j++)
-            if (j < K) s = add_m(s, mul_w(y[j], phat[j * Lp1 + i], phatf[j * Lp1 + i], q), q);
-        conv[(long)bb * cbs + (long)c * ccs + ((long)i << logN) + k] = s;
+        for (int j = 0; j < 16; j++) {
+            if (j < K) {
+                const double f = phatf[j * Lp1 + i];
+                s += fmul_rem(y[j], tw_w(f, q), f, q);
+                if ((j & 3) == 3) s = fred(s, q, qi);
+            }
+        }
+        conv[(long)bb * cbs + (long)c * ccs + ((long)i << logN) + k] = fcanon(s, q, qi);
     }
 }
 

@@ -25,9 +25,6 @@ namespace aesfhe {
 
 constexpr double kBigPrime = 4398046511104.0;  // 2^42
 
-__device__ __forceinline__ double tw_w(double wq, double q) {
-    return __builtin_fma(wq, q, kMagic52) - kMagic52;
-}
 __device__ __forceinline__ void ct_f(double& x, double& y, double wq, double q) {
     const double v = fmul_rem(y, tw_w(wq, q), wq, q);
     const double t = x;
