@@ -147,7 +147,7 @@ struct aesfhe_engine {
     // aesfhe_poly2 constant tables, keyed by (level, shape, coefficients)
     std::map<std::string, TwD*> poly2_tabs;
     // profiling
-    bool prof = false;
+    int prof = 0;  // bitmask of recorded families (1 << FAM_*)
     std::vector<ProfRec> recs;
     std::vector<hipEvent_t> spare;
     double prof_ms[4] = {0, 0, 0, 0};
@@ -204,8 +204,9 @@ struct ProfScope {
     int fam;
     double bytes;
     hipEvent_t a = nullptr, b = nullptr;
-    ProfScope(aesfhe_engine* e_, int f, double by) : e(e_), fam(f), bytes(by) {
-        if (!e->prof) return;
+    bool on;
+    ProfScope(aesfhe_engine* e_, int f, double by) : e(e_), fam(f), bytes(by), on((e_->prof >> f) & 1) {
+        if (!on) return;
         a = take();
         b = take();
         hipEventRecord(a, e->stream);
@@ -221,7 +222,7 @@ struct ProfScope {
         return x;
     }
     ~ProfScope() {
-        if (!e->prof) return;
+        if (!on) return;
         hipEventRecord(b, e->stream);
         e->recs.push_back({fam, a, b, bytes});
     }
@@ -661,9 +662,16 @@ extern "C" int aesfhe_engine_sync(aesfhe_engine* e) {
 extern "C" int aesfhe_engine_profile(aesfhe_engine* e, int32_t en) {
     API_BEGIN
     prof_flush(e);
-    e->prof = en != 0;
-    if (en)
+    e->prof = en == -1 ? 7 : (en & 7);
+    if (e->prof) {
         for (int i = 0; i < 4; i++) e->prof_ms[i] = e->prof_bytes[i] = 0, e->prof_n[i] = 0;
+        // pre-create events so that none is created inside a measured region
+        while (e->spare.size() < 65536) {
+            hipEvent_t x;
+            HIPC(hipEventCreate(&x));
+            e->spare.push_back(x);
+        }
+    }
     API_END
 }
 extern "C" int aesfhe_engine_profile_read(aesfhe_engine* e, const char* fam, int64_t* n,

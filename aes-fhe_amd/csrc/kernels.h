@@ -68,6 +68,16 @@ __device__ __forceinline__ double fmul_rem(double a, double w, double wq, double
     const double tl = __builtin_fma(qh, q, -t);
     return (p - t) + (pl - tl);
 }
+// Same remainder with the quotient from v_rndne_f64 (no 2^52 literal: the SGPR operands w, wq
+// then fit the single constant-bus slot of a VOP3).  |a*wq - a*w/q| <= 1/2 -> |r| <= q.
+__device__ __forceinline__ double fmul_rem_r(double a, double w, double wq, double q) {
+    const double p = a * w;
+    const double pl = __builtin_fma(a, w, -p);
+    const double qh = __builtin_rint(a * wq);
+    const double t = qh * q;
+    const double tl = __builtin_fma(qh, q, -t);
+    return (p - t) + (pl - tl);
+}
 // x - rint(x/q)*q for |x| < 2^53: result in [-q/2 - 1, q/2 + 1] (exact: qh*q < 2^53)
 __device__ __forceinline__ double fred(double x, double q, double qinv) {
     const double qh = __builtin_fma(x, qinv, kMagic52) - kMagic52;

@@ -538,18 +538,18 @@ __global__ void k_square(const u64* __restrict__ s, u64* __restrict__ o,
 }
 
 // Bivariate polynomial evaluation with shared power bases (aesfhe_poly2).  For outputs
-// t0 <= t < t0 + mc (mc <= 8) and element (batch bb, limb l, coefficient k):
+// t0 <= t < t0 + mc (mc <= kPoly2Out) and element (batch bb, limb l, coefficient k):
 //   a_{t,i} = F[t,i,0] + sum_{j>=1} F[t,i,j] * y^j       (inner sums, never rescaled)
 //   d_t     = (a_{t,0}, a'_{t,0}, 0) + sum_{i>=1} x^i (x) a_{t,i}
 // F: TwD table [nl][half][mtot][nx][ny]; the j = 0 entries are additive constants, the i = 0
 // row already carries the factor R = round(Delta_l) of the implicit x^0 ciphertext.
 // All arithmetic is exact integer arithmetic in fp64 (fmul_rem / fred): signed residues in
-// (-q, q), sums folded back below 2^53 every 5 terms.  The y basis lives in registers (as
+// [-q, q], sums folded back below 2^53 every 4 terms.  The y basis lives in registers (as
 // doubles), x^i is loaded once per i (outer loop), the mc output accumulators stay in
 // registers.  x/y: pointer, batch-stride and poly-stride arrays of 2-poly ciphertexts at level
 // >= nl-1 (only limbs 0..nl-1 are read: truncation).  out: [mtot][B][3][nl][N] (output t at
 // out + t*oos).  grid (N/256, nl, B)
-constexpr int kPoly2Max = 16, kPoly2Out = 8;
+constexpr int kPoly2Max = 16, kPoly2Out = 4;
 __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
                         const long* __restrict__ xps, int nx, const u64* const* __restrict__ yp,
                         const long* __restrict__ ybs, const long* __restrict__ yps, int ny,
@@ -593,9 +593,9 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
                 for (int j = 1; j < kPoly2Max; j++) {
                     if (j < ny) {
                         const TwD f = Fi[j];
-                        a0 += fmul_rem(y0[j - 1], f.w, f.wq, q);
-                        a1 += fmul_rem(y1[j - 1], f.w, f.wq, q);
-                        if (j == 5 || j == 10) {  // keep |sum| <= q/2 + 5q < 2^53
+                        a0 += fmul_rem_r(y0[j - 1], f.w, f.wq, q);
+                        a1 += fmul_rem_r(y1[j - 1], f.w, f.wq, q);
+                        if ((j & 3) == 0) {  // keep |sum| <= q/2 + 4q + q < 2^53
                             a0 = fred(a0, q, qi);
                             a1 = fred(a1, q, qi);
                         }

@@ -181,7 +181,7 @@ def main():
             dist.barrier()
 
     import ctypes as C
-    eng._check(eng._lib.engine_profile(eng._h, 1))
+    eng._check(eng._lib.engine_profile(eng._h, 1 | 2))  # ntt + keyswitch families only
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):

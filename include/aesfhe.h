@@ -100,7 +100,8 @@ int aesfhe_engine_scales(const aesfhe_engine *eng, double *scales_out);
 double aesfhe_engine_mul_scale(const aesfhe_engine *eng, int32_t level);
 int aesfhe_engine_sync(aesfhe_engine *eng);
 /* Per-kernel-family timing (HIP events on the engine stream; CPU wall time in the oracle).
- * family: "ntt" | "keyswitch" | "elementwise" | "all".  enable=1 starts recording, 0 stops. */
+ * family: "ntt" | "keyswitch" | "elementwise" | "all".  enable: bitmask of the families to
+ * record (1 ntt, 2 keyswitch, 4 elementwise; -1 all), 0 stops.  Enabling resets the counters. */
 int aesfhe_engine_profile(aesfhe_engine *eng, int32_t enable);
 int aesfhe_engine_profile_read(aesfhe_engine *eng, const char *family, int64_t *launches,
                                double *total_ms, double *bytes);

@@ -386,7 +386,7 @@ static void ntt_inv(const aesfhe_engine *e, u64 *a, int p) {
 }
 
 static void prof_add(aesfhe_engine *e, int fam, double ms) {
-    if (!e->profiling) return;
+    if (!((e->profiling >> fam) & 1)) return;
     e->prof_ms[fam] += ms;
     e->prof_n[fam] += 1;
 }
@@ -477,7 +477,7 @@ int aesfhe_engine_sync(aesfhe_engine *e) {
     return 0;
 }
 int aesfhe_engine_profile(aesfhe_engine *e, int32_t en) {
-    e->profiling = en;
+    e->profiling = en == -1 ? 7 : (en & 7);
     if (en) {
         memset(e->prof_ms, 0, sizeof e->prof_ms);
         memset(e->prof_n, 0, sizeof e->prof_n);
