@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=4, help="ciphertext sets per GPU per step")
+    ap.add_argument("--batch", type=int, default=16, help="ciphertext sets per GPU per step")
     ap.add_argument("--layout", choices=("rows", "bytes"), default="rows")
     ap.add_argument("--log-n", type=int, default=16)
     ap.add_argument("--max-level", type=int, default=30)
