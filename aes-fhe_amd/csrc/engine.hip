@@ -139,6 +139,10 @@ struct aesfhe_engine {
     std::vector<u64> h_iroot;
     // base conversion tables
     u64 *mu_hatinv, *mu_hat, *md_phatinv, *md_phat, *md_pinv, *rs_inv, *rs_mod, *pmod;
+    // combined ModDown + rescale (drop r = 1, 2 top Q primes with P), see build_tables
+    double *mdr_invf = nullptr, *mdr_hatf = nullptr, *mdr_dinvf = nullptr, *pmodf = nullptr;
+    double *mdr_einv = nullptr, *mdr_dmodf = nullptr;
+    u64* mdr_dinv = nullptr;
     double *mu_hatinvf, *mu_hatf, *md_phatinvf, *md_phatf, *md_pinvf, *rs_invf;
     // small-argument upload ring (device) + pinned staging
     char* ring_d = nullptr;
@@ -198,6 +202,7 @@ struct aesfhe_pt {
 // -----------------------------------------------------------------------------------------------
 // helpers
 static const int FAM_NTT = 0, FAM_KS = 1, FAM_EW = 2;
+static const int kMdrMaxR = 2, kMdrMaxE = 16;  // combined ModDown + rescale: r <= 2, K + r <= 16
 
 struct ProfScope {
     aesfhe_engine* e;
@@ -553,6 +558,58 @@ static void build_tables(aesfhe_engine* e) {
     up(hpinv, &e->md_pinv);
     up(hpinvf, &e->md_pinvf);
     up(hpmod, &e->pmod);
+    {
+        std::vector<double> hpmodf(Lp1);
+        for (int i = 0; i < Lp1; i++) hpmodf[i] = (double)hpmod[i] / (double)Q[i];
+        up(hpmodf, &e->pmodf);
+    }
+    // combined ModDown + rescale: E = {q_{l-r+1}..q_l, p_0..p_{K-1}} (acc limb order), D = prod E
+    //   mdr_invf[(r-1, l)][j]       = (D/e_j)^{-1} mod e_j, as w/e_j
+    //   mdr_hatf[(r-1, l)][j][i]    = (D/e_j) mod q_i, as w/q_i   (i <= l - r)
+    //   mdr_dinv[(r-1, l)][i] (+f)  = D^{-1} mod q_i
+    {
+        const size_t cells = (size_t)kMdrMaxR * Lp1;
+        std::vector<double> hinvf(cells * kMdrMaxE, 0.0), hhatf(cells * kMdrMaxE * Lp1, 0.0), hdinvf(cells * Lp1, 0.0);
+        std::vector<u64> hdinv(cells * Lp1, 0);
+        std::vector<double> heinv(cells * kMdrMaxE, 0.0), hdmodf(cells * Lp1, 0.0);
+        for (int r = 1; r <= kMdrMaxR && K + r <= kMdrMaxE; r++)
+            for (int l = r; l <= L; l++) {
+                const size_t cell = (size_t)(r - 1) * Lp1 + l;
+                std::vector<int> E;
+                for (int j = 0; j < r; j++) E.push_back(l - r + 1 + j);
+                for (int j = 0; j < K; j++) E.push_back(Lp1 + j);
+                for (size_t j = 0; j < E.size(); j++) {
+                    const u64 ej = Q[E[j]];
+                    u64 prod = 1;
+                    for (size_t j2 = 0; j2 < E.size(); j2++)
+                        if (j2 != j) prod = h_mulmod(prod, Q[E[j2]] % ej, ej);
+                    hinvf[cell * kMdrMaxE + j] = (double)h_invmod(prod, ej) / (double)ej;
+                    heinv[cell * kMdrMaxE + j] = 1.0 / (double)ej;
+                    for (int i = 0; i <= l - r; i++) {
+                        const u64 qi = Q[i];
+                        u64 h = 1;
+                        for (size_t j2 = 0; j2 < E.size(); j2++)
+                            if (j2 != j) h = h_mulmod(h, Q[E[j2]] % qi, qi);
+                        hhatf[(cell * kMdrMaxE + j) * Lp1 + i] = (double)h / (double)qi;
+                    }
+                }
+                for (int i = 0; i <= l - r; i++) {
+                    const u64 qi = Q[i];
+                    u64 D = 1;
+                    for (int ei : E) D = h_mulmod(D, Q[ei] % qi, qi);
+                    const u64 di = h_invmod(D, qi);
+                    hdinv[cell * Lp1 + i] = di;
+                    hdmodf[cell * Lp1 + i] = (double)D / (double)qi;
+                    hdinvf[cell * Lp1 + i] = (double)di / (double)qi;
+                }
+            }
+        up(hinvf, &e->mdr_invf);
+        up(hhatf, &e->mdr_hatf);
+        up(hdinv, &e->mdr_dinv);
+        up(hdinvf, &e->mdr_dinvf);
+        up(heinv, &e->mdr_einv);
+        up(hdmodf, &e->mdr_dmodf);
+    }
 
     // rescale tables rs_inv[l][i] = q_l^{-1} mod q_i, rs_mod[l][i] = q_l mod q_i
     std::vector<u64> hrinv((size_t)Lp1 * Lp1, 0), hrmod((size_t)Lp1 * Lp1, 0);
@@ -626,7 +683,8 @@ extern "C" void aesfhe_engine_destroy(aesfhe_engine* e) {
     void* ptrs[] = {e->q, e->psi, e->ipsi, e->ninv, e->qinv, e->psif, e->ipsif, e->ninvf,
                     e->mu_hatinv, e->mu_hat, e->md_phatinv, e->md_phat, e->md_pinv, e->rs_inv,
                     e->rs_mod, e->pmod, e->mu_hatinvf, e->mu_hatf, e->md_phatinvf, e->md_phatf,
-                    e->md_pinvf, e->rs_invf, e->ring_d, e->tw, e->itw};
+                    e->md_pinvf, e->rs_invf, e->ring_d, e->tw, e->itw, e->mdr_invf, e->mdr_hatf,
+                    e->mdr_dinv, e->mdr_dinvf, e->pmodf, e->mdr_einv, e->mdr_dmodf};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto& kv : e->poly2_tabs) hipFree(kv.second);
@@ -1225,13 +1283,19 @@ extern "C" int aesfhe_mul_const(aesfhe_engine* e, const aesfhe_ct* c, double re,
 // -----------------------------------------------------------------------------------------------
 // key switching of one polynomial per batch element.
 // d: NTT-domain polynomial of batch element b at d + b*dbs (level l, limbs contiguous).
-// Result: out poly 0/1 = addend_{0/1} + KS(d)_{0/1}, written into ct `o` (2 polys, level l).
+// Result: out poly 0/1 = addend_{0/1} + KS(d)_{0/1}, written into ct `o` (2 polys, level l - r).
+// r = 0: plain ModDown by P.  r >= 1: combined ModDown + rescale -- P * addend joins the
+// accumulators in the inner product and one base conversion from E = {q_{l-r+1}..q_l, P} divides
+// by D = P q_l ... q_{l-r+1} (oracle/ckks_oracle.c moddown_r states the same procedure).
 static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, const aesfhe_key* k,
-                      Opnd addend, aesfhe_ct* o) {
+                      Opnd addend, aesfhe_ct* o, int r = 0) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long lN = (long)(l + 1) * N, neN = (long)ne * N;
     const int beta = (l + 1 + K - 1) / K;
     if (beta > 12) throw_err(AESFHE_EUNSUPPORTED, "more than 12 key-switch digits");
+    if (r < 0 || r > kMdrMaxR || K + r > kMdrMaxE || l - r < 0) throw_err(AESFHE_EARG, "bad combined rescale depth %d", r);
+    const int lk = l - r;  // output level
+    const long kN = (long)(lk + 1) * N;
     Tmp dc(e, (size_t)B * lN), ext(e, (size_t)beta * B * neN), acc(e, (size_t)B * 2 * neN);
     // 1. INTT copy of the input
     Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1), sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
@@ -1261,27 +1325,35 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
     // 3. inner product with every key digit in one pass
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B));
-        hipLaunchKernelGGL(k_ks_inner_all, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, (const u64*)ext.p, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, e->logN);
+        hipLaunchKernelGGL(k_ks_inner_all, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, (const u64*)ext.p, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, addend, r ? (const double*)e->pmodf : (const double*)nullptr, e->logN);
     }
     HIPC(hipGetLastError());
-    // 4. ModDown: INTT special limbs of both accumulators
+    // 4. ModDown: INTT the dropped limbs (top r Q limbs + the special limbs) of both accumulators
     {
-        Span ssp = span_s(acc.p + lN, neN, K, 0, 0, e->Lp1);
-        ntt(e, ssp, ssp, B * 2 * K, true);
+        Span ssp = span_s(acc.p + (long)(lk + 1) * N, neN, K + r, r, lk + 1, e->Lp1);
+        ntt(e, ssp, ssp, B * 2 * (K + r), true);
     }
-    Tmp conv(e, (size_t)B * 2 * lN);
+    const size_t cell = r ? (size_t)(r - 1) * e->Lp1 + l : 0;
+    const double* invf = r ? e->mdr_invf + cell * kMdrMaxE : e->md_phatinvf;
+    const double* hatf = r ? e->mdr_hatf + cell * kMdrMaxE * e->Lp1 : e->md_phatf;
+    const u64* dinv = r ? e->mdr_dinv + cell * e->Lp1 : e->md_pinv;
+    const double* dinvf = r ? e->mdr_dinvf + cell * e->Lp1 : e->md_pinvf;
+    Tmp conv(e, (size_t)B * 2 * kN);
     {
-        ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + l + 1));
-        hipLaunchKernelGGL(k_moddown, dim3(N / 256, (l + 1 + 15) / 16, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, conv.p, 2 * lN, lN, K,
-                           (const double*)e->md_phatinvf, (const double*)e->md_phatf, e->Lp1, e->q, e->qinv, e->logN);
+        ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1));
+        hipLaunchKernelGGL(k_moddown, dim3(N / 256, (lk + 1 + 15) / 16, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, r, conv.p, 2 * kN, kN, K,
+                           invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : (const double*)nullptr,
+                           r ? e->mdr_dmodf + cell * e->Lp1 : (const double*)nullptr, e->Lp1, e->q, e->qinv, e->logN);
     }
     HIPC(hipGetLastError());
     {
-        Span sc = span_s(conv.p, lN, l + 1, l + 1, 0, e->Lp1);
-        ntt(e, sc, sc, B * 2 * (l + 1), false);
+        Span sc = span_s(conv.p, kN, lk + 1, lk + 1, 0, e->Lp1);
+        ntt(e, sc, sc, B * 2 * (lk + 1), false);
     }
-    ProfScope psf(e, FAM_KS, 8.0 * N * (double)B * 2 * (l + 1) * 4);
-    hipLaunchKernelGGL(k_moddown_finish, dim3(N / 256, l + 1, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, (const u64*)conv.p, 2 * lN, lN, addend, out_of(o), e->q, (const u64*)e->md_pinv, (const double*)e->md_pinvf, e->logN);
+    Opnd fin_add = addend;
+    if (r) fin_add.ptr = nullptr;  // already inside the accumulators (times P)
+    ProfScope psf(e, FAM_KS, 8.0 * N * (double)B * 2 * (lk + 1) * 4);
+    hipLaunchKernelGGL(k_moddown_finish, dim3(N / 256, lk + 1, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, (const u64*)conv.p, 2 * kN, kN, fin_add, out_of(o), e->q, dinv, dinvf, e->logN);
     HIPC(hipGetLastError());
 }
 
@@ -1293,6 +1365,26 @@ static aesfhe_ct* relin_ct(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_ke
     add.np = 2;  // d0, d1 are the addends of outputs 0, 1
     keyswitch(e, c->d + 2 * v.ps, v.bs, c->B, l, rlk, add, r);
     return r;
+}
+
+// relinearisation of a 3-polynomial ciphertext fused with r rescales (r = 1, 2): level l - r
+static aesfhe_ct* relin_rescale(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_key* rlk, int r) {
+    const int l = c->level;
+    if (r > 0 && e->K + r > kMdrMaxE) {  // no combined tables: separate steps
+        aesfhe_ct* x = relin_ct(e, c, rlk);
+        for (int i = 0; i < r; i++) {
+            aesfhe_ct* y = rescale_view(e, view_of(x));
+            aesfhe_ct_free(x);
+            x = y;
+        }
+        return x;
+    }
+    aesfhe_ct* out = ct_new(e, c->B, 2, l - r);
+    View v = view_of(c);
+    Opnd add = opnd(v, c->B);
+    add.np = 2;
+    keyswitch(e, c->d + 2 * v.ps, v.bs, c->B, l, rlk, add, out, r);
+    return out;
 }
 
 static aesfhe_ct* tensor_ct(aesfhe_engine* e, const View& a, const View& b, int B) {
@@ -1338,10 +1430,8 @@ static aesfhe_ct* mul_ct(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* 
     align_to(e, a, l, A);
     align_to(e, b, l, Bv);
     aesfhe_ct* t = tensor_ct(e, A.v, Bv.v, B);
-    aesfhe_ct* rl = relin_ct(e, t, rlk);
+    aesfhe_ct* r = relin_rescale(e, t, rlk, 1);
     aesfhe_ct_free(t);
-    aesfhe_ct* r = rescale_view(e, view_of(rl));
-    aesfhe_ct_free(rl);
     return r;
 }
 
@@ -1602,10 +1692,8 @@ extern "C" int aesfhe_dot(aesfhe_engine* e, const aesfhe_ct* const* a, const aes
             hipLaunchKernelGGL(k_dot, ew_grid(e, nl, B), dim3(256), 0, e->stream, (const u64* const*)dpa, (const long*)dsa, (const u64* const*)dpb, (const long*)dsb, m, (long)nl * e->N, out_of(acc), e->q, e->qinv, e->logN);
         }
         HIPC(hipGetLastError());
-        aesfhe_ct* rl = relin_ct(e, acc, rlk);
+        *out = relin_rescale(e, acc, rlk, 1);
         aesfhe_ct_free(acc);
-        *out = rescale_view(e, view_of(rl));
-        aesfhe_ct_free(rl);
     }
     API_END
 }
@@ -1728,13 +1816,15 @@ extern "C" int aesfhe_poly2(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_
                 hipLaunchKernelGGL(k_poly2, ew_grid(e, nl, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny, tab, ml, t0, std::min(kPoly2Out, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, e->logN);
         }
         HIPC(hipGetLastError());
-        aesfhe_ct* rl = relin_ct(e, d3, rlk);
+        aesfhe_ct* r2 = relin_rescale(e, d3, rlk, 2);
         aesfhe_ct_free(d3);
-        aesfhe_ct* r1 = rescale_view(e, view_of(rl));
-        aesfhe_ct_free(rl);
-        std::vector<aesfhe_ct*> res = rescale_groups(e, r1->d, ml, B, 2, l - 1);
-        aesfhe_ct_free(r1);
-        for (int t = 0; t < ml; t++) outs[live[t]] = res[t];
+        const size_t per_out = (size_t)B * 2 * (l - 1) * N;  // words of one output (batch B, level l-2)
+        for (int t = 0; t < ml; t++) {
+            aesfhe_ct* o = ct_new(e, B, 2, l - 2);
+            HIPC(hipMemcpyAsync(o->d, r2->d + t * per_out, per_out * 8, hipMemcpyDeviceToDevice, e->stream));
+            outs[live[t]] = o;
+        }
+        aesfhe_ct_free(r2);
     }
     for (int t = 0; t < m; t++)
         if (!outs[t]) outs[t] = ct_zero_new(e, B, 2, l - 2);

@@ -313,11 +313,14 @@ __global__ void k_ks_inner(const u64* __restrict__ d, long dbs, const u64* __res
 // All digits at once: acc[b][c][t] = sum_j e_j[b][t] * key_j,c[pid(t)], e_j = d (limbs of digit
 // j, NTT) or ext_j (other limbs).  key layout [dnum][2][np][N]; ext layout [beta][B][ne][N].
 // grid (N/256, ne, 1); loops over the batch so each key word is read once per batch.
+// With pmodf != nullptr (combined ModDown + rescale) the Q limbs also get P * addend_c
+// (pmodf = (P mod q_i) / q_i), so that the later division by P * q_l... keeps the addend.
 __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* __restrict__ ext,
                                long exs, long exj, const u64* __restrict__ key, long kdig,
                                long kcomp, u64* __restrict__ acc, long abs_, long acs, int B,
                                int beta, int K, int l, const u64* __restrict__ qall,
-                               const double* __restrict__ qinvall, int Lp1, int logN) {
+                               const double* __restrict__ qinvall, int Lp1, Opnd addend,
+                               const double* __restrict__ pmodf, int logN) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int t = blockIdx.y;
     const int pid = t <= l ? t : Lp1 + (t - l - 1);
@@ -351,51 +354,76 @@ __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* _
                 }
             }
         }
+        if (pmodf && t <= l) {
+            const double f = pmodf[t], w = tw_w(f, q);
+            s0 = fred(s0, q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 0, t, k, logN)), w, f, q);
+            s1 = fred(s1, q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, k, logN)), w, f, q);
+        }
         u64* a0 = acc + (long)bb * abs_ + ((long)t << logN) + k;
         a0[0] = fcanon(s0, q, qi);
         a0[acs] = fcanon(s1, q, qi);
     }
 }
 
-// ModDown base conversion P -> Q_l: acc special limbs already in coefficient form.
-// conv[b][c][i][k] = sum_k' (z_k' * Phatinv_k' mod p_k') * Phat[k'][i] mod q_i
-// grid (N/256, ceil((l+1)/16), B*2)
-__global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int l,
+// ModDown base conversion from the dropped limbs E = {q_{l-r+1}..q_l, p_0..p_{K-1}} (acc limbs
+// l-r+1 .. l+K, already in coefficient form) to the kept limbs q_0..q_{l-r}; r = 0 is the plain
+// ModDown by P, r >= 1 the combined ModDown + rescale by D = P q_l ... q_{l-r+1}:
+//   y_j = [x_j * (D/e_j)^{-1}]_{e_j} in [0, e_j),  conv[i] = sum_j y_j * ((D/e_j) mod q_i) mod q_i.
+// r >= 1 makes the conversion exact: v = rint(sum_j y_j * (1/e_j)) (fp64, j in order) counts the
+// multiples of D in sum_j y_j (D/e_j), and conv[i] -= v * (D mod q_i), so the division rounds to
+// nearest like a plain rescale (einv[j] = 1/e_j, dmodf[i] = (D mod q_i)/q_i).
+// invf[j], hatf[j * Lp1 + i]: w/q tables.  grid (N/256, ceil((l-r+1)/16), B*2)
+__global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int l, int r,
                           u64* __restrict__ conv, long cbs, long ccs, int K,
-                          const double* __restrict__ phatinvf, const double* __restrict__ phatf,
+                          const double* __restrict__ invf, const double* __restrict__ hatf,
+                          const double* __restrict__ einv, const double* __restrict__ dmodf,
                           int Lp1, const u64* __restrict__ qall, const double* __restrict__ qinvall,
                           int logN) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int bb = blockIdx.z >> 1, c = blockIdx.z & 1;
     const u64* src = acc + (long)bb * abs_ + (long)c * acs;
+    const int ne = K + r, t0 = l - r + 1;
     double y[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         y[j] = 0.0;
-        if (j < K) {
-            const double pp = (double)qall[Lp1 + j];
-            const double f = phatinvf[j];
-            const double r = fmul_rem(u2d(src[((long)(l + 1 + j) << logN) + k]), tw_w(f, pp), f, pp);
-            y[j] = r < 0.0 ? r + pp : r;  // canonical: the oracle's conversion
+        if (j < ne) {
+            const int pid = j < r ? t0 + j : Lp1 + (j - r);
+            const double pp = (double)qall[pid];
+            const double f = invf[j];
+            const double v = fmul_rem(u2d(src[((long)(t0 + j) << logN) + k]), tw_w(f, pp), f, pp);
+            y[j] = v < 0.0 ? v + pp : v;  // canonical: the oracle's conversion
         }
     }
+    double v = 0.0;
+    if (r > 0) {
+        double u = 0.0;
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            if (j < ne) u = u + y[j] * einv[j];
+        v = __builtin_rint(u);
+    }
     const int i0 = blockIdx.y * 16;
-    for (int i = i0; i < i0 + 16 && i <= l; i++) {
+    for (int i = i0; i < i0 + 16 && i <= l - r; i++) {
         const double q = (double)qall[i], qi = qinvall[i];
-        double s = 0.0;
+        double sum = 0.0;
+        if (r > 0) {
+            const double f = dmodf[i];
+            sum = fmul_rem(-v, tw_w(f, q), f, q);
+        }
 #pragma unroll
         for (int j = 0; j < 16; j++) {
-            if (j < K) {
-                const double f = phatf[j * Lp1 + i];
-                s += fmul_rem(y[j], tw_w(f, q), f, q);
-                if ((j & 3) == 3) s = fred(s, q, qi);
+            if (j < ne) {
+                const double f = hatf[j * Lp1 + i];
+                sum += fmul_rem(y[j], tw_w(f, q), f, q);
+                if ((j & 3) == 3) sum = fred(sum, q, qi);
             }
         }
-        conv[(long)bb * cbs + (long)c * ccs + ((long)i << logN) + k] = fcanon(s, q, qi);
+        conv[(long)bb * cbs + (long)c * ccs + ((long)i << logN) + k] = fcanon(sum, q, qi);
     }
 }
 
-// out[b][c][i] = addend_c + (acc[b][c][i] - conv[b][c][i]) * P^{-1} ; grid (N/256, l+1, B*2)
+// out[b][c][i] = addend_c + (acc[b][c][i] - conv[b][c][i]) * D^{-1}  (addend absent: r >= 1) ; grid (N/256, l+1, B*2)
 __global__ void k_moddown_finish(const u64* __restrict__ acc, long abs_, long acs,
                                  const u64* __restrict__ conv, long cbs, long ccs, Opnd addend,
                                  Out o, const u64* __restrict__ qs, const u64* __restrict__ pinv,

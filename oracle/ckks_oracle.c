@@ -1234,8 +1234,8 @@ int aesfhe_tensor(aesfhe_engine *e, const aesfhe_ct *a0, const aesfhe_ct *b0, ae
 /* ------------------------------------------------------------------------------------------ */
 /* hybrid key switching.  d: one polynomial, level l, NTT domain.             */
 /* out0/out1: (l+1) limbs each.                                                                */
-static void keyswitch(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k, u64 *out0, u64 *out1) {
-    double t0 = now_ms();
+/* inner product of the ModUp digits with the key: acc = 2 x (l+1+K) limbs over Q_l and P */
+static u64 *ks_acc(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k) {
     const int N = e->N, K = e->K, nq = e->L + 1, ne = l + 1 + K;
     int pid[MAXP];
     for (int t = 0; t < ne; t++) pid[t] = t <= l ? t : nq + (t - l - 1);
@@ -1289,58 +1289,126 @@ static void keyswitch(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k
         }
         (void)na;
     }
-    /* ModDown */
-    u64 Phatinv[MAXP], Phat[MAXP][MAXP], Pinv[MAXP];
-    for (int kk = 0; kk < K; kk++) {
-        u64 pk = e->q[nq + kk], prod = 1;
-        for (int k2 = 0; k2 < K; k2++)
-            if (k2 != kk) prod = mul_mod_slow(prod, e->q[nq + k2] % pk, pk);
-        Phatinv[kk] = inv_mod(prod, pk);
-        for (int i = 0; i <= l; i++) {
-            u64 qi = e->q[i], h = 1;
-            for (int k2 = 0; k2 < K; k2++)
-                if (k2 != kk) h = mul_mod_slow(h, e->q[nq + k2] % qi, qi);
-            Phat[kk][i] = h;
+    free(dc);
+    return acc;
+}
+
+/* ModDown of the accumulators by D = P * q_l ... q_{l-r+1} (r = 0: plain
+ * ModDown by P, r >= 1: combined with r rescales).  Dropped limbs E = {q_{l-r+1}..q_l, p_0..}:
+ * y_j = [INTT(acc_j) * (D/e_j)^{-1}]_{e_j}, conv_i = sum_j y_j (D/e_j mod q_i), out_i =
+ * (acc_i - conv_i) D^{-1} for i <= l - r.  For r >= 1 the conversion is exact: v = rint(sum_j
+ * y_j * (1/e_j)) (fp64, in j order) multiples of D are removed from conv (round-to-nearest
+ * division, as a plain rescale).  Output limbs: (l-r+1) per component. */
+static void moddown_r(aesfhe_engine *e, const u64 *acc, int l, int r, u64 *out0, u64 *out1) {
+    const int N = e->N, K = e->K, nq = e->L + 1, ne = l + 1 + K, nE = K + r, lk = l - r;
+    int Ep[MAXP];
+    for (int j = 0; j < nE; j++) Ep[j] = j < r ? lk + 1 + j : nq + (j - r);
+    u64 inv[MAXP], hat[MAXP][MAXP], Dinv[MAXP], Dmod[MAXP];
+    double einv[MAXP];
+    for (int j = 0; j < nE; j++) {
+        const u64 ej = e->q[Ep[j]];
+        u64 prod = 1;
+        for (int j2 = 0; j2 < nE; j2++)
+            if (j2 != j) prod = mul_mod_slow(prod, e->q[Ep[j2]] % ej, ej);
+        inv[j] = inv_mod(prod, ej);
+        einv[j] = 1.0 / (double)ej;
+        for (int i = 0; i <= lk; i++) {
+            const u64 qi = e->q[i];
+            u64 h = 1;
+            for (int j2 = 0; j2 < nE; j2++)
+                if (j2 != j) h = mul_mod_slow(h, e->q[Ep[j2]] % qi, qi);
+            hat[j][i] = h;
         }
     }
-    for (int i = 0; i <= l; i++) {
-        u64 qi = e->q[i], P = 1;
-        for (int k2 = 0; k2 < K; k2++) P = mul_mod_slow(P, e->q[nq + k2] % qi, qi);
-        Pinv[i] = inv_mod(P, qi);
+    for (int i = 0; i <= lk; i++) {
+        const u64 qi = e->q[i];
+        u64 D = 1;
+        for (int j = 0; j < nE; j++) D = mul_mod_slow(D, e->q[Ep[j]] % qi, qi);
+        Dinv[i] = inv_mod(D, qi);
+        Dmod[i] = D;
     }
     for (int c = 0; c < 2; c++) {
-        u64 *a = acc + (size_t)c * ne * N;
+        const u64 *a = acc + (size_t)c * ne * N;
         u64 *outc = c == 0 ? out0 : out1;
-        u64 *y = malloc(sizeof(u64) * (size_t)K * N);
+        u64 *y = malloc(sizeof(u64) * (size_t)nE * N);
 #pragma omp parallel for schedule(static)
-        for (int kk = 0; kk < K; kk++) {
-            int p = nq + kk;
-            u64 *z = y + (size_t)kk * N;
-            memcpy(z, a + (size_t)(l + 1 + kk) * N, sizeof(u64) * N);
+        for (int j = 0; j < nE; j++) {
+            const int p = Ep[j];
+            u64 *z = y + (size_t)j * N;
+            memcpy(z, a + (size_t)(lk + 1 + j) * N, sizeof(u64) * N);
             ntt_inv(e, z, p);
-            for (int x = 0; x < N; x++) z[x] = mul_mod_slow(z[x], Phatinv[kk], e->q[p]);
+            for (int x = 0; x < N; x++) z[x] = mul_mod_slow(z[x], inv[j], e->q[p]);
         }
 #pragma omp parallel for schedule(static)
-        for (int i = 0; i <= l; i++) {
+        for (int i = 0; i <= lk; i++) {
             const u64 qi = e->q[i];
             u64 *conv = malloc(sizeof(u64) * N);
             for (int x = 0; x < N; x++) {
-                u64 s = 0;
-                for (int kk = 0; kk < K; kk++)
-                    s = add_mod(s, mul_mod_slow(y[(size_t)kk * N + x] % qi, Phat[kk][i], qi), qi);
-                conv[x] = s;
+                u64 sum = 0;
+                for (int j = 0; j < nE; j++)
+                    sum = add_mod(sum, mul_mod_slow(y[(size_t)j * N + x] % qi, hat[j][i], qi), qi);
+                if (r > 0) {  /* exact conversion: remove the v multiples of D (v = rint(sum y_j / e_j)) */
+                    double u = 0.0;
+                    for (int j = 0; j < nE; j++) u = u + (double)y[(size_t)j * N + x] * einv[j];
+                    const u64 v = (u64)rint(u);
+                    sum = sub_mod(sum, mul_mod_slow(v % qi, Dmod[i], qi), qi);
+                }
+                conv[x] = sum;
             }
             ntt_fwd(e, conv, i);
-            u64 pinvp = shoup_pre(Pinv[i], qi);
+            const u64 dp = shoup_pre(Dinv[i], qi);
             for (int x = 0; x < N; x++)
-                outc[(size_t)i * N + x] = mul_shoup(sub_mod(a[(size_t)i * N + x], conv[x], qi), Pinv[i], pinvp, qi);
+                outc[(size_t)i * N + x] = mul_shoup(sub_mod(a[(size_t)i * N + x], conv[x], qi), Dinv[i], dp, qi);
             free(conv);
         }
         free(y);
     }
+}
+
+/* hybrid key switching of one polynomial, ModDown by P: out0/out1 (l+1 limbs each) */
+static void keyswitch(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k, u64 *out0, u64 *out1) {
+    double t0 = now_ms();
+    u64 *acc = ks_acc(e, d, l, k);
+    moddown_r(e, acc, l, 0, out0, out1);
     free(acc);
-    free(dc);
     prof_add(e, 1, now_ms() - t0);
+}
+
+static int relin_raw(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_key *rlk, aesfhe_ct **out);
+
+/* relinearisation fused with r rescales: acc_c += P * d_c on the Q limbs,
+ * then ModDown by P q_l ... q_{l-r+1}; the result is at level l - r. */
+static aesfhe_ct *relin_rescale_raw(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_key *rlk, int r) {
+    const int N = e->N, l = c->level, K = e->K, ne = l + 1 + K;
+    if (K + r > 16) {  /* the HIP engine's table limit: separate relinearisation and rescales */
+        aesfhe_ct *x;
+        relin_raw(e, c, rlk, &x);
+        for (int i = 0; i < r; i++) {
+            aesfhe_ct *y = rescale_raw(e, x);
+            aesfhe_ct_free(x);
+            x = y;
+        }
+        return x;
+    }
+    double t0 = now_ms();
+    aesfhe_ct *out = ct_new(e, c->B, 2, l - r);
+    for (int b = 0; b < c->B; b++) {
+        u64 *acc = ks_acc(e, limb(e, c, b, 2, 0), l, rlk);
+        for (int cc = 0; cc < 2; cc++)
+#pragma omp parallel for schedule(static)
+            for (int i = 0; i <= l; i++) {
+                const u64 qi = e->q[i];
+                u64 P = 1;
+                for (int kk = 0; kk < K; kk++) P = mul_mod_slow(P, e->q[e->L + 1 + kk] % qi, qi);
+                const u64 *dci = limb(e, c, b, cc, i);
+                u64 *ai = acc + ((size_t)cc * ne + i) * N;
+                for (int x = 0; x < N; x++) ai[x] = add_mod(ai[x], mul_mod_slow(dci[x], P, qi), qi);
+            }
+        moddown_r(e, acc, l, r, limb(e, out, b, 0, 0), limb(e, out, b, 1, 0));
+        free(acc);
+    }
+    prof_add(e, 1, now_ms() - t0);
+    return out;
 }
 
 static int relin_raw(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_key *rlk, aesfhe_ct **out) {
@@ -1391,10 +1459,9 @@ int aesfhe_mul(aesfhe_engine *e, const aesfhe_ct *a, const aesfhe_ct *b, const a
         *out = r;
         return 0;
     }
-    relin_raw(e, t, rlk, &rl);
+    (void)rl;
+    *out = relin_rescale_raw(e, t, rlk, 1);
     aesfhe_ct_free(t);
-    *out = rescale_raw(e, rl);
-    aesfhe_ct_free(rl);
     return 0;
 }
 
@@ -1531,11 +1598,8 @@ int aesfhe_dot(aesfhe_engine *e, const aesfhe_ct *const *a, const aesfhe_ct *con
         *out = r;
         return 0;
     }
-    aesfhe_ct *rl;
-    relin_raw(e, acc, rlk, &rl);
+    *out = relin_rescale_raw(e, acc, rlk, 1);
     aesfhe_ct_free(acc);
-    *out = rescale_raw(e, rl);
-    aesfhe_ct_free(rl);
     return 0;
 }
 
@@ -1638,13 +1702,8 @@ int aesfhe_poly2(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, const
                 }
             }
         }
-        aesfhe_ct *rl, *r1;
-        relin_raw(e, acc, rlk, &rl);
+        outs[t] = relin_rescale_raw(e, acc, rlk, 2);
         aesfhe_ct_free(acc);
-        r1 = rescale_raw(e, rl);
-        aesfhe_ct_free(rl);
-        outs[t] = rescale_raw(e, r1);
-        aesfhe_ct_free(r1);
     }
     free(A);
     free(Bc);
