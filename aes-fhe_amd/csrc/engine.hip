@@ -1325,7 +1325,8 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
     // 3. inner product with every key digit in one pass
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B));
-        hipLaunchKernelGGL(k_ks_inner_all, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, (const u64*)ext.p, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, addend, r ? (const double*)e->pmodf : (const double*)nullptr, e->logN);
+        auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
+        hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, (const u64*)ext.p, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, addend, r ? (const double*)e->pmodf : (const double*)nullptr, e->logN);
     }
     HIPC(hipGetLastError());
     // 4. ModDown: INTT the dropped limbs (top r Q limbs + the special limbs) of both accumulators

@@ -315,6 +315,7 @@ __global__ void k_ks_inner(const u64* __restrict__ d, long dbs, const u64* __res
 // grid (N/256, ne, 1); loops over the batch so each key word is read once per batch.
 // With pmodf != nullptr (combined ModDown + rescale) the Q limbs also get P * addend_c
 // (pmodf = (P mod q_i) / q_i), so that the later division by P * q_l... keeps the addend.
+template <int BM>  // digits held in registers (beta <= BM)
 __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* __restrict__ ext,
                                long exs, long exj, const u64* __restrict__ key, long kdig,
                                long kcomp, u64* __restrict__ acc, long abs_, long acs, int B,
@@ -327,9 +328,9 @@ __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* _
     const double q = (double)qall[pid];
     const double qi = qinvall[pid];
     const int own = t <= l ? t / K : -1;  // the digit whose limbs include t (Q limbs only)
-    double kb[12], ka[12], kbq[12], kaq[12];
+    double kb[BM], ka[BM], kbq[BM], kaq[BM];
 #pragma unroll
-    for (int j = 0; j < 12; j++) {
+    for (int j = 0; j < BM; j++) {
         kb[j] = ka[j] = kbq[j] = kaq[j] = 0.0;
         if (j < beta) {
             const long ko = (long)j * kdig + ((long)pid << logN) + k;
@@ -339,10 +340,11 @@ __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* _
             kaq[j] = ka[j] * qi;
         }
     }
+#pragma unroll 4
     for (int bb = 0; bb < B; bb++) {
         double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-        for (int j = 0; j < 12; j++) {
+        for (int j = 0; j < BM; j++) {
             if (j < beta) {
                 const double e = u2d((j == own) ? d[(long)bb * dbs + ((long)t << logN) + k]
                                                 : ext[(long)j * exj + (long)bb * exs + ((long)t << logN) + k]);
