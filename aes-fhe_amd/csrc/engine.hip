@@ -140,10 +140,12 @@ struct aesfhe_engine {
     // base conversion tables
     u64 *mu_hatinv, *mu_hat, *md_phatinv, *md_phat, *md_pinv, *rs_inv, *rs_mod, *pmod;
     // combined ModDown + rescale (drop r = 1, 2 top Q primes with P), see build_tables
-    double *mdr_invf = nullptr, *mdr_hatf = nullptr, *mdr_dinvf = nullptr, *pmodf = nullptr;
+    double *mdr_invf = nullptr, *mdr_dinvf = nullptr, *pmodf = nullptr;
+    TwD* mdr_hatf = nullptr;  // {w, w/q}
     double *mdr_einv = nullptr, *mdr_dmodf = nullptr;
     u64* mdr_dinv = nullptr;
-    double *mu_hatinvf, *mu_hatf, *md_phatinvf, *md_phatf, *md_pinvf, *rs_invf;
+    double *mu_hatinvf, *md_phatinvf, *md_pinvf, *rs_invf;
+    TwD *mu_hatf, *md_phatf;  // base-conversion constants {w, w/q}
     // small-argument upload ring (device) + pinned staging
     char* ring_d = nullptr;
     char* ring_h = nullptr;
@@ -500,7 +502,8 @@ static void build_tables(aesfhe_engine* e) {
     // ModUp tables per (digit j, alpha a): hatinv[i], hat[i][pid]
     const size_t mu_sets = (size_t)e->dnum * K;
     std::vector<u64> hhatinv(mu_sets * K, 0), hhat(mu_sets * K * np, 0);
-    std::vector<double> hhatinvf(mu_sets * K, 0), hhatf(mu_sets * K * np, 0);
+    std::vector<double> hhatinvf(mu_sets * K, 0);
+    std::vector<TwD> hhatf(mu_sets * K * np, TwD{0, 0});
     for (int j = 0; j < e->dnum; j++)
         for (int a = 1; a <= K; a++) {
             int lo = j * K, hi = lo + a;
@@ -518,7 +521,7 @@ static void build_tables(aesfhe_engine* e) {
                     for (int i2 = lo; i2 < hi; i2++)
                         if (i2 != i) h = h_mulmod(h, Q[i2] % qt, qt);
                     hhat[(set * K + (i - lo)) * np + pid] = h;
-                    hhatf[(set * K + (i - lo)) * np + pid] = (double)h / (double)qt;
+                    hhatf[(set * K + (i - lo)) * np + pid] = TwD{(double)h, (double)h / (double)qt};
                 }
             }
         }
@@ -529,7 +532,8 @@ static void build_tables(aesfhe_engine* e) {
 
     // ModDown tables
     std::vector<u64> hphatinv(K), hphat((size_t)K * Lp1), hpinv(Lp1), hpmod(np, 0);
-    std::vector<double> hphatinvf(K), hphatf((size_t)K * Lp1), hpinvf(Lp1);
+    std::vector<double> hphatinvf(K), hpinvf(Lp1);
+    std::vector<TwD> hphatf((size_t)K * Lp1);
     for (int k = 0; k < K; k++) {
         u64 pk = Q[Lp1 + k], prod = 1;
         for (int k2 = 0; k2 < K; k2++)
@@ -541,7 +545,7 @@ static void build_tables(aesfhe_engine* e) {
             for (int k2 = 0; k2 < K; k2++)
                 if (k2 != k) h = h_mulmod(h, Q[Lp1 + k2] % qi, qi);
             hphat[(size_t)k * Lp1 + i] = h;
-            hphatf[(size_t)k * Lp1 + i] = (double)h / (double)qi;
+            hphatf[(size_t)k * Lp1 + i] = TwD{(double)h, (double)h / (double)qi};
         }
     }
     for (int i = 0; i < Lp1; i++) {
@@ -565,11 +569,12 @@ static void build_tables(aesfhe_engine* e) {
     }
     // combined ModDown + rescale: E = {q_{l-r+1}..q_l, p_0..p_{K-1}} (acc limb order), D = prod E
     //   mdr_invf[(r-1, l)][j]       = (D/e_j)^{-1} mod e_j, as w/e_j
-    //   mdr_hatf[(r-1, l)][j][i]    = (D/e_j) mod q_i, as w/q_i   (i <= l - r)
+    //   mdr_hatf[(r-1, l)][j][i]    = (D/e_j) mod q_i, as {w, w/q_i}   (i <= l - r)
     //   mdr_dinv[(r-1, l)][i] (+f)  = D^{-1} mod q_i
     {
         const size_t cells = (size_t)kMdrMaxR * Lp1;
-        std::vector<double> hinvf(cells * kMdrMaxE, 0.0), hhatf(cells * kMdrMaxE * Lp1, 0.0), hdinvf(cells * Lp1, 0.0);
+        std::vector<double> hinvf(cells * kMdrMaxE, 0.0), hdinvf(cells * Lp1, 0.0);
+        std::vector<TwD> hhatf(cells * kMdrMaxE * Lp1, TwD{0, 0});
         std::vector<u64> hdinv(cells * Lp1, 0);
         std::vector<double> heinv(cells * kMdrMaxE, 0.0), hdmodf(cells * Lp1, 0.0);
         for (int r = 1; r <= kMdrMaxR && K + r <= kMdrMaxE; r++)
@@ -590,7 +595,7 @@ static void build_tables(aesfhe_engine* e) {
                         u64 h = 1;
                         for (size_t j2 = 0; j2 < E.size(); j2++)
                             if (j2 != j) h = h_mulmod(h, Q[E[j2]] % qi, qi);
-                        hhatf[(cell * kMdrMaxE + j) * Lp1 + i] = (double)h / (double)qi;
+                        hhatf[(cell * kMdrMaxE + j) * Lp1 + i] = TwD{(double)h, (double)h / (double)qi};
                     }
                 }
                 for (int i = 0; i <= l - r; i++) {
@@ -1308,7 +1313,7 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
             hipLaunchKernelGGL(k_modup, dim3(N / 256, (ne + 15) / 16, B), dim3(256), 0, e->stream, (const u64*)dc.p, lN, exj, neN, lo, alpha, l, ne,
-                               (const double*)(e->mu_hatinvf + set * K), (const double*)(e->mu_hatf + set * K * e->np),
+                               (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
                                e->np, e->q, e->qinv, e->Lp1, e->logN);
         }
         HIPC(hipGetLastError());
@@ -1336,7 +1341,7 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
     }
     const size_t cell = r ? (size_t)(r - 1) * e->Lp1 + l : 0;
     const double* invf = r ? e->mdr_invf + cell * kMdrMaxE : e->md_phatinvf;
-    const double* hatf = r ? e->mdr_hatf + cell * kMdrMaxE * e->Lp1 : e->md_phatf;
+    const TwD* hatf = r ? e->mdr_hatf + cell * kMdrMaxE * e->Lp1 : e->md_phatf;
     const u64* dinv = r ? e->mdr_dinv + cell * e->Lp1 : e->md_pinv;
     const double* dinvf = r ? e->mdr_dinvf + cell * e->Lp1 : e->md_pinvf;
     Tmp conv(e, (size_t)B * 2 * kN);

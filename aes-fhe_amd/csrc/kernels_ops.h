@@ -243,11 +243,11 @@ __global__ void k_rescale_finish_g(const u64* __restrict__ c, long cps, const u6
 // the extended basis (Q_l then P), exact fp64 arithmetic (kernels.h fmul_rem):
 //   y_i = [x_i * qhat_i^{-1}]_{q_i} in [0, q_i) (canonical, so the multiple of Q that the fast
 //   conversion adds is the oracle's), ext[t] = sum_i y_i * (qhat_i mod p_t) mod p_t.
-// Constants come from their w/q tables (w = rint(wq * q) is exact).  grid (N/256,
+// Constants: hatinv as w/q (w = rint(wq * q) is exact), hat as {w, w/q}.  grid (N/256,
 // ceil(ne/16), B): each thread converts one coefficient into up to 16 target limbs.
 __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ ext, long exs,
                         int lo, int alpha, int l, int ne, const double* __restrict__ hatinvf,
-                        const double* __restrict__ hatf, int np, const u64* __restrict__ qall,
+                        const TwD* __restrict__ hat, int np, const u64* __restrict__ qall,
                         const double* __restrict__ qinvall, int Lp1, int logN) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int bb = blockIdx.z;
@@ -272,8 +272,8 @@ __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             if (i < alpha) {
-                const double f = hatf[i * np + pid];
-                acc += fmul_rem(y[i], tw_w(f, qt), f, qt);
+                const TwD f = hat[i * np + pid];
+                acc += fmul_rem_r(y[i], f.w, f.wq, qt);
                 if ((i & 3) == 3) acc = fred(acc, qt, qti);
             }
         }
@@ -374,10 +374,10 @@ __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* _
 // r >= 1 makes the conversion exact: v = rint(sum_j y_j * (1/e_j)) (fp64, j in order) counts the
 // multiples of D in sum_j y_j (D/e_j), and conv[i] -= v * (D mod q_i), so the division rounds to
 // nearest like a plain rescale (einv[j] = 1/e_j, dmodf[i] = (D mod q_i)/q_i).
-// invf[j], hatf[j * Lp1 + i]: w/q tables.  grid (N/256, ceil((l-r+1)/16), B*2)
+// invf[j]: w/q table, hat[j * Lp1 + i]: {w, w/q}.  grid (N/256, ceil((l-r+1)/16), B*2)
 __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int l, int r,
                           u64* __restrict__ conv, long cbs, long ccs, int K,
-                          const double* __restrict__ invf, const double* __restrict__ hatf,
+                          const double* __restrict__ invf, const TwD* __restrict__ hat,
                           const double* __restrict__ einv, const double* __restrict__ dmodf,
                           int Lp1, const u64* __restrict__ qall, const double* __restrict__ qinvall,
                           int logN) {
@@ -416,8 +416,8 @@ __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int 
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             if (j < ne) {
-                const double f = hatf[j * Lp1 + i];
-                sum += fmul_rem(y[j], tw_w(f, q), f, q);
+                const TwD f = hat[j * Lp1 + i];
+                sum += fmul_rem_r(y[j], f.w, f.wq, q);
                 if ((j & 3) == 3) sum = fred(sum, q, qi);
             }
         }
