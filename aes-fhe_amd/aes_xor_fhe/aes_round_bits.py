@@ -12,13 +12,14 @@ the expensive operations disappear.  The state is carried as +-1 bits B = (-1)^b
   of the high / low nibble bits (11 products each, depth 2), the 8 output bits are
   out_t = sum_{S,T} W_t[S,T] M^hi_S M^lo_T: one fused Engine.poly2 call per row (inner sums
   never rescaled, one relinearisation per output bit), depth 2.
-* MixColumns -- XOR is multiplication.  With a_r the SubBytes bytes of row r:
-  out_r = xtime(a_r ^ a_{r+1}) ^ a_r ^ t, t = a_0 ^ a_1 ^ a_2 ^ a_3.  Per bit j:
-  U_rj = A_rj A_{r+1,j}; T_j = U_0j U_2j; xtime(u)_j = u_{j-1} (j = 0: u_7), times u_7 for
-  j in {1, 3, 4}; OUT_rj = (A_rj T_j) XT_rj.  116 products, depth 4.
-* AddRoundKey -- 32 products with the encrypted key bits (B = 1, broadcast), depth 1.
-Round depth 4 + 4 + 1 = 9 (three rounds per 30-level budget); 24 + 88 + 4 + 116 + 32 = 264 key
-switches per 8192 blocks against ~960 for the byte-major nibble-domain round (aes_round.py).
+* MixColumns + AddRoundKey -- XOR is multiplication.  With a_r the SubBytes bytes of row r and
+  U_r = a_r ^ a_{r+1}: out_r = xtime(a_r ^ a_{r+1}) ^ a_{r+1} ^ a_{r+2} ^ a_{r+3}
+  = xtime(U_r) ^ U_{r+1} ^ a_{r+3}; xtime(u)_j = u_{j-1} (j = 0: u_7), times u_7 for j in
+  {1, 3, 4}.  The round-key bit (B = 1, broadcast) joins a_{r+3} at depth 0:
+  out_rj ^ k_rj = xtime(U_r)_j * (U_{r+1,j} * (a_{r+3,j} * K_rj)): 32 + 12 + 96 = 140
+  products, depth 3 (plain MixColumns alone: 108 products, depth 3).
+Round depth 4 + 3 = 7 (four rounds per 30-level budget); 24 + 88 + 4 + 140 = 256 key switches
+per 8192 blocks against ~960 for the byte-major nibble-domain round (aes_round.py).
 """
 from __future__ import annotations
 
@@ -131,18 +132,25 @@ class AESRowRound:
                                     self.W, self.rlk))
         return out
 
+    def _xtime_terms(self, U, r, j):
+        """xtime(u_r) bit j: U[r][j-1] (j = 0: U[r][7]), times U[r][7] for j in {1, 3, 4}."""
+        src, carry = XT_OF[j]
+        return self.mul(U[r][src], U[r][7]) if carry else U[r][src]
+
     def mix_columns(self, A: List[List[Ciphertext]]) -> List[List[Ciphertext]]:
+        """out_r = xtime(a_r ^ a_{r+1}) ^ a_{r+1} ^ a_{r+2} ^ a_{r+3}
+               = xtime(U_r) ^ U_{r+1} ^ a_{r+3},   U_r = a_r ^ a_{r+1}:  108 products, depth 3."""
         U = [[self.mul(A[r][j], A[(r + 1) % 4][j]) for j in range(8)] for r in range(4)]
-        Tt = [self.mul(U[0][j], U[2][j]) for j in range(8)]
-        out = []
-        for r in range(4):
-            row = []
-            for j in range(8):
-                src, carry = XT_OF[j]
-                xt = self.mul(U[r][src], U[r][7]) if carry else U[r][src]
-                row.append(self.mul(self.mul(A[r][j], Tt[j]), xt))
-            out.append(row)
-        return out
+        return [[self.mul(self._xtime_terms(U, r, j), self.mul(U[(r + 1) % 4][j], A[(r + 3) % 4][j]))
+                 for j in range(8)] for r in range(4)]
+
+    def mix_columns_add_round_key(self, A, key) -> List[List[Ciphertext]]:
+        """MixColumns then AddRoundKey in one product tree: the key bit joins a_{r+3} first,
+        out_rj ^ k_rj = xtime(U_r)_j * (U_{r+1,j} * (a_{r+3,j} * K_rj)): 140 products, depth 3."""
+        U = [[self.mul(A[r][j], A[(r + 1) % 4][j]) for j in range(8)] for r in range(4)]
+        return [[self.mul(self._xtime_terms(U, r, j),
+                          self.mul(U[(r + 1) % 4][j], self.mul(A[(r + 3) % 4][j], key[r][j])))
+                 for j in range(8)] for r in range(4)]
 
     def add_round_key(self, S: List[List[Ciphertext]], key) -> List[List[Ciphertext]]:
         return [[self.mul(S[r][j], key[r][j]) for j in range(8)] for r in range(4)]
@@ -163,8 +171,6 @@ class AESRowRound:
         t = mark("shift_rows", t)
         A = self.sub_bytes(bits)
         t = mark("sub_bytes", t)
-        M = self.mix_columns(A)
-        t = mark("mix_columns", t)
-        out = self.add_round_key(M, key)
-        mark("add_round_key", t)
+        out = self.mix_columns_add_round_key(A, key)
+        mark("mix_columns_add_round_key", t)
         return out

@@ -1,7 +1,7 @@
 """Row-sliced bit-domain AES round (aes_xor_fhe.aes_round_bits, the bench's default step).
 
 CPU: the oracle engine runs every stage (ShiftRows, SubBytes as a Walsh polynomial over
-nibble-bit monomials, MixColumns, AddRoundKey) and three chained rounds inside one 30-level
+nibble-bit monomials, MixColumns, AddRoundKey) and four chained rounds inside one 30-level
 budget, each checked against FIPS-197 (aes_tables, itself pinned by the FIPS-197 appendix
 vectors in test_aes_tables.py).
 GPU: the HIP engine produces residue-identical ciphertexts to the oracle for a full round at
@@ -66,23 +66,26 @@ def test_row_round_stages_oracle(oracle_lib):
     M = R.mix_columns(A)
     ref = T.mix_columns(ref)
     assert np.array_equal(R.decrypt_blocks(M), ref)
+    assert 30 - M[0][0].level == 4 + 3          # SubBytes 4, MixColumns 3
     K = R.add_round_key(M, R.encrypt_round_key(rk))
     assert np.array_equal(R.decrypt_blocks(K), T.aes_round(blocks, rk))
-    assert 30 - K[0][0].level == 9              # depth per round
+    KM = R.mix_columns_add_round_key(A, R.encrypt_round_key(rk))
+    assert np.array_equal(R.decrypt_blocks(KM), T.aes_round(blocks, rk))
+    assert 30 - KM[0][0].level == 7              # depth per round
 
 
-def test_three_chained_rounds_oracle(oracle_lib):
+def test_four_chained_rounds_oracle(oracle_lib):
     e, R = _setup(oracle_lib, 10, seed=8)
     rng = np.random.default_rng(2)
     blocks = rng.integers(0, 256, (1, R.n_blk, 16), dtype=np.uint8)
     rks = T.expand_key(rng.integers(0, 256, 16, dtype=np.uint8))
     st = R.encrypt_blocks(blocks)
     ref = blocks
-    for r in (1, 2, 3):
+    for r in (1, 2, 3, 4):
         st = R.round(st, R.encrypt_round_key(rks[r]))
         ref = T.aes_round(ref, rks[r])
         assert np.array_equal(R.decrypt_blocks(st), ref)
-    assert st[0][0].level == 3
+    assert st[0][0].level == 2
 
 
 @pytest.mark.gpu
@@ -111,7 +114,7 @@ def test_row_round_full_params(product_lib, gpu_available):
     rks = T.expand_key(rng.integers(0, 256, 16, dtype=np.uint8))
     st = R.encrypt_blocks(blocks)
     ref = blocks
-    for r in (1, 2, 3):                           # three rounds inside one 30-level budget
+    for r in (1, 2, 3, 4):                        # four rounds inside one 30-level budget
         st = R.round(st, R.encrypt_round_key(rks[r]))
         ref = T.aes_round(ref, rks[r])
         assert np.array_equal(R.decrypt_blocks(st), ref)
