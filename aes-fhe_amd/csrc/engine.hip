@@ -384,7 +384,7 @@ static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse
             else hipLaunchKernelGGL(k_nttf_inv_rows, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
         }
         ProfScope ps(e, FAM_NTT, by);
-        if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_rows, dim3(16, total), dim3(256), 0, e->stream, dst, T);
+        if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_rows_t<false>, dim3(16, total), dim3(256), 0, e->stream, dst, T, RowFin{});
         else hipLaunchKernelGGL(k_nttf_inv_cols, dim3(16, total), dim3(256), 0, e->stream, dst, T);
         return;
     }
@@ -406,6 +406,9 @@ static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse
 }
 
 static bool g_ntt_generic = getenv("AESFHE_NTT_GENERIC") != nullptr;
+static bool g_no_fuse = getenv("AESFHE_NO_FUSE") != nullptr;  // unfused key-switch epilogues (A/B)
+// the N = 2^16 fp64 passes with fused epilogues are available
+static bool fused_ntt(const aesfhe_engine* e) { return e->logN == 16 && !g_ntt_generic && !g_ntt_int && !g_no_fuse; }
 
 static void ntt(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
     if (total <= 0) return;
@@ -1352,12 +1355,25 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
                            r ? e->mdr_dmodf + cell * e->Lp1 : (const double*)nullptr, e->Lp1, e->q, e->qinv, e->logN);
     }
     HIPC(hipGetLastError());
-    {
-        Span sc = span_s(conv.p, kN, lk + 1, lk + 1, 0, e->Lp1);
-        ntt(e, sc, sc, B * 2 * (lk + 1), false);
-    }
+    Span sc = span_s(conv.p, kN, lk + 1, lk + 1, 0, e->Lp1);
     Opnd fin_add = addend;
     if (r) fin_add.ptr = nullptr;  // already inside the accumulators (times P)
+    if (fused_ntt(e)) {
+        // conv NTT with the finish in the row pass's epilogue: conv never reaches HBM
+        Tabs T = e->tabs();
+        const int total = B * 2 * (lk + 1);
+        {
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+            hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, sc, sc, T);
+        }
+        RowFin f{(const u64*)acc.p, 2 * neN, neN, Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}, o->d,
+                 2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf, lk + 1};
+        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+        hipLaunchKernelGGL(k_nttf_fwd_rows_t<true>, dim3(16, total), dim3(256), 0, e->stream, sc, T, f);
+        HIPC(hipGetLastError());
+        return;
+    }
+    ntt(e, sc, sc, B * 2 * (lk + 1), false);
     ProfScope psf(e, FAM_KS, 8.0 * N * (double)B * 2 * (lk + 1) * 4);
     hipLaunchKernelGGL(k_moddown_finish, dim3(N / 256, lk + 1, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, (const u64*)conv.p, 2 * kN, kN, fin_add, out_of(o), e->q, dinv, dinvf, e->logN);
     HIPC(hipGetLastError());

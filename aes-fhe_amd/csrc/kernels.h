@@ -94,6 +94,12 @@ __device__ __forceinline__ u64 fcanon(double x, double q, double qinv) {
 __device__ __forceinline__ double tw_w(double wq, double q) {
     return __builtin_fma(wq, q, kMagic52) - kMagic52;
 }
+// an optional operand (ptr == nullptr or component >= np reads as zero), for fused epilogues
+struct Opnd2 {
+    const u64* ptr;
+    long bs, ps;
+    int np;
+};
 struct alignas(16) TwD {
     double w;   // constant as an exact double (< 2^52)
     double wq;  // w / q

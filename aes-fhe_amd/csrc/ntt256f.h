@@ -96,9 +96,24 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_cols(Span src, Span dst, Tabs 
     for (int bb = 0; bb < 16; bb++) st_d(&out[(ap * 16 + bb) * 256 + c], x[bb]);
 }
 
+// ModDown finish fused into the row pass of the conv NTT (key switch): limb y of
+// the span is (batch b, component c, limb i) = (y / nl / 2, y / nl % 2, y % nl) and the pass
+// writes out[b][c][i] = (acc[b][c][i] - conv) * D^{-1} (+ addend) instead of conv itself.
+struct RowFin {
+    const u64* acc;
+    long abs_, acs;
+    Opnd2 addend;
+    u64* out;
+    long obs, ops;
+    const double* dinvf;
+    int nl;
+};
+
 // Forward, row pass: stages m = 256..32768 within rows of 256 contiguous elements; raw doubles
-// in, canonical u64 out.  Workgroup = 16 rows [r0, r0+16); lane (b, rl) = (tid & 15, tid >> 4).
-__global__ __launch_bounds__(256) void k_nttf_fwd_rows(Span dst, Tabs T) {
+// in, canonical u64 out (FIN: the ModDown finish above).  Workgroup = 16 rows [r0, r0+16);
+// lane (b, rl) = (tid & 15, tid >> 4).
+template <bool FIN>
+__global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFin fin) {
     __shared__ double s[16 * 16 * kPadF];
     int pid;
     u64* io = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
@@ -150,11 +165,28 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows(Span dst, Tabs T) {
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) sr[ap * kPadF + bb] = __longlong_as_double((long long)fcanon(x[bb], q, qi));
     __syncthreads();
-    u64* base = io + (long)blockIdx.x * 16 * 256;
+    if (!FIN) {
+        u64* base = io + (long)blockIdx.x * 16 * 256;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
-        base[e] = (u64)__double_as_longlong(s[r * 16 * kPadF + (cc >> 4) * kPadF + (cc & 15)]);
+        for (int k = 0; k < 16; k++) {
+            const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
+            base[e] = (u64)__double_as_longlong(s[r * 16 * kPadF + (cc >> 4) * kPadF + (cc & 15)]);
+        }
+    } else {
+        const int y = blockIdx.y, p = y / fin.nl, i = y - p * fin.nl, bb = p >> 1, c = p & 1;
+        const long off = ((long)i << T.logN) + (long)blockIdx.x * 16 * 256;
+        const u64* ap = fin.acc + (long)bb * fin.abs_ + (long)c * fin.acs + off;
+        const u64* dp = fin.addend.ptr && c < fin.addend.np ? fin.addend.ptr + (long)bb * fin.addend.bs + (long)c * fin.addend.ps + off : nullptr;
+        u64* op = fin.out + (long)bb * fin.obs + (long)c * fin.ops + off;
+        const double f = fin.dinvf[i], w = tw_w(f, q);
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
+            const double conv = u2d((u64)__double_as_longlong(s[r * 16 * kPadF + (cc >> 4) * kPadF + (cc & 15)]));
+            double v = fmul_rem(u2d(ap[e]) - conv, w, f, q);
+            if (dp) v += u2d(dp[e]);
+            op[e] = fcanon(v, q, qi);
+        }
     }
 }
 
