@@ -407,6 +407,8 @@ static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse
 
 static bool g_ntt_generic = getenv("AESFHE_NTT_GENERIC") != nullptr;
 static bool g_no_fuse = getenv("AESFHE_NO_FUSE") != nullptr;  // unfused key-switch epilogues (A/B)
+// base conversions: output-limb groups per coefficient (inputs are re-read once per group)
+static int g_bconv_groups = getenv("AESFHE_BCONV_GROUPS") ? atoi(getenv("AESFHE_BCONV_GROUPS")) : 1;
 // the N = 2^16 fp64 passes with fused epilogues are available
 static bool fused_ntt(const aesfhe_engine* e) { return e->logN == 16 && !g_ntt_generic && !g_ntt_int && !g_no_fuse; }
 
@@ -1315,7 +1317,7 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
         // 2. ModUp base conversion of digit j to every other limb, then NTT those limbs
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
-            hipLaunchKernelGGL(k_modup, dim3(N / 256, (ne + 15) / 16, B), dim3(256), 0, e->stream, (const u64*)dc.p, lN, exj, neN, lo, alpha, l, ne,
+            hipLaunchKernelGGL(k_modup, dim3(N / 256, g_bconv_groups, B), dim3(256), 0, e->stream, (const u64*)dc.p, lN, exj, neN, lo, alpha, l, ne,
                                (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
                                e->np, e->q, e->qinv, e->Lp1, e->logN);
         }
@@ -1350,7 +1352,7 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
     Tmp conv(e, (size_t)B * 2 * kN);
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1));
-        hipLaunchKernelGGL(k_moddown, dim3(N / 256, (lk + 1 + 15) / 16, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, r, conv.p, 2 * kN, kN, K,
+        hipLaunchKernelGGL(k_moddown, dim3(N / 256, g_bconv_groups, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, r, conv.p, 2 * kN, kN, K,
                            invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : (const double*)nullptr,
                            r ? e->mdr_dmodf + cell * e->Lp1 : (const double*)nullptr, e->Lp1, e->q, e->qinv, e->logN);
     }

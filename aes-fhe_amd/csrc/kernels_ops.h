@@ -263,8 +263,8 @@ __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ 
             y[i] = r < 0.0 ? r + qp : r;
         }
     }
-    const int t0 = blockIdx.y * 16;
-    for (int t = t0; t < t0 + 16 && t < ne; t++) {
+    const int tg = (ne + gridDim.y - 1) / gridDim.y, t0 = blockIdx.y * tg;  // targets per thread
+    for (int t = t0; t < t0 + tg && t < ne; t++) {
         if (t >= lo && t < lo + alpha) continue;
         const int pid = t <= l ? t : Lp1 + (t - l - 1);
         const double qt = (double)qall[pid], qti = qinvall[pid];
@@ -405,8 +405,8 @@ __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int 
             if (j < ne) u = u + y[j] * einv[j];
         v = __builtin_rint(u);
     }
-    const int i0 = blockIdx.y * 16;
-    for (int i = i0; i < i0 + 16 && i <= l - r; i++) {
+    const int ig = (l - r + 1 + gridDim.y - 1) / gridDim.y, i0 = blockIdx.y * ig;  // outputs per thread
+    for (int i = i0; i < i0 + ig && i <= l - r; i++) {
         const double q = (double)qall[i], qi = qinvall[i];
         double sum = 0.0;
         if (r > 0) {
