@@ -102,6 +102,9 @@ SIGNATURES = [
     ("aesfhe_poly2", C.c_int,
      [c_eng_p, _P(c_ct_p), C.c_int32, _P(c_ct_p), C.c_int32, _P(C.c_double), _P(C.c_double),
       C.c_int32, c_key_p, _P(c_ct_p)]),
+    ("aesfhe_poly2_int", C.c_int,
+     [c_eng_p, _P(c_ct_p), C.c_int32, _P(c_ct_p), C.c_int32, _P(C.c_int32), C.c_int32,
+      C.c_int32, c_key_p, _P(c_ct_p)]),
     ("aesfhe_ntt_host", C.c_int,
      [c_eng_p, _P(C.c_uint64), C.c_int32, _P(C.c_int32), C.c_int32]),
     ("aesfhe_bench_ntt", C.c_int,

@@ -10,8 +10,8 @@ the expensive operations disappear.  The state is carried as +-1 bits B = (-1)^b
 * SubBytes -- every Boolean function of a byte is a multilinear polynomial in its +-1 bits
   whose coefficients are its Walsh spectrum.  With M^hi_S / M^lo_T the 15 non-empty monomials
   of the high / low nibble bits (11 products each, depth 2), the 8 output bits are
-  out_t = sum_{S,T} W_t[S,T] M^hi_S M^lo_T: one fused Engine.poly2 call per row (inner sums
-  never rescaled, one relinearisation per output bit), depth 2.
+  out_t = sum_{S,T} W_t[S,T] M^hi_S M^lo_T: one fused Engine.poly2_int call per row (64 W is
+  an integer in [-8, 8]: exact integer inner sums, one relinearisation per output bit), depth 2.
 * MixColumns + AddRoundKey -- XOR is multiplication.  With a_r the SubBytes bytes of row r and
   U_r = a_r ^ a_{r+1}: out_r = xtime(a_r ^ a_{r+1}) ^ a_{r+1} ^ a_{r+2} ^ a_{r+3}
   = xtime(U_r) ^ U_{r+1} ^ a_{r+3}; xtime(u)_j = u_{j-1} (j = 0: u_7), times u_7 for j in
@@ -55,6 +55,8 @@ class AESRowRound:
         self.sc = engine.slot_count
         self.n_blk = self.sc // 4
         self.W = walsh_sbox()
+        self.W64 = np.rint(self.W * 64).astype(np.int32)  # 64 W is an integer in [-8, 8]
+        assert np.array_equal(self.W64 / 64.0, self.W)
         if rotation_keys is None:
             rotation_keys = {r: engine.create_fixed_rotation_key(sk, -r * self.n_blk) for r in (1, 2, 3)}
         self.rot_keys = rotation_keys
@@ -128,8 +130,8 @@ class AESRowRound:
         for row in bits:
             mh = self.monomials(row[4:8])
             ml = self.monomials(row[0:4])
-            out.append(self.e.poly2([mh[i] for i in range(1, 16)], [ml[j] for j in range(1, 16)],
-                                    self.W, self.rlk))
+            out.append(self.e.poly2_int([mh[i] for i in range(1, 16)], [ml[j] for j in range(1, 16)],
+                                        self.W64, 64, self.rlk))
         return out
 
     def _xtime_terms(self, U, r, j):

@@ -481,6 +481,26 @@ class Engine:
                                     _as_ptr(im, C.c_double), m, relinearization_key._h, outs))
         return [self._ct(outs[i]) for i in range(m)]
 
+    def poly2_int(self, x_basis: Sequence[Ciphertext], y_basis: Sequence[Ciphertext], weights,
+                  den: int, relinearization_key: RelinearizationKey) -> list:
+        """poly2 with integer-weight coefficients C = weights / den (aesfhe_poly2_int): exact
+        integer inner sums, one constant per pair of basis levels."""
+        Wi = np.asarray(weights)
+        if Wi.ndim == 2:
+            Wi = Wi[None]
+        if not np.array_equal(Wi, np.round(Wi)):
+            raise ValueError("poly2_int: weights must be integers")
+        Wi = np.ascontiguousarray(Wi, dtype=np.int32)
+        m, nx, ny = Wi.shape
+        if len(x_basis) != nx - 1 or len(y_basis) != ny - 1:
+            raise ValueError("poly2_int: basis lengths must be nx-1 and ny-1")
+        xa = (c_ct_p * max(nx - 1, 1))(*[c._h for c in x_basis])
+        ya = (c_ct_p * max(ny - 1, 1))(*[c._h for c in y_basis])
+        outs = (c_ct_p * m)()
+        self._check(self._lib.poly2_int(self._h, xa, nx, ya, ny, _as_ptr(Wi, C.c_int32), int(den), m,
+                                        relinearization_key._h, outs))
+        return [self._ct(outs[i]) for i in range(m)]
+
     def align(self, cts: Sequence[Ciphertext], level: int | None = None) -> list:
         """Exact-scale level-down of every ciphertext to `level` (default: the lowest)."""
         level = min(c.level for c in cts) if level is None else level

@@ -1855,6 +1855,161 @@ extern "C" int aesfhe_poly2(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_
     API_END
 }
 
+// Integer-weight bivariate polynomial: out_t = sum_{i,j} (w[t][i][j] / den) x^i y^j (the Walsh
+// spectra of Boolean functions are of this form).  Constant rule (oracle: aesfhe_poly2_int):
+// classes cx(i) = 0 for i = 0, else 1 + rank of level(x^i) among the distinct x levels (highest
+// first); cy likewise.  H(cx, cy) = llround(S1 * r_x * r_y / den) mod q, times R = llround(D_l)
+// for cx = 0 and again for cy = 0, with S1, r_x, r_y as in aesfhe_poly2; F_ij = w_ij * H mod q.
+// Output: level l - 2, scale exactly D_{l-2} (up to the rounding of H).
+extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_t nx, const aesfhe_ct* const* yb, int32_t ny, const int32_t* w, int32_t den, int32_t m, const aesfhe_key* rlk, aesfhe_ct** outs) {
+    API_BEGIN
+    if (nx < 1 || ny < 1 || nx > kPoly2Max || ny > kPoly2Max || m < 1)
+        throw_err(AESFHE_EARG, "poly2 needs 1 <= nx, ny <= %d and m >= 1", kPoly2Max);
+    if (nx + ny < 3) throw_err(AESFHE_EARG, "poly2 needs at least one basis ciphertext");
+    if (den < 1) throw_err(AESFHE_EARG, "poly2_int needs den >= 1");
+    if (!rlk || rlk->kind != 2) throw_err(AESFHE_EARG, "poly2 needs a relinearization key");
+    int l = INT32_MAX, B = 1;
+    auto check = [&](const aesfhe_ct* c) {
+        if (c->np != 2) throw_err(AESFHE_EDEGREE, "poly2 inputs should have 2 polynomials");
+        if (c->is_zero) throw_err(AESFHE_EARG, "poly2 basis ciphertext is zero");
+        l = std::min(l, c->level);
+        B = std::max(B, c->B);
+    };
+    for (int i = 0; i < nx - 1; i++) check(xb[i]);
+    for (int j = 0; j < ny - 1; j++) check(yb[j]);
+    for (int i = 0; i < nx - 1; i++)
+        if (xb[i]->B != B && xb[i]->B != 1) throw_err(AESFHE_EARG, "batch mismatch");
+    for (int j = 0; j < ny - 1; j++)
+        if (yb[j]->B != B && yb[j]->B != 1) throw_err(AESFHE_EARG, "batch mismatch");
+    if (l < 2) throw_err(AESFHE_ELEVEL, "no level left for a bivariate polynomial");
+    for (int t = 0; t < m; t++)
+        for (int i = 0; i < nx; i++) {
+            long sum = 0;
+            for (int j = 0; j < ny; j++) sum += std::labs((long)w[((size_t)t * nx + i) * ny + j]);
+            if (sum > 512) throw_err(AESFHE_EARG, "poly2_int: sum of |w| over a row exceeds 512");
+        }
+    const int nl = l + 1, N = e->N;
+    const double* D = e->chain.scale.data();
+    const double S1 = D[l - 2] / D[l] * ((double)e->chain.q[l] / D[l]) * (double)e->chain.q[l - 1];
+    const int64_t R = llround(D[l]);
+    // classes by level (highest first); y sorted so each class is a contiguous run of j
+    auto classes = [&](const aesfhe_ct* const* b, int n, std::vector<int>& cls, std::vector<int>& lev) {
+        lev.clear();
+        for (int i = 0; i < n - 1; i++)
+            if (std::find(lev.begin(), lev.end(), b[i]->level) == lev.end()) lev.push_back(b[i]->level);
+        std::sort(lev.rbegin(), lev.rend());
+        cls.assign(n, 0);
+        for (int i = 1; i < n; i++) cls[i] = 1 + (int)(std::find(lev.begin(), lev.end(), b[i - 1]->level) - lev.begin());
+    };
+    std::vector<int> cx, cy0, lx, ly;
+    classes(xb, nx, cx, lx);
+    classes(yb, ny, cy0, ly);
+    std::vector<int> perm(ny), permx(nx);  // perm[j'] = original j (classes contiguous)
+    for (int j = 0; j < ny; j++) perm[j] = j;
+    for (int i = 0; i < nx; i++) permx[i] = i;
+    std::stable_sort(perm.begin() + 1, perm.end(), [&](int a, int b) { return cy0[a] < cy0[b]; });
+    std::stable_sort(permx.begin() + 1, permx.end(), [&](int a, int b) { return cx[a] < cx[b]; });
+    std::vector<int> cy(ny), cxs(nx);
+    for (int j = 0; j < ny; j++) cy[j] = cy0[perm[j]];
+    for (int i = 0; i < nx; i++) cxs[i] = cx[permx[i]];
+    const int cxn = 1 + (int)lx.size(), cyn = 1 + (int)ly.size();
+    // weights (permuted), live outputs
+    std::vector<int> live;
+    std::vector<double> Wt;
+    for (int t = 0; t < m; t++) {
+        bool any = false;
+        for (size_t c = 0; c < (size_t)nx * ny; c++) any |= w[(size_t)t * nx * ny + c] != 0;
+        if (!any) {
+            outs[t] = nullptr;
+            continue;
+        }
+        live.push_back(t);
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < ny; j++) Wt.push_back((double)w[((size_t)t * nx + permx[i]) * ny + perm[j]]);
+    }
+    const int ml = (int)live.size();
+    if (ml > 0) {
+        // y' factors Rt[c][cy] = H(c, cy), C0[c] = H(c, 0)
+        std::vector<TwD> Rt((size_t)nl * cxn * cyn);
+        std::vector<double> C0((size_t)nl * cxn);
+        for (int li = 0; li < nl; li++) {
+            const u64 q = e->chain.q[li];
+            const u64 r1 = h_smod(R, q);
+            std::vector<u64> H((size_t)cxn * cyn);
+            for (int a = 0; a < cxn; a++)
+                for (int b = 0; b < cyn; b++) {
+                    const double rx = a == 0 ? 1.0 : D[l] / D[lx[a - 1]];
+                    const double ry = b == 0 ? 1.0 : D[l] / D[ly[b - 1]];
+                    u64 h = h_smod(llround(S1 * rx * ry / (double)den), q);
+                    if (a == 0) h = h_mulmod(h, r1, q);
+                    if (b == 0) h = h_mulmod(h, r1, q);
+                    H[(size_t)a * cyn + b] = h;
+                }
+            for (int a = 0; a < cxn; a++) {
+                C0[(size_t)li * cxn + a] = (double)H[(size_t)a * cyn];
+                for (int b = 0; b < cyn; b++) {
+                    const u64 v = H[(size_t)a * cyn + b];
+                    Rt[((size_t)li * cxn + a) * cyn + b] = TwD{(double)v, (double)v / (double)q};
+                }
+            }
+        }
+        std::vector<const u64*> px, py;
+        std::vector<long> sx, sy, qx, qy;
+        for (int i = 1; i < nx; i++) {
+            const View v = view_of(xb[permx[i] - 1]);
+            if (v.B > 1 && v.bs != (long)v.np * v.ps) throw_err(AESFHE_EARG, "poly2: non-compact basis view");
+            px.push_back(v.d), sx.push_back(v.B == 1 && B > 1 ? 0 : v.bs), qx.push_back(v.ps);
+        }
+        for (int j = 1; j < ny; j++) {
+            const View v = view_of(yb[perm[j] - 1]);
+            if (v.B > 1 && v.bs != (long)v.np * v.ps) throw_err(AESFHE_EARG, "poly2: non-compact basis view");
+            py.push_back(v.d), sy.push_back(v.B == 1 && B > 1 ? 0 : v.bs), qy.push_back(v.ps);
+        }
+        if (px.empty()) px.push_back(nullptr), sx.push_back(0), qx.push_back(0);
+        if (py.empty()) py.push_back(nullptr), sy.push_back(0), qy.push_back(0);
+        auto dpx = upload_small(e, px.data(), px.size());
+        auto dpy = upload_small(e, py.data(), py.size());
+        auto dsx = upload_small(e, sx.data(), sx.size());
+        auto dsy = upload_small(e, sy.data(), sy.size());
+        auto dqx = upload_small(e, qx.data(), qx.size());
+        auto dqy = upload_small(e, qy.data(), qy.size());
+        std::vector<int> xstart(cxn + 1, nx);
+        for (int i = nx - 1; i >= 0; i--) xstart[cxs[i]] = i;
+        auto dcx = upload_small(e, xstart.data(), xstart.size());
+        auto dcy = upload_small(e, cy.data(), cy.size());
+        auto dW = upload_small(e, Wt.data(), Wt.size());
+        auto dR = upload_small(e, Rt.data(), Rt.size());
+        auto dC0 = upload_small(e, C0.data(), C0.size());
+        const long obs = 3L * nl * N;
+        aesfhe_ct* d3 = ct_new(e, ml * B, 3, l);
+        {
+            ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml));
+            for (int t0 = 0; t0 < ml; t0 += kPoly2Out)
+                for (int la = 0; la < nl;) {  // runs of limbs of one prime-size class
+                    const bool big = e->chain.q[la] >= (1ULL << 42);
+                    int lb = la + 1;
+                    while (lb < nl && (e->chain.q[lb] >= (1ULL << 42)) == big) lb++;
+                    hipLaunchKernelGGL(big ? k_poly2_int<true> : k_poly2_int<false>, dim3(N / 256, lb - la, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny,
+                                       (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, ml, t0, std::min(kPoly2Out, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN);
+                    la = lb;
+                }
+        }
+        HIPC(hipGetLastError());
+        aesfhe_ct* r2 = relin_rescale(e, d3, rlk, 2);
+        aesfhe_ct_free(d3);
+        const size_t per_out = (size_t)B * 2 * (l - 1) * N;
+        for (int t = 0; t < ml; t++) {
+            aesfhe_ct* o = ct_new(e, B, 2, l - 2);
+            HIPC(hipMemcpyAsync(o->d, r2->d + t * per_out, per_out * 8, hipMemcpyDeviceToDevice, e->stream));
+            outs[live[t]] = o;
+        }
+        aesfhe_ct_free(r2);
+    }
+    for (int t = 0; t < m; t++)
+        if (!outs[t]) outs[t] = ct_zero_new(e, B, 2, l - 2);
+    API_END
+}
+
 // -----------------------------------------------------------------------------------------------
 // raw NTT entry points
 extern "C" int aesfhe_ntt_host(aesfhe_engine* e, uint64_t* limbs, int32_t nlimb, const int32_t* pids, int32_t inv) {

@@ -661,4 +661,115 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
     }
 }
 
+// Integer-weight bivariate polynomial (aesfhe_poly2_int): out_t = sum (w_tij / den) x^i y^j.
+// Constants factor as F_ij = w_ij * H(cx(i), cy(j)) (classes: x^0 / y^0 and one per basis level).
+// The H factor lives on the y basis: y'_j = H(c, cy(j)) * y_j for the current x class c (x is
+// sorted by class; entering class c multiplies y' by Rt[c][cy(j)] = H(c,cy) H(c-1,cy)^{-1}, or
+// H(0,cy) for c = 0), so every inner sum is a_i = c0 * w_i0 + sum_j w_ij y'_j with small integer
+// weights: exact fp64 FMAs for primes below 2^42 (|a| <= (wsum+1) q < 2^52, host-checked), no
+// folding; the tensor accumulators stay below 2^49 without folding.  Larger primes (q_0) use
+// remainder products and fold.  Wt: [mtot][nx][ny] doubles (scalar loads), Rt: [nl][cxn][cyn]
+// {w, w/q}, C0: [nl][cxn] = H(c, 0) as doubles, xstart[c]..xstart[c+1]: the i of class c.  BIG: the q >= 2^42 path; the host launches
+// each run of limbs of one size class (limbs l0 .. l0 + gridDim.y - 1 of nl).  grid (N/256, run, B)
+template <bool BIG>
+__global__ void __launch_bounds__(256) k_poly2_int(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
+                        const long* __restrict__ xps, int nx, const u64* const* __restrict__ yp,
+                        const long* __restrict__ ybs, const long* __restrict__ yps, int ny,
+                        const int* __restrict__ xstart, const int* __restrict__ ycls, int cxn,
+                        int cyn, const double* __restrict__ Wt, const TwD* __restrict__ Rt,
+                        const double* __restrict__ C0, int mtot, int t0, int mc,
+                        u64* __restrict__ out, long oos, long obs, const u64* __restrict__ qs,
+                        const double* __restrict__ qinv, int l0, int nl, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = l0 + blockIdx.y, bb = blockIdx.z;
+    const double q = (double)qs[l];
+    const double qi = qinv[l];
+    constexpr bool big = BIG;
+    const long off = ((long)l << logN) + k;
+    double d0[kPoly2Out], d1[kPoly2Out], d2[kPoly2Out];
+#pragma unroll
+    for (int t = 0; t < kPoly2Out; t++) d0[t] = d1[t] = d2[t] = 0.0;
+    const TwD* Rl = Rt + (size_t)l * cxn * cyn;
+#pragma unroll 1
+    for (int c = 0; c < cxn; c++) {  // x classes in order: y' = H(c, cy(j)) * y_j, reloaded
+        const TwD* Rc = Rl + c * cyn;
+        double y0[kPoly2Max - 1], y1[kPoly2Max - 1];
+#pragma unroll
+        for (int j = 0; j < kPoly2Max - 1; j++) {
+            y0[j] = y1[j] = 0.0;
+            if (j < ny - 1) {
+                const u64* p = yp[j] + (long)bb * ybs[j] + off;
+                const TwD r = Rc[ycls[j + 1]];
+                y0[j] = fred(fmul_rem_r(u2d(p[0]), r.w, r.wq, q), q, qi);
+                y1[j] = fred(fmul_rem_r(u2d(p[yps[j]]), r.w, r.wq, q), q, qi);
+            }
+        }
+        const double c0 = C0[(size_t)l * cxn + c];
+#pragma unroll 1
+    for (int i = xstart[c]; i < xstart[c + 1]; i++) {
+        double xa = 0.0, xb = 0.0;
+        if (i > 0) {
+            const u64* p = xp[i - 1] + (long)bb * xbs[i - 1] + off;
+            xa = u2d(p[0]);
+            xb = u2d(p[xps[i - 1]]);
+        }
+#pragma unroll
+        for (int t = 0; t < kPoly2Out; t++) {
+            if (t < mc) {
+                const double* w = Wt + ((size_t)(t0 + t) * nx + i) * ny;
+                double a0, a1;
+                if constexpr (!big) {
+                    a0 = w[0] * c0;  // exact: |w0| <= 1024, c0 < 2^42
+                    a1 = 0.0;
+#pragma unroll
+                    for (int j = 1; j < kPoly2Max; j++) {
+                        if (j < ny) {
+                            a0 = __builtin_fma(w[j], y0[j - 1], a0);
+                            a1 = __builtin_fma(w[j], y1[j - 1], a1);
+                        }
+                    }
+                } else {
+                    const double w0 = w[0];
+                    a0 = fmul_rem(c0, w0, w0 * qi, q);
+                    a1 = 0.0;
+#pragma unroll
+                    for (int j = 1; j < kPoly2Max; j++) {
+                        if (j < ny) {
+                            const double wj = w[j], wjq = wj * qi;
+                            a0 = fred(a0 + fmul_rem(y0[j - 1], wj, wjq, q), q, qi);
+                            a1 = fred(a1 + fmul_rem(y1[j - 1], wj, wjq, q), q, qi);
+                        }
+                    }
+                }
+                if (i == 0) {
+                    d0[t] += a0;
+                    d1[t] += a1;
+                } else {
+                    const double a0q = a0 * qi, a1q = a1 * qi;
+                    d0[t] += fmul_rem(xa, a0, a0q, q);
+                    d1[t] += fmul_rem(xa, a1, a1q, q) + fmul_rem(xb, a0, a0q, q);
+                    d2[t] += fmul_rem(xb, a1, a1q, q);
+                }
+                if constexpr (big) {
+                    d0[t] = fred(d0[t], q, qi);
+                    d1[t] = fred(d1[t], q, qi);
+                    d2[t] = fred(d2[t], q, qi);
+                }
+            }
+        }
+    }
+    }
+    u64* o = out + (long)bb * obs + off;
+    const long pstr = (long)nl << logN;
+#pragma unroll
+    for (int t = 0; t < kPoly2Out; t++) {
+        if (t < mc) {
+            u64* ot = o + (long)(t0 + t) * oos;
+            ot[0] = fcanon(d0[t], q, qi);
+            ot[pstr] = fcanon(d1[t], q, qi);
+            ot[2 * pstr] = fcanon(d2[t], q, qi);
+        }
+    }
+}
+
 }  // namespace aesfhe

@@ -221,6 +221,15 @@ int aesfhe_dot(aesfhe_engine *eng, const aesfhe_ct *const *a, const aesfhe_ct *c
 int aesfhe_poly2(aesfhe_engine *eng, const aesfhe_ct *const *xb, int32_t nx,
                  const aesfhe_ct *const *yb, int32_t ny, const double *re, const double *im,
                  int32_t m, const aesfhe_key *rlk, aesfhe_ct **outs);
+/* aesfhe_poly2 for integer-weight coefficients C[t][i][j] = w[t][i][j] / den (Walsh spectra of
+ * Boolean functions -- the S-box bits of the bench round, aes_round_bits.py): constants
+ * F_ij = w_ij * H(class_x(i), class_y(j)) mod q, one H = llround(S1 * r_x * r_y / den)
+ * (x R for an x^0 / y^0 factor) per pair of basis levels, so inner sums are exact integer
+ * combinations.  Classes: 0 for x^0 / y^0, then one per distinct basis level, highest first.
+ * Requires sum_j |w[t][i][j]| <= 512.  Output level l - 2, scale D_{l-2}. */
+int aesfhe_poly2_int(aesfhe_engine *eng, const aesfhe_ct *const *xb, int32_t nx,
+                     const aesfhe_ct *const *yb, int32_t ny, const int32_t *w, int32_t den,
+                     int32_t m, const aesfhe_key *rlk, aesfhe_ct **outs);
 
 /* ---- raw kernels (known-answer tests and roofline measurement) ------------------------- */
 /* In-place forward (inverse=0) / inverse NTT of nlimb host limbs; limb i uses prime pids[i]

@@ -1711,6 +1711,133 @@ int aesfhe_poly2(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, const
     return 0;
 }
 
+/* Integer-weight bivariate polynomial (include/aesfhe.h aesfhe_poly2_int): term by term with
+ * F_ij = w_ij * H(cx(i), cy(j)) mod q; classes cx = 0 for x^0, else 1 + rank of the basis level
+ * among the distinct levels (highest first); H = llround(S1 * r_x * r_y / den) mod q (times R
+ * per x^0 / y^0 factor).  Tensor, relinearisation and two rescales as aesfhe_poly2. */
+static int level_class(const aesfhe_ct *const *b, int n, int i, int *lev, int *nlev) {
+    if (i == 0) return 0;
+    (void)n;
+    int L = b[i - 1]->level, rank = 0;
+    for (int k = 0; k < *nlev; k++)
+        if (lev[k] > L) rank++;
+    return 1 + rank;
+}
+
+int aesfhe_poly2_int(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, const aesfhe_ct *const *yb,
+                     int32_t ny, const int32_t *w, int32_t den, int32_t m, const aesfhe_key *rlk,
+                     aesfhe_ct **outs) {
+    if (nx < 1 || ny < 1 || nx > 16 || ny > 16 || m < 1)
+        return fail(AESFHE_EARG, "poly2 needs 1 <= nx, ny <= %d and m >= 1", 16);
+    if (nx + ny < 3) return fail(AESFHE_EARG, "poly2 needs at least one basis ciphertext");
+    if (den < 1) return fail(AESFHE_EARG, "poly2_int needs den >= 1");
+    if (!rlk || rlk->kind != 2) return fail(AESFHE_EARG, "poly2 needs a relinearization key");
+    const aesfhe_ct *all[32] = {0};
+    int na = 0;
+    for (int i = 0; i < nx - 1; i++) all[na++] = xb[i];
+    for (int j = 0; j < ny - 1; j++) all[na++] = yb[j];
+    int l = all[0]->level, B = 1;
+    for (int a = 0; a < na; a++) {
+        if (all[a]->npoly != 2) return fail(AESFHE_EDEGREE, "poly2 inputs should have 2 polynomials");
+        if (all[a]->is_zero) return fail(AESFHE_EARG, "poly2 basis ciphertext is zero");
+        if (all[a]->level < l) l = all[a]->level;
+        if (all[a]->B > B) B = all[a]->B;
+    }
+    for (int a = 0; a < na; a++)
+        if (all[a]->B != B && all[a]->B != 1) return fail(AESFHE_EARG, "batch mismatch");
+    if (l < 2) return fail(AESFHE_ELEVEL, "no level left for a bivariate polynomial");
+    for (int t = 0; t < m; t++)
+        for (int i = 0; i < nx; i++) {
+            long sum = 0;
+            for (int j = 0; j < ny; j++) sum += labs((long)w[((size_t)t * nx + i) * ny + j]);
+            if (sum > 512) return fail(AESFHE_EARG, "poly2_int: sum of |w| over a row exceeds 512");
+        }
+    const double *D = e->scales;
+    const double S1 = D[l - 2] / D[l] * ((double)e->q[l] / D[l]) * (double)e->q[l - 1];
+    const i64 R = llround(D[l]);
+    int levx[16], nlx = 0, levy[16], nly = 0;  /* distinct basis levels */
+    for (int i = 0; i < nx - 1; i++) {
+        int f = 0;
+        for (int k = 0; k < nlx; k++) f |= levx[k] == xb[i]->level;
+        if (!f) levx[nlx++] = xb[i]->level;
+    }
+    for (int j = 0; j < ny - 1; j++) {
+        int f = 0;
+        for (int k = 0; k < nly; k++) f |= levy[k] == yb[j]->level;
+        if (!f) levy[nly++] = yb[j]->level;
+    }
+    int cx[16], cy[16];
+    for (int i = 0; i < nx; i++) cx[i] = level_class(xb, nx, i, levx, &nlx);
+    for (int j = 0; j < ny; j++) cy[j] = level_class(yb, ny, j, levy, &nly);
+    /* level of each class (index 1..): the class rank order */
+    double rxc[17], ryc[17];
+    rxc[0] = ryc[0] = 1.0;
+    for (int i = 1; i < nx; i++) rxc[cx[i]] = D[l] / D[xb[i - 1]->level];
+    for (int j = 1; j < ny; j++) ryc[cy[j]] = D[l] / D[yb[j - 1]->level];
+    const int N = e->N;
+    aesfhe_ct *al[32];
+    for (int a = 0; a < na; a++) al[a] = truncate_ct(e, all[a], l);
+    aesfhe_ct **X = al, **Y = al + (nx - 1);
+    for (int t = 0; t < m; t++) {
+        int any = 0;
+        for (int c = 0; c < nx * ny; c++) any |= w[(size_t)t * nx * ny + c] != 0;
+        if (!any) {
+            outs[t] = ct_new(e, B, 2, l - 2);
+            outs[t]->is_zero = 1;
+            continue;
+        }
+        aesfhe_ct *acc = ct_new(e, B, 3, l);
+#pragma omp parallel for schedule(static)
+        for (int li = 0; li <= l; li++) {
+            const u64 q = e->q[li];
+            const mont_t *mt = &e->mont[li];
+            const u64 r1 = smod(R, q);
+            u64 F[16][16], Fp[16][16];
+            for (int i = 0; i < nx; i++)
+                for (int j = 0; j < ny; j++) {
+                    u64 h = smod(llround(S1 * rxc[cx[i]] * ryc[cy[j]] / (double)den), q);
+                    if (cx[i] == 0) h = mul_mod_slow(h, r1, q);
+                    if (cy[j] == 0) h = mul_mod_slow(h, r1, q);
+                    F[i][j] = mul_mod_slow(smod(w[((size_t)t * nx + i) * ny + j], q), h, q);
+                    Fp[i][j] = shoup_pre(F[i][j], q);
+                }
+            for (int b = 0; b < B; b++) {
+                u64 *d0 = limb(e, acc, b, 0, li), *d1 = limb(e, acc, b, 1, li), *d2 = limb(e, acc, b, 2, li);
+                for (int k = 0; k < N; k++) {
+                    u64 s0 = 0, s1 = 0, s2 = 0;
+                    for (int i = 0; i < nx; i++) {
+                        u64 a0 = F[i][0], a1 = 0;
+                        for (int j = 1; j < ny; j++) {
+                            const aesfhe_ct *y = Y[j - 1];
+                            const int yb_ = y->B == 1 ? 0 : b;
+                            a0 = add_mod(a0, mul_shoup(limb(e, y, yb_, 0, li)[k], F[i][j], Fp[i][j], q), q);
+                            a1 = add_mod(a1, mul_shoup(limb(e, y, yb_, 1, li)[k], F[i][j], Fp[i][j], q), q);
+                        }
+                        if (i == 0) {
+                            s0 = add_mod(s0, a0, q);
+                            s1 = add_mod(s1, a1, q);
+                        } else {
+                            const aesfhe_ct *x = X[i - 1];
+                            const int xb_ = x->B == 1 ? 0 : b;
+                            const u64 x0 = limb(e, x, xb_, 0, li)[k], x1 = limb(e, x, xb_, 1, li)[k];
+                            s0 = add_mod(s0, mul_mod(x0, a0, mt), q);
+                            s1 = add_mod(s1, add_mod(mul_mod(x0, a1, mt), mul_mod(x1, a0, mt), q), q);
+                            s2 = add_mod(s2, mul_mod(x1, a1, mt), q);
+                        }
+                    }
+                    d0[k] = s0;
+                    d1[k] = s1;
+                    d2[k] = s2;
+                }
+            }
+        }
+        outs[t] = relin_rescale_raw(e, acc, rlk, 2);
+        aesfhe_ct_free(acc);
+    }
+    for (int a = 0; a < na; a++) aesfhe_ct_free(al[a]);
+    return 0;
+}
+
 int aesfhe_ntt_host(aesfhe_engine *e, uint64_t *limbs, int32_t nlimb, const int32_t *pids, int32_t inv) {
     for (int i = 0; i < nlimb; i++)
         if (pids[i] < 0 || pids[i] >= e->np) return fail(AESFHE_EARG, "bad prime index");

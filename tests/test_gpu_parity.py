@@ -156,3 +156,24 @@ def test_poly2_bit_exact(product_lib, oracle_lib, gpu_available):
     dec = g.decrypt(res[0][0], kg["sk"])
     want = sum(C[0, i, j] * zx ** i * zy ** j for i in range(4) for j in range(3))
     np.testing.assert_allclose(dec, want, atol=1e-4)
+
+
+def test_poly2_int_bit_exact(product_lib, oracle_lib, gpu_available):
+    """Integer-weight bivariate evaluation: 6 outputs (two chunks), a zero output, mixed basis
+    levels (power bases), a broadcast basis element, negative weights."""
+    g, o = _pair(product_lib, oracle_lib, **SMALL)
+    kg, ko = _keys(g), _keys(o)
+    rng = np.random.default_rng(8)
+    zx = np.exp(-2j * np.pi * rng.integers(0, 16, (2, g.slot_count)) / 16)
+    zy = np.exp(-2j * np.pi * rng.integers(0, 16, g.slot_count) / 16)
+    W = rng.integers(-8, 9, (6, 4, 5))
+    W[2] = 0
+    res = []
+    for eng, k in ((g, kg), (o, ko)):
+        xb = eng.make_power_basis(eng.encrypt(zx, k["pk"]), 3, k["rlk"])
+        yb = eng.make_power_basis(eng.encrypt(zy, k["pk"]), 4, k["rlk"])
+        res.append(eng.poly2_int(xb, yb, W, 64, k["rlk"]))
+    for a, b in zip(*res):
+        _same(g, o, a, b)
+    want = sum(W[0, i, j] / 64 * zx ** i * zy ** j for i in range(4) for j in range(5))
+    np.testing.assert_allclose(g.decrypt(res[0][0], kg["sk"]), want, atol=1e-4)

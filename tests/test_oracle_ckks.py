@@ -150,3 +150,23 @@ def test_poly2_semantics(env):
         e.poly2(xb[:2], yb, C, rlk)
     with pytest.raises(RuntimeError, match="at least one basis"):
         e._check(e._lib.poly2(e._h, None, 1, None, 1, None, None, 1, None, None))
+
+
+def test_poly2_int_semantics(env):
+    """aesfhe_poly2_int = sum (w/den) x^i y^j at level l-2, basis at mixed levels."""
+    e, sk, pk, rlk, _ = env
+    rng = np.random.default_rng(10)
+    zx = np.exp(-2j * np.pi * rng.integers(0, 16, e.slot_count) / 16)
+    zy = np.exp(-2j * np.pi * rng.integers(0, 16, e.slot_count) / 16)
+    xb = e.make_power_basis(e.encrypt(zx, pk), 3, rlk)
+    yb = e.make_power_basis(e.encrypt(zy, pk), 4, rlk)
+    W = rng.integers(-8, 9, (3, 4, 5))
+    W[1] = 0
+    outs = e.poly2_int(xb, yb, W, 64, rlk)
+    lv = min(c.level for c in xb + yb)
+    for t in range(3):
+        assert outs[t].level == lv - 2
+        want = sum(W[t, i, j] / 64 * zx ** i * zy ** j for i in range(4) for j in range(5))
+        np.testing.assert_allclose(e.decrypt(outs[t], sk), want, atol=1e-4)
+    with pytest.raises(RuntimeError, match="exceeds 512"):
+        e.poly2_int(xb, yb, np.full((1, 4, 5), 300), 64, rlk)
