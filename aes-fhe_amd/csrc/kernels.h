@@ -54,33 +54,26 @@ __device__ __forceinline__ u64 mul_w(u64 a, u64 w, double wq, u64 q) {
 }
 
 // ---- all-fp64 modular arithmetic on exact integers carried in doubles (|x| < 2^52) ----------
-// a*w - rint(a*w/q)*q computed exactly: p + pl = a*w (fma split), t + tl = qh*q, and
-// (p - t) + (pl - tl) has no rounding (Sterbenz once qh != 0; integers < 2^53 otherwise).
-// Result in (-q, q) when wq = w/q rounded (|quotient error| < 1); signed inputs are fine.
-// tools/mulmod_bench.hip: 2.65 T/s vs 2.17 T/s for mul_w on gfx950.
-// rint(v) = (v + 1.5*2^52) - 1.5*2^52 for |v| < 2^51 (signed: the sum stays in [2^52, 2^53))
-constexpr double kMagic52 = 6755399441055744.0;
+// r = a*w - qh*q with qh = rint(a*w/q) (quotient from w/q rounded: |a*w/q - qh| <= 1):
+// p + pl = a*w exactly (fma split); u = fma(-qh, q, p) is exact because p - qh*q is an integer
+// of magnitude <= q + |pl| < 2^53 (one rounding of an exactly representable value); r = u + pl is
+// exact for the same reason.  Six full-rate fp64 ops, |r| <= q for a constant w with wq = w/q,
+// <= 1.5q with an on-the-fly quotient wq = w * (1/q); signed a allowed (|a| < 2^52).
+// tools/mulmod_bench.hip; verified on 1.6e8 random/edge operands per prime size (CPU, same ops).
+constexpr double kMagic52 = 6755399441055744.0;  // 1.5 * 2^52: rint(v) = (v + M) - M, |v| < 2^51
 __device__ __forceinline__ double fmul_rem(double a, double w, double wq, double q) {
     const double p = a * w;
     const double pl = __builtin_fma(a, w, -p);
-    const double qh = __builtin_fma(a, wq, kMagic52) - kMagic52;
-    const double t = qh * q;
-    const double tl = __builtin_fma(qh, q, -t);
-    return (p - t) + (pl - tl);
-}
-// Same remainder with the quotient from v_rndne_f64 (no 2^52 literal: the SGPR operands w, wq
-// then fit the single constant-bus slot of a VOP3).  |a*wq - a*w/q| <= 1/2 -> |r| <= q.
-__device__ __forceinline__ double fmul_rem_r(double a, double w, double wq, double q) {
-    const double p = a * w;
-    const double pl = __builtin_fma(a, w, -p);
     const double qh = __builtin_rint(a * wq);
-    const double t = qh * q;
-    const double tl = __builtin_fma(qh, q, -t);
-    return (p - t) + (pl - tl);
+    const double u = __builtin_fma(-qh, q, p);
+    return u + pl;
+}
+__device__ __forceinline__ double fmul_rem_r(double a, double w, double wq, double q) {
+    return fmul_rem(a, w, wq, q);
 }
 // x - rint(x/q)*q for |x| < 2^53: result in [-q/2 - 1, q/2 + 1] (exact: qh*q < 2^53)
 __device__ __forceinline__ double fred(double x, double q, double qinv) {
-    const double qh = __builtin_fma(x, qinv, kMagic52) - kMagic52;
+    const double qh = __builtin_rint(x * qinv);
     return __builtin_fma(-qh, q, x);
 }
 // canonical residue in [0, q) of |x| < 2^53, as u64
@@ -92,7 +85,7 @@ __device__ __forceinline__ u64 fcanon(double x, double q, double qinv) {
 }
 // w from its table entry wq = w/q (w < q < 2^52): rint(wq * q) is exact, |wq*q - w| < 2^-4
 __device__ __forceinline__ double tw_w(double wq, double q) {
-    return __builtin_fma(wq, q, kMagic52) - kMagic52;
+    return __builtin_rint(wq * q);
 }
 // an optional operand (ptr == nullptr or component >= np reads as zero), for fused epilogues
 struct Opnd2 {

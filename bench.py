@@ -39,6 +39,21 @@ PEAK_HBM_GBS = 8000.0
 METRIC = "AES-128 blocks/sec (homomorphic full round) at N=2^16, L=30; 1/2/4/8 MI355X"
 
 
+PMC_FILE = ROOT / "profiles" / "r01" / "pmc" / "ntt_traffic.json"
+PMC_NOTE = ("HBM bytes per NTT launch = algorithmic bytes x the HBM/algorithmic ratio measured by "
+            "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 calibration) + WRITE_SIZE on the same NTT kernels "
+            "at the same parameters (profiles/r01/pmc/ntt_traffic.json)")
+
+
+def traffic_per_launch(alg_bytes):
+    """HBM bytes per NTT launch from the committed PMC measurement (None if absent)."""
+    try:
+        ratio = json.loads(PMC_FILE.read_text())["traffic_over_alg"]
+    except (OSError, ValueError, KeyError):
+        return None
+    return round(alg_bytes * ratio)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -234,9 +249,11 @@ def main():
                 "verified": ok,
             },
             "roofline": {
-                "bound": "hbm", "kernel": "ntt (k_ntt_*_cols / k_ntt_*_rows pass launches)",
+                "bound": "hbm", "kernel": "ntt (k_nttf_*_cols / k_nttf_*_rows pass launches)",
                 "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                "frac": round(achieved / PEAK_HBM_GBS, 4),
+                "traffic": traffic_per_launch(by_ntt.value / max(n_ntt.value, 1)),
+                "traffic_source": PMC_NOTE,
                 "launches": n_ntt.value, "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "alg_bytes_per_launch": round(by_ntt.value / max(n_ntt.value, 1)),
                 "ntt_share_of_step": round(ms_ntt.value / (elapsed * 1e3), 3),
