@@ -6,7 +6,8 @@ the expensive operations disappear.  The state is carried as +-1 bits B = (-1)^b
 
 * layout -- one ciphertext per state row r and bit j: slot = c * n_blk + block with
   n_blk = slot_count / 4 (8192 blocks at N = 2^16).  ShiftRows (out(r,c) = in(r, c+r)) is a
-  single whole-ciphertext rotation of row r by -r*n_blk slots, no masks (24 per 8192 blocks).
+  single whole-ciphertext rotation of row r by -r*n_blk slots, no masks (24 per 8192 blocks),
+  applied to the SubBytes output (it commutes with SubBytes; 4 levels lower = fewer limbs).
 * SubBytes -- every Boolean function of a byte is a multilinear polynomial in its +-1 bits
   whose coefficients are its Walsh spectrum.  With M^hi_S / M^lo_T the 15 non-empty monomials
   of the high / low nibble bits (11 products each, depth 2), the 8 output bits are
@@ -158,7 +159,7 @@ class AESRowRound:
         return [[self.mul(S[r][j], key[r][j]) for j in range(8)] for r in range(4)]
 
     def round(self, bits, key, timings: dict | None = None):
-        """ShiftRows -> SubBytes -> MixColumns -> AddRoundKey on the row-sliced +-1 bit state."""
+        """SubBytes -> ShiftRows -> MixColumns -> AddRoundKey on the row-sliced +-1 bit state."""
         import time
 
         def mark(name, t0):
@@ -169,10 +170,10 @@ class AESRowRound:
             timings[name] = timings.get(name, 0.0) + (t1 - t0)
             return t1
         t = mark("start", 0.0) if timings is not None else 0.0
-        bits = self.shift_rows(bits)
+        A = self.sub_bytes(bits)  # SubBytes first: ShiftRows commutes with it and is cheaper
+        t = mark("sub_bytes", t)  # on the SubBytes output (level l-4: fewer limbs per rotation)
+        A = self.shift_rows(A)
         t = mark("shift_rows", t)
-        A = self.sub_bytes(bits)
-        t = mark("sub_bytes", t)
         out = self.mix_columns_add_round_key(A, key)
         mark("mix_columns_add_round_key", t)
         return out
