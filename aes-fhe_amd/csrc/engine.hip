@@ -1370,7 +1370,8 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
         }
         RowFin f{(const u64*)acc.p, 2 * neN, neN, Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}, o->d,
                  2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf, lk + 1};
-        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+        // the row pass (credited half an NTT) plus the finish: acc read, output written (+ addend)
+        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total * (3.0 + (fin_add.ptr ? 1.0 : 0.0)));
         hipLaunchKernelGGL(k_nttf_fwd_rows_t<true>, dim3(16, total), dim3(256), 0, e->stream, sc, T, f);
         HIPC(hipGetLastError());
         return;
