@@ -252,6 +252,7 @@ def main():
                 "bound": "hbm", "kernel": "ntt (k_nttf_*_cols / k_nttf_*_rows pass launches)",
                 "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
+                "frac_per_pass_rw": round(2 * achieved / PEAK_HBM_GBS, 4),  # each pass's own read+write
                 "traffic": traffic_per_launch(by_ntt.value / max(n_ntt.value, 1)),
                 "traffic_source": PMC_NOTE,
                 "launches": n_ntt.value, "avg_launch_us": round(avg_launch_ms * 1e3, 2),

@@ -120,13 +120,13 @@ int main() {
         std::vector<double> hf(1, 1.0 / q); double* dnf; CK(hipMalloc(&dnf, 8)); CK(hipMemcpy(dnf, hf.data(), 8, hipMemcpyHostToDevice));
         T.ninvf = dnf;
         timeit("f64 fwd_cols", [&] { hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, L), dim3(256), 0, 0, s, s2, T); });
-        timeit("f64 fwd_rows", [&] { hipLaunchKernelGGL(k_nttf_fwd_rows, dim3(16, L), dim3(256), 0, 0, s2, T); });
+        timeit("f64 fwd_rows", [&] { hipLaunchKernelGGL(k_nttf_fwd_rows_t<false>, dim3(16, L), dim3(256), 0, 0, s2, T, RowFin{}); });
         timeit("f64 inv_rows", [&] { hipLaunchKernelGGL(k_nttf_inv_rows, dim3(16, L), dim3(256), 0, 0, s, s2, T); });
         timeit("f64 inv_cols", [&] { hipLaunchKernelGGL(k_nttf_inv_cols, dim3(16, L), dim3(256), 0, 0, s2, T); });
         // a 40-bit prime (no folding path)
         u64 q40 = 1099511480321ULL; CK(hipMemcpy(dq, &q40, 8, hipMemcpyHostToDevice)); double qi40 = 1.0 / q40; CK(hipMemcpy(dqi, &qi40, 8, hipMemcpyHostToDevice));
         timeit("f64 fwd_cols q40", [&] { hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, L), dim3(256), 0, 0, s, s2, T); });
-        timeit("f64 fwd_rows q40", [&] { hipLaunchKernelGGL(k_nttf_fwd_rows, dim3(16, L), dim3(256), 0, 0, s2, T); });
+        timeit("f64 fwd_rows q40", [&] { hipLaunchKernelGGL(k_nttf_fwd_rows_t<false>, dim3(16, L), dim3(256), 0, 0, s2, T, RowFin{}); });
         timeit("f64 inv_rows q40", [&] { hipLaunchKernelGGL(k_nttf_inv_rows, dim3(16, L), dim3(256), 0, 0, s, s2, T); });
         timeit("f64 inv_cols q40", [&] { hipLaunchKernelGGL(k_nttf_inv_cols, dim3(16, L), dim3(256), 0, 0, s2, T); });
         timeit("int fwd_rows q40", [&] { hipLaunchKernelGGL(k_ntt256_fwd_rows, dim3(16, L), dim3(256), 0, 0, s, T); });
