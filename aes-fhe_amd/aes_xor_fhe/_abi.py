@@ -105,6 +105,11 @@ SIGNATURES = [
     ("aesfhe_poly2_int", C.c_int,
      [c_eng_p, _P(c_ct_p), C.c_int32, _P(c_ct_p), C.c_int32, _P(C.c_int32), C.c_int32,
       C.c_int32, c_key_p, _P(c_ct_p)]),
+    ("aesfhe_key_secret_sparse", C.c_int, [c_eng_p, C.c_uint64, C.c_int32, _P(c_key_p)]),
+    ("aesfhe_key_switch", C.c_int, [c_eng_p, c_key_p, c_key_p, _P(c_key_p)]),
+    ("aesfhe_mod_raise", C.c_int, [c_eng_p, c_ct_p, C.c_int32, _P(c_ct_p)]),
+    ("aesfhe_mul_i", C.c_int, [c_eng_p, c_ct_p, C.c_int32, _P(c_ct_p)]),
+    ("aesfhe_dot_pt", C.c_int, [c_eng_p, _P(c_ct_p), _P(c_pt_p), C.c_int32, _P(c_ct_p)]),
     ("aesfhe_ntt_host", C.c_int,
      [c_eng_p, _P(C.c_uint64), C.c_int32, _P(C.c_int32), C.c_int32]),
     ("aesfhe_bench_ntt", C.c_int,

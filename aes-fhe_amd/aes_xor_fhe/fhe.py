@@ -22,7 +22,7 @@ from typing import Sequence
 
 import numpy as np
 
-from ._abi import Lib, Params, c_ct_p, load_product
+from ._abi import Lib, Params, c_ct_p, c_pt_p, load_product
 
 # HomomorphicEncryption.org 128-bit bound on log2(QP) for ternary secrets
 SECURITY_BUDGET = {11: 54, 12: 109, 13: 218, 14: 438, 15: 881, 16: 1772, 17: 3544}
@@ -299,6 +299,25 @@ class Engine:
         k.delta = int(delta)
         return k
 
+    def create_sparse_secret_key(self, hw: int, seed: int = 0) -> SecretKey:
+        """Ternary secret with exactly hw nonzeros (aesfhe_key_secret_sparse)."""
+        out = C.c_void_p()
+        self._check(self._lib.key_secret_sparse(self._h, seed, int(hw), C.byref(out)))
+        sk = SecretKey(self._lib, out.value, self._lib.key_free)
+        sk.engine = self
+        return sk
+
+    def create_switching_key(self, sk_from: SecretKey, sk_to: SecretKey) -> GaloisKey:
+        """Key switching key sk_from -> sk_to, applied with switch_key (aesfhe_key_switch)."""
+        out = C.c_void_p()
+        self._check(self._lib.key_switch(self._h, sk_from._h, sk_to._h, C.byref(out)))
+        k = GaloisKey(self._lib, out.value, self._lib.key_free)
+        k.galois_elt = 1
+        return k
+
+    def switch_key(self, ct: Ciphertext, swk: GaloisKey) -> Ciphertext:
+        return self._call_ct(self._lib.galois, ct._h, swk._h)
+
     def create_small_bootstrap_key(self, sk: SecretKey) -> BootstrapKey:
         return BootstrapKey(small=True)
 
@@ -432,6 +451,23 @@ class Engine:
             "CKKS bootstrapping is not implemented yet (SURVEY.md section 8f item 1)")
 
     # -- fused building blocks used by the optimised AES round ---------------------------------
+    def mod_raise(self, ct: Ciphertext, level: int | None = None) -> Ciphertext:
+        """Limb 0 lifted to every limb of `level` (aesfhe_mod_raise): encrypts m + q_0 I."""
+        return self._call_ct(self._lib.mod_raise, ct._h, self.max_level if level is None else int(level))
+
+    def multiply_i(self, ct: Ciphertext, sign: int = 1) -> Ciphertext:
+        """Every slot times i (sign > 0) or -i, exactly, without using a level (aesfhe_mul_i)."""
+        return self._call_ct(self._lib.mul_i, ct._h, 1 if sign > 0 else -1)
+
+    def dot_plain(self, cts: Sequence[Ciphertext], plains: Sequence["Plaintext"]) -> Ciphertext:
+        """sum_i cts[i] * plains[i] with one rescale (aesfhe_dot_pt)."""
+        n = len(cts)
+        lv = min(c.level for c in cts)
+        s = self._lib.engine_mul_scale(self._h, lv)
+        arr = (c_ct_p * n)(*[c._h for c in cts])
+        pts = (c_pt_p * n)(*[p.device(lv, s) for p in plains])
+        return self._call_ct(self._lib.dot_pt, arr, pts, n)
+
     def lincomb(self, cts: Sequence[Ciphertext], coeffs: Sequence[complex]) -> Ciphertext:
         n = len(cts)
         arr = (c_ct_p * n)(*[c._h for c in cts])

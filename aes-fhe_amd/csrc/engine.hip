@@ -863,12 +863,14 @@ extern "C" int aesfhe_key_public(aesfhe_engine* e, const aesfhe_key* sk, aesfhe_
     API_END
 }
 
-static aesfhe_key* make_ksk(aesfhe_engine* e, const aesfhe_key* sk, const u64* sprime, int kind, u64 g) {
+static aesfhe_key* make_ksk(aesfhe_engine* e, const aesfhe_key* sk, const u64* sprime, int kind, u64 g,
+                            u64 salt = 0) {
     const int N = e->N, np = e->np;
     aesfhe_key* k = key_new(e, kind, (size_t)e->dnum * 2 * np * N);
     k->galois = g;
     k->keyseed = sk->keyseed;
     u64 base = derive(derive(sk->keyseed, 4 + (u64)kind), g);
+    if (salt) base = derive(base, salt);
     Tmp et(e, (size_t)np * N);
     for (int d = 0; d < e->dnum; d++) {
         u64* kb = k->d + ((size_t)d * 2 + 0) * np * N;
@@ -900,6 +902,44 @@ extern "C" int aesfhe_key_galois(aesfhe_engine* e, const aesfhe_key* sk, uint64_
     Span src = span_s(sk->d, 0, e->np, e->Lp1, 0, e->Lp1), dst = span_s(sg.p, 0, e->np, e->Lp1, 0, e->Lp1);
     hipLaunchKernelGGL(k_galois, dim3(e->N / 256, e->np), dim3(256), 0, e->stream, src, dst, (u64)g, e->logN, e->Lp1);
     *out = make_ksk(e, sk, sg.p, 3, g);
+    API_END
+}
+
+// Sparse ternary secret with exactly hw nonzero coefficients (bootstrapping's ephemeral secret):
+// key = derive(derive(seed_e, seed), 9); partial Fisher-Yates over 0..N-1: position i swaps with
+// i + rnd(key, i) mod (N - i), the coefficient there is -1 if rnd(key, N + i) is odd else +1.
+extern "C" int aesfhe_key_secret_sparse(aesfhe_engine* e, uint64_t seed, int32_t hw, aesfhe_key** out) {
+    API_BEGIN
+    const int N = e->N;
+    if (hw < 1 || hw > N) throw_err(AESFHE_EARG, "sparse secret weight must be in [1, N]");
+    aesfhe_key* k = key_new(e, 0, (size_t)e->np * N);
+    k->keyseed = derive(e->seed, seed);
+    const u64 key = derive(k->keyseed, 9);
+    std::vector<int> idx(N);
+    for (int i = 0; i < N; i++) idx[i] = i;
+    std::vector<int64_t> co(N, 0);
+    for (int i = 0; i < hw; i++) {
+        const int j = i + (int)(rnd(key, (u64)i) % (u64)(N - i));
+        std::swap(idx[i], idx[j]);
+        co[idx[i]] = (rnd(key, (u64)N + i) & 1) ? -1 : 1;
+    }
+    Tmp dco(e, N);
+    HIPC(hipMemcpyAsync(dco.p, co.data(), (size_t)N * 8, hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, e->np, 1), dim3(256), 0, e->stream, (const i64*)dco.p, k->d, e->np, e->q, e->logN);
+    Span s = span_s(k->d, 0, e->np, e->Lp1, 0, e->Lp1);
+    s.pstride = (long)e->np * N;
+    ntt(e, s, s, e->np, false);
+    HIPC(hipStreamSynchronize(e->stream));
+    *out = k;
+    API_END
+}
+
+// Switching key from secret sk_from to sk_to (a galois-kind key with element 1: aesfhe_galois
+// applies it as a plain key switch).
+extern "C" int aesfhe_key_switch(aesfhe_engine* e, const aesfhe_key* sk_from, const aesfhe_key* sk_to, aesfhe_key** out) {
+    API_BEGIN
+    if (!sk_from || !sk_to || sk_from->kind != 0 || sk_to->kind != 0) throw_err(AESFHE_EARG, "switching key needs two secret keys");
+    *out = make_ksk(e, sk_to, sk_from->d, 3, 1, sk_from->keyseed | 1);
     API_END
 }
 
@@ -1286,6 +1326,93 @@ extern "C" int aesfhe_mul_const(aesfhe_engine* e, const aesfhe_ct* c, double re,
         mul_const_into(e, view_of(c), A, Bc, t, 0);
         *out = rescale_view(e, view_of(t));
         aesfhe_ct_free(t);
+    }
+    API_END
+}
+
+// ModRaise (bootstrapping): the level-0 content of ct (limb 0, mod q_0, centred) lifted to
+// every limb of `level`.  The result encrypts t = m + q_0 I; its scale is the caller's business.
+extern "C" int aesfhe_mod_raise(aesfhe_engine* e, const aesfhe_ct* c, int32_t level, aesfhe_ct** out) {
+    API_BEGIN
+    if (level < 0 || level > e->L) throw_err(AESFHE_EARG, "bad mod-raise level");
+    const int N = e->N, P = c->B * c->np, nl = level + 1;
+    aesfhe_ct* r = ct_new(e, c->B, c->np, level);
+    if (c->is_zero) {
+        HIPC(hipMemsetAsync(r->d, 0, r->bytes, e->stream));
+        r->is_zero = 1;
+    } else {
+        Tmp x(e, (size_t)P * N);
+        const View v = view_of(c);
+        Span src = span_s((u64*)v.d, v.ps, 1, 1, 0, e->Lp1), dx = span_s(x.p, N, 1, 1, 0, e->Lp1);
+        if (v.B > 1 && v.bs != (long)v.np * v.ps) throw_err(AESFHE_EARG, "mod-raise of non-compact view");
+        ntt(e, src, dx, P, true);
+        hipLaunchKernelGGL(k_lift0, dim3(N / 256, nl, P), dim3(256), 0, e->stream, (const u64*)x.p, r->d, nl, e->chain.q[0], e->q, e->logN);
+        HIPC(hipGetLastError());
+        Span so = span_s(r->d, (long)nl * N, nl, nl, 0, e->Lp1);
+        ntt(e, so, so, P * nl, false);
+    }
+    *out = r;
+    API_END
+}
+
+// Multiplication by X^{N/2} (sign +1) or -X^{N/2}: every slot times i / -i, exact, no level.
+extern "C" int aesfhe_mul_i(aesfhe_engine* e, const aesfhe_ct* c, int32_t sign, aesfhe_ct** out) {
+    API_BEGIN
+    aesfhe_ct* r = ct_new(e, c->B, c->np, c->level);
+    if (c->is_zero) {
+        HIPC(hipMemsetAsync(r->d, 0, r->bytes, e->stream));
+        r->is_zero = 1;
+    } else {
+        mul_const_into(e, view_of(c), 0, sign >= 0 ? 1 : -1, r, 0);
+    }
+    *out = r;
+    API_END
+}
+
+// sum_i ct_i * pt_i, one rescale (the diagonal sums of homomorphic linear transforms); plaintexts
+// must hold at least level l + 1 limbs, l = the lowest ciphertext level.
+extern "C" int aesfhe_dot_pt(aesfhe_engine* e, const aesfhe_ct* const* cts, const aesfhe_pt* const* pts, int32_t n, aesfhe_ct** out) {
+    API_BEGIN
+    if (n < 1 || n > 256) throw_err(AESFHE_EARG, "dot_pt needs 1..256 terms");
+    int l = cts[0]->level, B = 1, np = cts[0]->np;
+    for (int i = 0; i < n; i++) {
+        l = std::min(l, cts[i]->level);
+        B = std::max(B, cts[i]->B);
+        if (cts[i]->np != np) throw_err(AESFHE_EDEGREE, "dot_pt inputs should have the same number of polynomials");
+    }
+    for (int i = 0; i < n; i++) {
+        if (cts[i]->B != B && cts[i]->B != 1) throw_err(AESFHE_EARG, "batch mismatch");
+        if (pts[i]->level < l) throw_err(AESFHE_EARG, "plaintext level %d below ciphertext level %d", pts[i]->level, l);
+    }
+    if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a plaintext dot product");
+    const int nl = l + 1;
+    std::vector<std::unique_ptr<Aligned>> al;
+    std::vector<const u64*> pc, pp;
+    std::vector<long> sb;
+    for (int i = 0; i < n; i++) {
+        if (cts[i]->is_zero) continue;
+        al.emplace_back(new Aligned());
+        align_to(e, cts[i], l, *al.back());
+        const View& v = al.back()->v;
+        if (v.ps != (long)nl * e->N) throw_err(AESFHE_EARG, "dot_pt: non-compact view");
+        pc.push_back(v.d);
+        sb.push_back(v.B == 1 && B > 1 ? 0 : v.bs);
+        pp.push_back(pts[i]->d);
+    }
+    if (pc.empty()) {
+        *out = ct_zero_new(e, B, np, l - 1);
+    } else {
+        aesfhe_ct* acc = ct_new(e, B, np, l);
+        auto dpc = upload_small(e, pc.data(), pc.size());
+        auto dpp = upload_small(e, pp.data(), pp.size());
+        auto dsb = upload_small(e, sb.data(), sb.size());
+        {
+            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (pc.size() + 1));
+            hipLaunchKernelGGL(k_dot_pt, ew_grid(e, nl, B * np), dim3(256), 0, e->stream, (const u64* const*)dpc, (const long*)dsb, (long)nl * e->N, (const u64* const*)dpp, (int)pc.size(), out_of(acc), np, e->q, e->qinv, e->logN);
+        }
+        HIPC(hipGetLastError());
+        *out = rescale_view(e, view_of(acc));
+        aesfhe_ct_free(acc);
     }
     API_END
 }

@@ -772,4 +772,40 @@ __global__ void __launch_bounds__(256) k_poly2_int(const u64* const* __restrict_
     }
 }
 
+// ModRaise: x = limb 0 of every polynomial in coefficient form (mod q_0); out limb i =
+// centred x mod q_i for i < nl.  x: [P][N] (P = B * npoly), out: [P][nl][N].  grid (N/256, nl, P)
+__global__ void k_lift0(const u64* __restrict__ x, u64* __restrict__ out, int nl, u64 q0,
+                        const u64* __restrict__ qs, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y, p = blockIdx.z;
+    const u64 v = x[((long)p << logN) + k], q = qs[i];
+    u64 r;
+    if (v > (q0 >> 1)) {  // negative: v - q0
+        const u64 m = (q0 - v) % q;
+        r = m ? q - m : 0;
+    } else {
+        r = v % q;
+    }
+    out[(((long)p * nl + i) << logN) + k] = r;
+}
+
+// Sum of ciphertext x plaintext products: out[b][p][l] = sum_i ct_i[b][p][l] * pt_i[l] (lazy
+// fp64 sums folded every 4 terms).  grid (N/256, nl, B*np)
+__global__ void k_dot_pt(const u64* const* __restrict__ cp, const long* __restrict__ cbs, long cps,
+                         const u64* const* __restrict__ pp, int n, Out o, int np,
+                         const u64* __restrict__ qs, const double* __restrict__ qinv, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z / np, p = blockIdx.z - bb * np;
+    const double q = (double)qs[l], qi = qinv[l];
+    const long off = ((long)l << logN) + k;
+    double acc = 0.0;
+    for (int i = 0; i < n; i++) {
+        const double c = u2d(cp[i][(long)bb * cbs[i] + (long)p * cps + off]);
+        const double w = u2d(pp[i][off]);
+        acc += fmul_rem(c, w, w * qi, q);
+        if ((i & 3) == 3) acc = fred(acc, q, qi);
+    }
+    o.ptr[(long)bb * o.bs + (long)p * o.ps + off] = fcanon(acc, q, qi);
+}
+
 }  // namespace aesfhe

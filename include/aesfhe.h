@@ -130,6 +130,16 @@ int aesfhe_key_relin(aesfhe_engine *eng, const aesfhe_key *sk, aesfhe_key **out)
 int aesfhe_key_galois(aesfhe_engine *eng, const aesfhe_key *sk, uint64_t galois_elt,
                       aesfhe_key **out);
 uint64_t aesfhe_galois_elt(int32_t log_n, int64_t rotation, int32_t conjugate);
+/* Sparse ternary secret with exactly hw nonzeros (bootstrapping's ephemeral secret, for the
+ * ModRaise overflow bound): key = derive(derive(seed_e, seed), 9); partial Fisher-Yates over
+ * 0..N-1 -- step i swaps i with i + rnd(key, i) mod (N - i) and sets that coefficient to -1 if
+ * rnd(key, N + i) is odd, else +1.  (Replaces desilofhe's internal bootstrap key material,
+ * engine_context.py:62-73 create_bootstrap_key.) */
+int aesfhe_key_secret_sparse(aesfhe_engine *eng, uint64_t seed, int32_t hw, aesfhe_key **out);
+/* Key switching key sk_from -> sk_to; apply with aesfhe_galois (it is a galois-kind key with
+ * element 1, the identity automorphism). */
+int aesfhe_key_switch(aesfhe_engine *eng, const aesfhe_key *sk_from, const aesfhe_key *sk_to,
+                      aesfhe_key **out);
 /* kind: 0 secret 1 public 2 relin 3 galois; galois_elt for kind 3 */
 int aesfhe_key_info(const aesfhe_key *key, int32_t *kind, uint64_t *galois_elt);
 void aesfhe_key_free(aesfhe_key *key);
@@ -230,6 +240,17 @@ int aesfhe_poly2(aesfhe_engine *eng, const aesfhe_ct *const *xb, int32_t nx,
 int aesfhe_poly2_int(aesfhe_engine *eng, const aesfhe_ct *const *xb, int32_t nx,
                      const aesfhe_ct *const *yb, int32_t ny, const int32_t *w, int32_t den,
                      int32_t m, const aesfhe_key *rlk, aesfhe_ct **outs);
+
+/* ---- bootstrapping primitives (Engine.bootstrap, xor_service.py:120-129) ----------------- */
+/* ModRaise: limb 0 of ct (mod q_0, centred) lifted to every limb of `level`; the result encrypts
+ * t = m + q_0 I (scale bookkeeping is the caller's). */
+int aesfhe_mod_raise(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t level, aesfhe_ct **out);
+/* ct * X^{N/2} (sign >= 0) or ct * -X^{N/2}: every slot times i / -i, exact, no level used. */
+int aesfhe_mul_i(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t sign, aesfhe_ct **out);
+/* sum_i cts[i] * pts[i] with one rescale (aligned to the lowest ciphertext level l; plaintexts
+ * encoded at mul_scale(l) with >= l+1 limbs): the diagonal sums of homomorphic linear maps. */
+int aesfhe_dot_pt(aesfhe_engine *eng, const aesfhe_ct *const *cts, const aesfhe_pt *const *pts,
+                  int32_t n, aesfhe_ct **out);
 
 /* ---- raw kernels (known-answer tests and roofline measurement) ------------------------- */
 /* In-place forward (inverse=0) / inverse NTT of nlimb host limbs; limb i uses prime pids[i]

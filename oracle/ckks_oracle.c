@@ -751,8 +751,14 @@ int aesfhe_key_public(aesfhe_engine *e, const aesfhe_key *sk, aesfhe_key **out) 
 }
 
 /* switching key from s' (NTT, all np primes) to s: [dnum][2][np][N] (b, a) */
+static aesfhe_key *make_ksk_salt(aesfhe_engine *e, const aesfhe_key *sk, const u64 *sprime, int kind,
+                                 u64 g, u64 salt);
 static aesfhe_key *make_ksk(aesfhe_engine *e, const aesfhe_key *sk, const u64 *sprime, int kind,
                             u64 g) {
+    return make_ksk_salt(e, sk, sprime, kind, g, 0);
+}
+static aesfhe_key *make_ksk_salt(aesfhe_engine *e, const aesfhe_key *sk, const u64 *sprime, int kind,
+                                 u64 g, u64 salt) {
     const int N = e->N, np = e->np, nq = e->L + 1;
     aesfhe_key *k = calloc(1, sizeof *k);
     k->kind = kind;
@@ -760,6 +766,7 @@ static aesfhe_key *make_ksk(aesfhe_engine *e, const aesfhe_key *sk, const u64 *s
     k->keyseed = sk->keyseed;
     k->data = malloc(sizeof(u64) * (size_t)e->dnum * 2 * np * N);
     u64 base = derive(derive(sk->keyseed, 4 + (u64)kind), g);
+    if (salt) base = derive(base, salt);
     /* P mod q_i */
     u64 Pmod[MAXP];
     for (int p = 0; p < nq; p++) {
@@ -806,6 +813,41 @@ int aesfhe_key_relin(aesfhe_engine *e, const aesfhe_key *sk, aesfhe_key **out) {
         }
     *out = make_ksk(e, sk, s2, 2, 0);
     free(s2);
+    return 0;
+}
+
+/* sparse ternary secret (include/aesfhe.h aesfhe_key_secret_sparse) */
+int aesfhe_key_secret_sparse(aesfhe_engine *e, uint64_t seed, int32_t hw, aesfhe_key **out) {
+    const int N = e->N;
+    if (hw < 1 || hw > N) return fail(AESFHE_EARG, "sparse secret weight must be in [1, N]");
+    aesfhe_key *k = calloc(1, sizeof *k);
+    k->kind = 0;
+    k->keyseed = derive(e->seed, seed);
+    k->data = malloc(sizeof(u64) * (size_t)e->np * N);
+    i64 *s = calloc(N, sizeof(i64));
+    int *idx = malloc(sizeof(int) * N);
+    for (int i = 0; i < N; i++) idx[i] = i;
+    const u64 key = derive(k->keyseed, 9);
+    for (int i = 0; i < hw; i++) {
+        const int j = i + (int)(rnd(key, (u64)i) % (u64)(N - i));
+        const int t = idx[i];
+        idx[i] = idx[j];
+        idx[j] = t;
+        s[idx[i]] = (rnd(key, (u64)N + i) & 1) ? -1 : 1;
+    }
+#pragma omp parallel for schedule(static)
+    for (int p = 0; p < e->np; p++) coeffs_to_ntt(e, s, k->data + (size_t)p * N, p);
+    free(s);
+    free(idx);
+    *out = k;
+    return 0;
+}
+
+/* switching key sk_from -> sk_to: galois kind with element 1 */
+int aesfhe_key_switch(aesfhe_engine *e, const aesfhe_key *sk_from, const aesfhe_key *sk_to, aesfhe_key **out) {
+    if (!sk_from || !sk_to || sk_from->kind != 0 || sk_to->kind != 0)
+        return fail(AESFHE_EARG, "switching key needs two secret keys");
+    *out = make_ksk_salt(e, sk_to, sk_from->data, 3, 1, sk_from->keyseed | 1);
     return 0;
 }
 
@@ -1835,6 +1877,87 @@ int aesfhe_poly2_int(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, c
         aesfhe_ct_free(acc);
     }
     for (int a = 0; a < na; a++) aesfhe_ct_free(al[a]);
+    return 0;
+}
+
+/* ModRaise (include/aesfhe.h aesfhe_mod_raise) */
+int aesfhe_mod_raise(aesfhe_engine *e, const aesfhe_ct *c, int32_t level, aesfhe_ct **out) {
+    if (level < 0 || level > e->L) return fail(AESFHE_EARG, "bad mod-raise level");
+    const int N = e->N;
+    aesfhe_ct *r = ct_new(e, c->B, c->npoly, level);
+    if (c->is_zero) {
+        r->is_zero = 1;
+        *out = r;
+        return 0;
+    }
+    const u64 q0 = e->q[0];
+    for (int b = 0; b < c->B; b++)
+        for (int pp = 0; pp < c->npoly; pp++) {
+            i64 *x = malloc(sizeof(i64) * N);
+            u64 *t = malloc(sizeof(u64) * N);
+            memcpy(t, limb(e, c, b, pp, 0), sizeof(u64) * N);
+            ntt_inv(e, t, 0);
+            for (int k = 0; k < N; k++) x[k] = t[k] > (q0 >> 1) ? (i64)t[k] - (i64)q0 : (i64)t[k];
+#pragma omp parallel for schedule(static)
+            for (int i = 0; i <= level; i++) coeffs_to_ntt(e, x, limb(e, r, b, pp, i), i);
+            free(x);
+            free(t);
+        }
+    *out = r;
+    return 0;
+}
+
+/* multiplication by +-X^{N/2} (every slot times +-i), exact */
+int aesfhe_mul_i(aesfhe_engine *e, const aesfhe_ct *c, int32_t sign, aesfhe_ct **out) {
+    aesfhe_ct *r;
+    aesfhe_ct_copy(e, c, &r);
+    if (!c->is_zero) mul_int_const_inplace(e, r, 0, sign >= 0 ? 1 : -1);
+    *out = r;
+    return 0;
+}
+
+/* sum_i ct_i * pt_i, one rescale (include/aesfhe.h aesfhe_dot_pt) */
+int aesfhe_dot_pt(aesfhe_engine *e, const aesfhe_ct *const *cts, const aesfhe_pt *const *pts, int32_t n,
+                  aesfhe_ct **out) {
+    if (n < 1 || n > 256) return fail(AESFHE_EARG, "dot_pt needs 1..256 terms");
+    int l = cts[0]->level, B = 1, np = cts[0]->npoly;
+    for (int i = 0; i < n; i++) {
+        if (cts[i]->level < l) l = cts[i]->level;
+        if (cts[i]->B > B) B = cts[i]->B;
+        if (cts[i]->npoly != np) return fail(AESFHE_EDEGREE, "dot_pt inputs should have the same number of polynomials");
+    }
+    for (int i = 0; i < n; i++) {
+        if (cts[i]->B != B && cts[i]->B != 1) return fail(AESFHE_EARG, "batch mismatch");
+        if (pts[i]->level < l) return fail(AESFHE_EARG, "plaintext level %d below ciphertext level %d", pts[i]->level, l);
+    }
+    if (l < 1) return fail(AESFHE_ELEVEL, "no level left for a plaintext dot product");
+    aesfhe_ct *acc = ct_new(e, B, np, l);
+    int any = 0;
+    for (int i = 0; i < n; i++) {
+        if (cts[i]->is_zero) continue;
+        any = 1;
+        aesfhe_ct *t = level_down_raw(e, cts[i], l);
+        for (int b = 0; b < B; b++)
+            for (int pp = 0; pp < np; pp++)
+#pragma omp parallel for schedule(static)
+                for (int x = 0; x <= l; x++) {
+                    const u64 q = e->q[x];
+                    const u64 *src = limb(e, t, t->B == 1 ? 0 : b, pp, x);
+                    const u64 *pv = pts[i]->data + (size_t)x * e->N;
+                    u64 *dst = limb(e, acc, b, pp, x);
+                    for (int j = 0; j < e->N; j++) dst[j] = add_mod(dst[j], mul_mod(src[j], pv[j], &e->mont[x]), q);
+                }
+        aesfhe_ct_free(t);
+    }
+    if (!any) {
+        aesfhe_ct_free(acc);
+        aesfhe_ct *r = ct_new(e, B, np, l - 1);
+        r->is_zero = 1;
+        *out = r;
+        return 0;
+    }
+    *out = rescale_raw(e, acc);
+    aesfhe_ct_free(acc);
     return 0;
 }
 
