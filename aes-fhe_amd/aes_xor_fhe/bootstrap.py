@@ -1,0 +1,255 @@
+"""CKKS bootstrapping over the engine primitives (Engine.bootstrap; the reference calls desilofhe's
+at xor_service.py:120-129 and mixcolumns_service.py:72-75).
+
+Pipeline for a ciphertext c at level 0 encrypting slots z (message m at the canonical scale D_0):
+
+1. sparse-secret encapsulation: switch c to an ephemeral sparse ternary secret s' (hw nonzeros)
+   at level 0, ModRaise to level L (now encrypts t = m + q_0 I with |I| <= K w.h.p.), switch back
+   to the main secret s at level L;
+2. CoeffToSlot: slots of the raised ciphertext are V u_t / D_L with u_k = t_k + i t_{k+n} and
+   V_jk = xi^(5^j k) (verified against the codec); V = B_log(n) ... B_1 P (butterfly stages, P the
+   bit reversal).  CtS applies (D_L / (2 q_0 Bnd)) B_1^-1 ... B_log(n)^-1 (merged into `groups`
+   linear maps evaluated baby-step giant-step with aesfhe_dot_pt), giving the bit-reversed
+   u_t / (2 q_0 Bnd);  x_re = w + conj(w), x_im = -i (w - conj(w)) hold t / (q_0 Bnd) in [-1, 1];
+3. EvalMod: sin(2 pi Bnd x) via a Chebyshev approximation of cos(2 pi (Bnd x - 1/4) / 2^r) and r
+   double-angle steps; sin(2 pi t/q_0) / (2 pi) = m / q_0 for |m| << q_0;
+4. SlotToCoeff: (q_0 / (2 pi D_0)) B_log(n) ... B_1 applied to y_re + i y_im (the bit reversal
+   cancels) returns the slots z at level L - depth.
+
+Depth = 1 + 2 * groups + ceil(log2(deg + 1)) + 1 + r (16 with the defaults at any N).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List
+
+import numpy as np
+
+from .fhe import Ciphertext, Engine
+
+
+# ---- the encoding map in butterfly form --------------------------------------------------------
+def _stage(n: int, N: int, length: int, inverse: bool) -> Dict[int, np.ndarray]:
+    """Diagonal form {offset d: D_d} of one butterfly stage (block length `length`) of V or of its
+    inverse: (S x)[p] = sum_d D_d[p] x[(p + d) mod n]."""
+    h = length // 2
+    M = 2 * N
+    lenq = length << 2
+    gap = M // lenq
+    j = np.arange(h)
+    w = np.exp(2j * np.pi * ((np.array([pow(5, int(x), lenq) for x in j]) * gap) % M) / M)
+    p = np.arange(n)
+    top = (p % length) < h
+    jj = np.where(top, p % length, p % length - h)
+    wp = w[jj]
+    D0 = np.zeros(n, complex)
+    Dp = np.zeros(n, complex)
+    Dm = np.zeros(n, complex)
+    if not inverse:  # top: x[p] + w x[p+h]; bottom: x[p-h] - w x[p]
+        D0[top], Dp[top] = 1.0, wp[top]
+        Dm[~top], D0[~top] = 1.0, -wp[~top]
+    else:  # top: (x[p] + x[p+h]) / 2; bottom: conj(w) (x[p-h] - x[p]) / 2
+        D0[top], Dp[top] = 0.5, 0.5
+        Dm[~top], D0[~top] = np.conj(wp[~top]) / 2, -np.conj(wp[~top]) / 2
+    out = {0: D0}
+    for d, D in ((h % n, Dp), ((-h) % n, Dm)):  # h == -h (mod n) in the last stage: sum them
+        out[d] = out.get(d, 0) + D
+    return out
+
+
+def _compose(A: Dict[int, np.ndarray], B: Dict[int, np.ndarray], n: int) -> Dict[int, np.ndarray]:
+    """Diagonal form of A @ B: C_{a+b}[p] += A_a[p] B_b[p + a]."""
+    C: Dict[int, np.ndarray] = {}
+    for a, Da in A.items():
+        for b, Db in B.items():
+            d = (a + b) % n
+            v = Da * np.roll(Db, -a)
+            C[d] = C.get(d, 0) + v
+    return {d: v for d, v in C.items() if np.any(np.abs(v) > 1e-14)}
+
+
+def apply_diag(M: Dict[int, np.ndarray], x: np.ndarray) -> np.ndarray:
+    return sum(D * np.roll(x, -d) for d, D in M.items())
+
+
+def transform_groups(n: int, N: int, groups: int, inverse: bool) -> List[Dict[int, np.ndarray]]:
+    """The log2(n) stages merged into `groups` maps, in application order.  Forward (StC):
+    B_1 first ... B_log(n) last; inverse (CtS): B_log(n)^-1 first ... B_1^-1 last."""
+    L = int(math.log2(n))
+    lengths = [2 << s for s in range(L)]  # B_1 .. B_L block lengths 2 .. n
+    order = list(reversed(lengths)) if inverse else lengths
+    sizes = [len(a) for a in np.array_split(np.arange(L), groups)]
+    out, i = [], 0
+    for sz in sizes:
+        M = None
+        for length in order[i:i + sz]:  # later stages act after earlier ones: M = S @ M
+            S = _stage(n, N, length, inverse)
+            M = S if M is None else _compose(S, M, n)
+        out.append(M)
+        i += sz
+    return out
+
+
+def _bsgs_plan(offsets: List[int], n: int):
+    """Offsets are k*u (k in a symmetric range); baby steps k1*u (0 <= k1 < g), giants g*k2*u."""
+    nz = sorted(offsets)
+    u = math.gcd(*[d for d in nz if d]) if any(nz) else 1
+    u = math.gcd(u, n)
+    ks = sorted({((d // u + n // (2 * u)) % (n // u)) - n // (2 * u) for d in nz})  # signed k
+    span = max(ks) - min(ks) + 1
+    g = 1 << max(0, math.ceil(math.log2(math.sqrt(span))))
+    return u, ks, g
+
+
+# ---- the bootstrapper --------------------------------------------------------------------------
+class Bootstrapper:
+    def __init__(self, engine: Engine, sk, rlk, cjk=None, *, hw: int = 32, K: float = 12.0,
+                 r: int = 3, deg: int = 31, groups: int = 3, seed: int = 7):
+        e = self.e = engine
+        self.rlk = rlk
+        self.cjk = cjk if cjk is not None else e.create_conjugation_key(sk)
+        self.N = 1 << e.log_coeff_count
+        self.n = self.N // 2
+        self.L = e.max_level
+        self.r, self.deg, self.B = r, deg, K + 1.0
+        # sparse-secret encapsulation keys
+        s_sparse = e.create_sparse_secret_key(hw, seed)
+        self.to_sparse = e.create_switching_key(sk, s_sparse)
+        self.from_sparse = e.create_switching_key(s_sparse, sk)
+        q0 = float(e.primes[0])
+        D = e.scales
+        n, N = self.n, self.N
+        # CtS: (D_L / (2 q0 Bnd)) * prod of inverse stages; StC: (q0 / (2 pi D_0)) * forward stages
+        cts = transform_groups(n, N, groups, inverse=True)
+        stc = transform_groups(n, N, groups, inverse=False)
+        # c_in = D_L / (2 q0 Bnd) ~ 2^-15 folded into the diagonals would leave their plaintext
+        # integers ~25 bits.  It is applied as its own constant multiply instead (one level): the
+        # engine multiplies by exactly A / s (A = llround(c_in s)), and the bound is re-derived
+        # from that value so that 2 pi Bnd x = 2 pi t / q0 holds exactly.
+        s = e._lib.engine_mul_scale(e._h, self.L)
+        self.c_in = round(D[self.L] / (2.0 * q0 * self.B) * s) / s
+        self.B = D[self.L] / (2.0 * q0 * self.c_in)
+        c_out = q0 / (2.0 * math.pi * D[0])
+        stc_bits = [dict(M) for M in stc]
+        stc[-1] = {d: v * c_out for d, v in stc[-1].items()}
+        # bit mode: slots b + i b' -> coefficients (q0 / 4) (b, b') at level 0
+        c_bits = q0 / (4.0 * D[0])
+        stc_bits[-1] = {d: v * c_bits for d, v in stc_bits[-1].items()}
+        self.cts, self.stc = [self._prepare(M) for M in cts], [self._prepare(M) for M in stc]
+        self.stc_bits = [self._prepare(M) for M in stc_bits]
+        # rotation keys for every baby / giant step
+        shifts = set()
+        for plan in self.cts + self.stc:  # stc_bits has the offsets of stc
+            u, g = plan["u"], plan["g"]
+            shifts.update((k1 * u) % n for k1 in range(1, g))
+            shifts.update((g * k2 * u) % n for k2 in plan["giants"] if (g * k2 * u) % n)
+        self.rot = {d: e.create_fixed_rotation_key(sk, -d) for d in sorted(shifts)}
+        # EvalMod: Chebyshev coefficients of cos(2 pi (Bnd x - 1/4) / 2^r) on [-1, 1]
+        kk = np.arange(deg + 1)
+        xs = np.cos(np.pi * (kk + 0.5) / (deg + 1))
+        f = np.cos(2 * np.pi * (self.B * xs - 0.25) / (1 << r))
+        self.cheb = np.polynomial.chebyshev.chebfit(xs, f, deg)
+        self.depth = 1 + 2 * groups + math.ceil(math.log2(deg + 1)) + 1 + r
+        self.bits_level = self.L - (1 + groups + math.ceil(math.log2(deg + 1)) + 1 + r)
+
+    def _prepare(self, M: Dict[int, np.ndarray]):
+        u, ks, g = _bsgs_plan(list(M), self.n)
+        giants = sorted({(k - (k % g)) // g for k in ks})
+        terms = {}
+        for k in ks:
+            d = (k * u) % self.n
+            k2 = (k - (k % g)) // g
+            k1 = k - g * k2
+            # sum_k2 rot( sum_k1 rot(D_k, -g k2 u) * rot(x, k1 u), g k2 u )
+            terms.setdefault(k2, []).append((k1, self.e.encode(np.roll(M[d], g * k2 * u))))
+        return {"u": u, "g": g, "giants": giants, "terms": terms}
+
+    def _rot(self, ct: Ciphertext, d: int) -> Ciphertext:
+        """x -> x[p + d] (d slots to the left)."""
+        d %= self.n
+        return ct if d == 0 else self.e.rotate(ct, self.rot[d])
+
+    def linear(self, ct: Ciphertext, plan) -> Ciphertext:
+        e, u, g = self.e, plan["u"], plan["g"]
+        baby = {0: ct}
+        for k2, tl in plan["terms"].items():
+            for k1, _ in tl:
+                if k1 not in baby:
+                    baby[k1] = self._rot(ct, k1 * u)
+        out = None
+        for k2, tl in sorted(plan["terms"].items()):
+            part = e.dot_plain([baby[k1] for k1, _ in tl], [pt for _, pt in tl])
+            part = self._rot(part, g * k2 * u)
+            out = part if out is None else e.add(out, part)
+        return out
+
+    def chebyshev(self, x: Ciphertext) -> Ciphertext:
+        """sum_k c_k T_k(x): T_{a+b} = 2 T_a T_b - T_{|a-b|}, a the largest power of two < k."""
+        e = self.e
+        T = {1: x}
+        for k in range(2, self.deg + 1):
+            a = 1 << (k.bit_length() - 1)
+            if a == k:
+                a = k // 2
+            b = k - a
+            prod = e.multiply(T[a], T[b], self.rlk)
+            t2 = e.add(prod, prod)
+            T[k] = e.add(t2, -1.0) if a == b else e.subtract(t2, T[a - b])
+        ks = [k for k in range(1, self.deg + 1) if abs(self.cheb[k]) > 1e-13]
+        out = e.lincomb([T[k] for k in ks], [complex(self.cheb[k]) for k in ks])
+        return e.add(out, complex(self.cheb[0]))
+
+    def evalmod(self, x: Ciphertext) -> Ciphertext:
+        e = self.e
+        c = self.chebyshev(x)
+        for _ in range(self.r):
+            sq = e.multiply(c, c, self.rlk)
+            c = e.add(e.add(sq, sq), -1.0)
+        return c  # sin(2 pi Bnd x)
+
+    def _raise_to_slots(self, c: Ciphertext):
+        """Level-0 ciphertext (coefficients t mod q0) -> (x_re, x_im) with slots t / (q0 Bnd) of
+        the bit-reversed real / imaginary coefficient halves, at level L - 1 - groups."""
+        e = self.e
+        c = e.switch_key(c, self.to_sparse)
+        c = e.mod_raise(c, self.L)
+        c = e.switch_key(c, self.from_sparse)
+        c = e.multiply(c, self.c_in)
+        for plan in self.cts:
+            c = self.linear(c, plan)
+        cj = e.conjugate(c, self.cjk)
+        return e.add(c, cj), e.multiply_i(e.subtract(c, cj), -1)
+
+    def bootstrap(self, ct: Ciphertext) -> Ciphertext:
+        """General complex slots (CtS -> EvalMod -> StC): output at level L - depth."""
+        e = self.e
+        c = ct if ct.level == 0 else e.level_down(ct, 0)
+        x_re, x_im = self._raise_to_slots(c)
+        y = e.add(self.evalmod(x_re), e.multiply_i(self.evalmod(x_im), 1))
+        for plan in self.stc:
+            y = self.linear(y, plan)
+        return y
+
+    def bootstrap_bits(self, a: Ciphertext, b: Ciphertext | None = None):
+        """Refresh one or two ciphertexts whose real slots hold bits +-1 (SlotToCoeff first).
+
+        StC at the bottom levels puts the bits into the coefficients as +-q0/4 (a in the first
+        half, b in the second); after ModRaise t/q0 = I +- 1/4 + eps, so EvalMod's
+        sin(2 pi t / q0) = +-cos(2 pi eps) returns the bits in the slots directly -- the
+        error of the input bits enters squared, and the signal is O(1) (no q0 / D_0 gain at the
+        end).  Inputs need level >= groups; outputs are at level L - 1 - 2 groups... - r
+        (``self.bits_level``).  Returns (a', b') (b' None when b is None)."""
+        e = self.e
+        lv = len(self.stc_bits)
+        x = a if b is None else e.add(e.level_down(a, min(a.level, b.level)),
+                                       e.multiply_i(e.level_down(b, min(a.level, b.level)), 1))
+        if x.level < lv:
+            raise ValueError(f"bootstrap_bits needs level >= {lv}, got {x.level}")
+        if x.level > lv:
+            x = e.level_down(x, lv)
+        for plan in self.stc_bits:
+            x = self.linear(x, plan)
+        x_re, x_im = self._raise_to_slots(x)
+        ya = self.evalmod(x_re)
+        yb = self.evalmod(x_im) if b is not None else None
+        return ya, yb

@@ -107,11 +107,24 @@ class RotationKey:
 
 
 class BootstrapKey:
-    """Placeholder returned by create_(small_)bootstrap_key (engine_context.py:72-73 creates
-    them unconditionally).  Bootstrapping itself is SURVEY.md section 8f item 1 (next)."""
+    """Returned by create_(small_)bootstrap_key (engine_context.py:72-73 creates both
+    unconditionally).  The key material (sparse-secret switching keys, the CoeffToSlot /
+    SlotToCoeff rotation keys) is generated on first use, by bootstrap.Bootstrapper, since most
+    contexts never bootstrap.  `small` selects more, smaller linear-transform groups (fewer
+    diagonals, one more level per transform)."""
 
-    def __init__(self, small: bool):
+    def __init__(self, engine: "Engine", sk: "SecretKey", small: bool):
+        self.engine = engine
+        self._sk = sk
         self.small = small
+        self._bs = None
+
+    def bootstrapper(self, relinearization_key, conjugation_key=None):
+        if self._bs is None:
+            from .bootstrap import Bootstrapper
+            self._bs = Bootstrapper(self.engine, self._sk, relinearization_key, conjugation_key,
+                                    groups=4 if self.small else 3)
+        return self._bs
 
 
 # ------------------------------------------------------------------------------------------
@@ -166,7 +179,7 @@ class Engine:
 
     ``mode`` is accepted for compatibility; execution is always the HIP engine on
     ``device_id`` (the product has no CPU path).  Extra keyword overrides (``log_n``,
-    ``special_primes``, ``scale_bits``, ``seed``) select explicit parameters; ``_lib`` injects
+    ``special_primes``, ``scale_bits``, ``base_bits``, ``special_bits``, ``seed``) select explicit parameters; ``_lib`` injects
     another implementation of the ABI (tests use it for the CPU oracle).
     """
 
@@ -175,6 +188,7 @@ class Engine:
                  max_level: int | None = None, log_coeff_count: int | None = None,
                  special_prime_count: int | None = None, log_n: int | None = None,
                  special_primes: int | None = None, scale_bits: int | None = None,
+                 base_bits: int | None = None, special_bits: int | None = None,
                  seed: int | None = None, _lib: Lib | None = None):
         ints = [a for a in args if isinstance(a, (int, np.integer)) and not isinstance(a, bool)]
         strs = [a for a in args if isinstance(a, str)]
@@ -192,12 +206,12 @@ class Engine:
                 1, (budget - DEFAULT_PARAMS["base_bits"] - k * DEFAULT_PARAMS["special_bits"])
                 // DEFAULT_PARAMS["scale_bits"])
             p = _params_for(log_n=log_n or ln, max_level=lvl, special_primes=special_primes or k,
-                            scale_bits=scale_bits, seed=seed, threads=thread_count,
-                            device=device_id)
+                            scale_bits=scale_bits, base_bits=base_bits, special_bits=special_bits,
+                            seed=seed, threads=thread_count, device=device_id)
         else:                                    # signatures 1 and 2
             p = _params_for(log_n=log_n, max_level=max_level, special_primes=special_primes,
-                            scale_bits=scale_bits, seed=seed, threads=thread_count,
-                            device=device_id)
+                            scale_bits=scale_bits, base_bits=base_bits, special_bits=special_bits,
+                            seed=seed, threads=thread_count, device=device_id)
         self.mode = mode
         self.use_bootstrap = use_bootstrap
         self.use_multiparty = use_multiparty
@@ -319,10 +333,10 @@ class Engine:
         return self._call_ct(self._lib.galois, ct._h, swk._h)
 
     def create_small_bootstrap_key(self, sk: SecretKey) -> BootstrapKey:
-        return BootstrapKey(small=True)
+        return BootstrapKey(self, sk, small=True)
 
     def create_bootstrap_key(self, sk: SecretKey) -> BootstrapKey:
-        return BootstrapKey(small=False)
+        return BootstrapKey(self, sk, small=False)
 
     # -- codec --------------------------------------------------------------------------------
     def encode(self, vec, level: int | None = None, scale: float | None = None) -> Plaintext:
@@ -446,9 +460,14 @@ class Engine:
             out = self._call_ct(self._lib.ct_copy, ct._h)
         return out
 
-    def bootstrap(self, ct, *keys):
-        raise NotImplementedError(
-            "CKKS bootstrapping is not implemented yet (SURVEY.md section 8f item 1)")
+    def bootstrap(self, ct: Ciphertext, relinearization_key: RelinearizationKey,
+                  conjugation_key: ConjugationKey, bootstrap_key: BootstrapKey) -> Ciphertext:
+        """Refresh `ct` (any level) to level max_level - depth (xor_service.py:120-129 calls
+        this with the context's rlk, conjugation and bootstrap keys).  bootstrap.Bootstrapper
+        states the algorithm; the slots come back with the precision DESIGN.md section 7 lists."""
+        if not isinstance(bootstrap_key, BootstrapKey):
+            raise TypeError("bootstrap needs the key from create_bootstrap_key")
+        return bootstrap_key.bootstrapper(relinearization_key, conjugation_key).bootstrap(ct)
 
     # -- fused building blocks used by the optimised AES round ---------------------------------
     def mod_raise(self, ct: Ciphertext, level: int | None = None) -> Ciphertext:

@@ -142,7 +142,7 @@ struct aesfhe_engine {
     // combined ModDown + rescale (drop r = 1, 2 top Q primes with P), see build_tables
     double *mdr_invf = nullptr, *mdr_dinvf = nullptr, *pmodf = nullptr;
     TwD* mdr_hatf = nullptr;  // {w, w/q}
-    double *mdr_einv = nullptr, *mdr_dmodf = nullptr;
+    double *mdr_einv = nullptr, *mdr_dmodf = nullptr, *md_einv = nullptr;
     u64* mdr_dinv = nullptr;
     double *mu_hatinvf, *md_phatinvf, *md_pinvf, *rs_invf;
     TwD *mu_hatf, *md_phatf;  // base-conversion constants {w, w/q}
@@ -571,6 +571,9 @@ static void build_tables(aesfhe_engine* e) {
         std::vector<double> hpmodf(Lp1);
         for (int i = 0; i < Lp1; i++) hpmodf[i] = (double)hpmod[i] / (double)Q[i];
         up(hpmodf, &e->pmodf);
+        std::vector<double> heinv0(kMdrMaxE, 0.0);  // 1/p_k: the exact conversion of plain ModDown
+        for (int k = 0; k < K; k++) heinv0[k] = 1.0 / (double)Q[Lp1 + k];
+        up(heinv0, &e->md_einv);
     }
     // combined ModDown + rescale: E = {q_{l-r+1}..q_l, p_0..p_{K-1}} (acc limb order), D = prod E
     //   mdr_invf[(r-1, l)][j]       = (D/e_j)^{-1} mod e_j, as w/e_j
@@ -694,7 +697,7 @@ extern "C" void aesfhe_engine_destroy(aesfhe_engine* e) {
                     e->mu_hatinv, e->mu_hat, e->md_phatinv, e->md_phat, e->md_pinv, e->rs_inv,
                     e->rs_mod, e->pmod, e->mu_hatinvf, e->mu_hatf, e->md_phatinvf, e->md_phatf,
                     e->md_pinvf, e->rs_invf, e->ring_d, e->tw, e->itw, e->mdr_invf, e->mdr_hatf,
-                    e->mdr_dinv, e->mdr_dinvf, e->pmodf, e->mdr_einv, e->mdr_dmodf};
+                    e->mdr_dinv, e->mdr_dinvf, e->pmodf, e->mdr_einv, e->mdr_dmodf, e->md_einv};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto& kv : e->poly2_tabs) hipFree(kv.second);
@@ -1421,7 +1424,9 @@ extern "C" int aesfhe_dot_pt(aesfhe_engine* e, const aesfhe_ct* const* cts, cons
 // key switching of one polynomial per batch element.
 // d: NTT-domain polynomial of batch element b at d + b*dbs (level l, limbs contiguous).
 // Result: out poly 0/1 = addend_{0/1} + KS(d)_{0/1}, written into ct `o` (2 polys, level l - r).
-// r = 0: plain ModDown by P.  r >= 1: combined ModDown + rescale -- P * addend joins the
+// r = 0: plain ModDown by P.  Either way the base conversion is exact (round-to-nearest
+// division: v = rint(sum_j y_j / e_j) multiples of D removed), so the rounding noise is
+// |eps| <= 1/2 per coefficient instead of the fast conversion's 0..K overflow.  r >= 1: combined ModDown + rescale -- P * addend joins the
 // accumulators in the inner product and one base conversion from E = {q_{l-r+1}..q_l, P} divides
 // by D = P q_l ... q_{l-r+1} (oracle/ckks_oracle.c moddown_r states the same procedure).
 static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, const aesfhe_key* k,
@@ -1480,8 +1485,8 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1));
         hipLaunchKernelGGL(k_moddown, dim3(N / 256, g_bconv_groups, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, r, conv.p, 2 * kN, kN, K,
-                           invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : (const double*)nullptr,
-                           r ? e->mdr_dmodf + cell * e->Lp1 : (const double*)nullptr, e->Lp1, e->q, e->qinv, e->logN);
+                           invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv,
+                           r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN);
     }
     HIPC(hipGetLastError());
     Span sc = span_s(conv.p, kN, lk + 1, lk + 1, 0, e->Lp1);

@@ -398,7 +398,7 @@ __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int 
         }
     }
     double v = 0.0;
-    if (r > 0) {
+    {  // exact conversion (every r): v multiples of D, round-to-nearest division
         double u = 0.0;
 #pragma unroll
         for (int j = 0; j < 16; j++)
@@ -408,11 +408,8 @@ __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int 
     const int ig = (l - r + 1 + gridDim.y - 1) / gridDim.y, i0 = blockIdx.y * ig;  // outputs per thread
     for (int i = i0; i < i0 + ig && i <= l - r; i++) {
         const double q = (double)qall[i], qi = qinvall[i];
-        double sum = 0.0;
-        if (r > 0) {
-            const double f = dmodf[i];
-            sum = fmul_rem(-v, tw_w(f, q), f, q);
-        }
+        const double f = dmodf[i];
+        double sum = fmul_rem(-v, tw_w(f, q), f, q);
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             if (j < ne) {

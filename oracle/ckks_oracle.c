@@ -1338,7 +1338,7 @@ static u64 *ks_acc(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k) {
 /* ModDown of the accumulators by D = P * q_l ... q_{l-r+1} (r = 0: plain
  * ModDown by P, r >= 1: combined with r rescales).  Dropped limbs E = {q_{l-r+1}..q_l, p_0..}:
  * y_j = [INTT(acc_j) * (D/e_j)^{-1}]_{e_j}, conv_i = sum_j y_j (D/e_j mod q_i), out_i =
- * (acc_i - conv_i) D^{-1} for i <= l - r.  For r >= 1 the conversion is exact: v = rint(sum_j
+ * (acc_i - conv_i) D^{-1} for i <= l - r.  The conversion is exact (every r): v = rint(sum_j
  * y_j * (1/e_j)) (fp64, in j order) multiples of D are removed from conv (round-to-nearest
  * division, as a plain rescale).  Output limbs: (l-r+1) per component. */
 static void moddown_r(aesfhe_engine *e, const u64 *acc, int l, int r, u64 *out0, u64 *out1) {
@@ -1389,7 +1389,7 @@ static void moddown_r(aesfhe_engine *e, const u64 *acc, int l, int r, u64 *out0,
                 u64 sum = 0;
                 for (int j = 0; j < nE; j++)
                     sum = add_mod(sum, mul_mod_slow(y[(size_t)j * N + x] % qi, hat[j][i], qi), qi);
-                if (r > 0) {  /* exact conversion: remove the v multiples of D (v = rint(sum y_j / e_j)) */
+                {  /* exact conversion: remove the v multiples of D (v = rint(sum y_j / e_j)) */
                     double u = 0.0;
                     for (int j = 0; j < nE; j++) u = u + (double)y[(size_t)j * N + x] * einv[j];
                     const u64 v = (u64)rint(u);

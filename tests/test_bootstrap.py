@@ -1,0 +1,135 @@
+"""CKKS bootstrapping (aes_xor_fhe.bootstrap; Engine.bootstrap, called by the reference at
+xor_service.py:120-129,274-277 and mixcolumns_service.py:72-75).
+
+desilofhe's bootstrap is closed and absent, so parity is unpinned against the reference's engine:
+these tests check the algorithm's own invariants -- the butterfly factorisation of the encoding
+map against the codec's V, the key-switch rounding noise of the exact ModDown, decrypt(boot(ct))
+~ decrypt(ct) within the precision DESIGN.md section 7 states, the quadratic error squash of the
+bit mode -- on the CPU oracle, and residue-identical outputs of the HIP engine (integer work,
+bit-exact) plus the precision at BASELINE's N = 2^16, L = 30 on the GPU."""
+import math
+
+import numpy as np
+import pytest
+
+from aes_xor_fhe.bootstrap import Bootstrapper, apply_diag, transform_groups
+from aes_xor_fhe.fhe import Engine
+
+
+def _brv(n):
+    L = int(math.log2(n))
+    return np.array([int(format(i, f"0{L}b")[::-1], 2) for i in range(n)])
+
+
+@pytest.mark.parametrize("log_n,groups", [(6, 1), (8, 3), (10, 3), (10, 4)])
+def test_transform_factorisation(log_n, groups):
+    N = 1 << log_n
+    n, M = N // 2, 2 * N
+    xi = np.exp(2j * np.pi / M)
+    rot = np.array([pow(5, j, M) for j in range(n)])
+    V = xi ** (np.outer(rot, np.arange(n)) % M)  # z = V u / scale (the codec, fhe.decode)
+    u = np.random.default_rng(0).standard_normal(n) + 1j
+    x = u[_brv(n)]
+    for Mx in transform_groups(n, N, groups, False):
+        x = apply_diag(Mx, x)
+    np.testing.assert_allclose(x, V @ u, atol=1e-9)
+    y = V @ u
+    for Mx in transform_groups(n, N, groups, True):
+        y = apply_diag(Mx, y)
+    np.testing.assert_allclose(y, u[_brv(n)], atol=1e-9)
+
+
+def _engine(lib, log_n=10, scale_bits=44, max_level=24):
+    e = Engine(log_n=log_n, max_level=max_level, special_primes=4, scale_bits=scale_bits, seed=3,
+               _lib=lib)
+    sk = e.create_secret_key(1)
+    return e, sk, e.create_public_key(sk), e.create_relinearization_key(sk)
+
+
+def test_keyswitch_rounding_noise(oracle_lib):
+    """Exact ModDown: the added noise is eps * s_to with |eps| <= 1/2 (std sqrt(h/12))."""
+    e, sk, pk, _ = _engine(oracle_lib)
+    n = e.slot_count
+    x = np.random.default_rng(2).uniform(-1, 1, n) * 1e-2
+    for s_to, h in ((e.create_secret_key(9), 2 * e.slot_count * 2 / 3),
+                    (e.create_sparse_secret_key(32, 4), 32)):
+        swk = e.create_switching_key(sk, s_to)
+        c = e.encrypt(x, pk, level=10)
+        e0 = e.decrypt(c, sk) - x
+        add = (e.decrypt(e.switch_key(c, swk), s_to) - x) - e0
+        co = e._encode_coeffs(add, e.scales[10]).astype(float)
+        assert co.std() < 1.5 * math.sqrt(h / 12) + 1, (h, co.std())
+
+
+def test_bootstrap_general_oracle(oracle_lib):
+    e, sk, pk, rlk = _engine(oracle_lib)
+    bk = e.create_bootstrap_key(sk)
+    cjk = e.create_conjugation_key(sk)
+    n = e.slot_count
+    rng = np.random.default_rng(1)
+    z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
+    ct = e.encrypt(z, pk, level=2)
+    out = e.bootstrap(ct, rlk, cjk, bk)
+    bs = bk.bootstrapper(rlk, cjk)
+    assert out.level == e.max_level - bs.depth
+    assert np.abs(e.decrypt(out, sk) - z).max() < 1e-3
+
+
+def test_bootstrap_bits_oracle(oracle_lib):
+    e, sk, pk, rlk = _engine(oracle_lib)
+    bs = Bootstrapper(e, sk, rlk)
+    n = e.slot_count
+    rng = np.random.default_rng(4)
+    a, b = rng.choice([-1.0, 1.0], n), rng.choice([-1.0, 1.0], n)
+    noise = 0.03 * rng.standard_normal((2, n))
+    ya, yb = bs.bootstrap_bits(e.encrypt(a + noise[0], pk, level=6),
+                               e.encrypt(b + noise[1], pk, level=4))
+    assert ya.level == yb.level == bs.bits_level == e.max_level - 13
+    # the input error enters squared: 1 - cos(2 pi e / 4) <= 1.24 e^2
+    for y, v, nz in ((ya, a, noise[0]), (yb, b, noise[1])):
+        err = np.abs(e.decrypt(y, sk) - v)
+        assert np.all(err <= 1.24 * nz ** 2 + 1e-5)
+    # one ciphertext alone, constant slots (all coefficients but one zero)
+    y1, none = bs.bootstrap_bits(e.encrypt(np.ones(n), pk, level=3))
+    assert none is None and np.abs(e.decrypt(y1, sk) - 1).max() < 1e-5
+    with pytest.raises(ValueError):
+        bs.bootstrap_bits(e.encrypt(a, pk, level=2))
+
+
+@pytest.mark.gpu
+def test_bootstrap_bits_bit_exact_vs_oracle(product_lib, oracle_lib, gpu_available):
+    outs = []
+    for lib in (product_lib, oracle_lib):
+        e, sk, pk, rlk = _engine(lib)
+        bs = Bootstrapper(e, sk, rlk)
+        rng = np.random.default_rng(4)
+        n = e.slot_count
+        a, b = rng.choice([-1.0, 1.0], n), rng.choice([-1.0, 1.0], n)
+        ya, yb = bs.bootstrap_bits(e.encrypt(a, pk, level=3), e.encrypt(b, pk, level=3))
+        g = e.bootstrap(e.encrypt(a + 0.5j * b, pk, level=0), rlk, bs.cjk,
+                        _key_for(e, sk, bs))
+        outs.append([e.export_residues(c) for c in (ya, yb, g)])
+    for h, o in zip(*outs):
+        assert np.array_equal(h, o)
+
+
+def _key_for(e, sk, bs):
+    k = e.create_bootstrap_key(sk)
+    k._bs = bs
+    return k
+
+
+@pytest.mark.gpu
+def test_bootstrap_bits_full_params(product_lib, gpu_available):
+    """BASELINE's N = 2^16, L = 30 (44-bit scale, log QP = 1770 <= 1772)."""
+    e = Engine(log_n=16, max_level=30, special_primes=8, scale_bits=44, seed=3, _lib=product_lib)
+    sk = e.create_secret_key(1)
+    pk = e.create_public_key(sk)
+    bs = Bootstrapper(e, sk, e.create_relinearization_key(sk))
+    n = e.slot_count
+    rng = np.random.default_rng(5)
+    a, b = rng.choice([-1.0, 1.0], n), rng.choice([-1.0, 1.0], n)
+    ya, yb = bs.bootstrap_bits(e.encrypt(a, pk, level=3), e.encrypt(b, pk, level=3))
+    assert ya.level == 17
+    assert np.abs(e.decrypt(ya, sk) - a).max() < 1e-3
+    assert np.abs(e.decrypt(yb, sk) - b).max() < 1e-3

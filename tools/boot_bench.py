@@ -1,0 +1,67 @@
+"""Time bit-mode and general bootstrapping on the HIP engine at N = 2^16, L = 30 (44-bit scale).
+
+python tools/boot_bench.py [--log-n 16] [--reps 3]  -> one JSON line per mode."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "aes-fhe_amd"))
+
+import numpy as np  # noqa: E402
+
+from aes_xor_fhe.bootstrap import Bootstrapper  # noqa: E402
+from aes_xor_fhe.fhe import Engine  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--log-n", type=int, default=16)
+    ap.add_argument("--max-level", type=int, default=30)
+    ap.add_argument("--scale-bits", type=int, default=44)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--general", action="store_true")
+    a = ap.parse_args()
+    e = Engine(log_n=a.log_n, max_level=a.max_level, special_primes=8, scale_bits=a.scale_bits, seed=3)
+    sk = e.create_secret_key(1)
+    pk = e.create_public_key(sk)
+    t = time.time()
+    bs = Bootstrapper(e, sk, e.create_relinearization_key(sk))
+    e.synchronize()
+    setup = time.time() - t
+    n = e.slot_count
+    rng = np.random.default_rng(5)
+    bits = [rng.choice([-1.0, 1.0], n) for _ in range(2)]
+    cts = [e.encrypt(b, pk, level=3) for b in bits]
+    bs.bootstrap_bits(*cts)
+    e.synchronize()
+    ts = []
+    for _ in range(a.reps):
+        t = time.time()
+        ya, yb = bs.bootstrap_bits(*cts)
+        e.synchronize()
+        ts.append(time.time() - t)
+    err = max(np.abs(e.decrypt(y, sk) - b).max() for y, b in zip((ya, yb), bits))
+    print(json.dumps({"mode": "bits", "log_n": a.log_n, "max_level": a.max_level,
+                      "scale_bits": a.scale_bits, "setup_s": round(setup, 2),
+                      "ms_per_bootstrap": round(1e3 * min(ts), 1), "cts_per_bootstrap": 2,
+                      "out_level": ya.level, "max_err": float(err),
+                      "rotation_keys": len(bs.rot)}), flush=True)
+    if a.general:
+        z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
+        c = e.encrypt(z, pk, level=0)
+        bs.bootstrap(c)
+        e.synchronize()
+        t = time.time()
+        y = bs.bootstrap(c)
+        e.synchronize()
+        dt = time.time() - t
+        print(json.dumps({"mode": "general", "ms_per_bootstrap": round(1e3 * dt, 1),
+                          "out_level": y.level,
+                          "max_err": float(np.abs(e.decrypt(y, sk) - z).max())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
