@@ -21,6 +21,12 @@ the expensive operations disappear.  The state is carried as +-1 bits B = (-1)^b
   products, depth 3 (plain MixColumns alone: 108 products, depth 3).
 Round depth 4 + 3 = 7 (four rounds per 30-level budget); 24 + 88 + 4 + 140 = 256 key switches
 per 8192 blocks against ~960 for the byte-major nibble-domain round (aes_round.py).
+
+Full AES-128 (`encrypt_aes128`, BASELINE configs 4-5): AddRoundKey(k0), rounds 1-9, and the
+final round without MixColumns (depth 4 + 1), with bit-mode bootstrapping
+(bootstrap.Bootstrapper.bootstrap_bits: two bit ciphertexts per refresh, batched) whenever the
+next round would leave fewer levels than SlotToCoeff needs.  At L = 30: ARK0 -> 29, rounds 1-3
+-> 8, then {refresh -> 17, two rounds -> 3} x 3 and {refresh, final round}: four refreshes.
 """
 from __future__ import annotations
 
@@ -157,6 +163,55 @@ class AESRowRound:
 
     def add_round_key(self, S: List[List[Ciphertext]], key) -> List[List[Ciphertext]]:
         return [[self.mul(S[r][j], key[r][j]) for j in range(8)] for r in range(4)]
+
+    ROUND_DEPTH, FINAL_DEPTH = 7, 5
+
+    def final_round(self, bits, key):
+        """SubBytes -> ShiftRows -> AddRoundKey (AES round 10: no MixColumns), depth 5."""
+        return self.add_round_key(self.shift_rows(self.sub_bytes(bits)), key)
+
+    def refresh(self, bits, bs, pairs_per_call: int = 8):
+        """Bootstrap all 32 bit ciphertexts, two per refresh (bit j with bit j + 4 of a row),
+        `pairs_per_call` pairs concatenated along the batch per Bootstrapper call."""
+        e = self.e
+        pairs = [(r, j) for r in range(4) for j in range(4)]
+        out = [[None] * 8 for _ in range(4)]
+        for i in range(0, len(pairs), pairs_per_call):
+            grp = pairs[i:i + pairs_per_call]
+            nb = bits[0][0].batch
+            a = e.concat([bits[r][j] for r, j in grp])
+            b = e.concat([bits[r][j + 4] for r, j in grp])
+            ya, yb = bs.bootstrap_bits(a, b)
+            for k, (r, j) in enumerate(grp):
+                out[r][j] = e.slice(ya, k * nb, nb)
+                out[r][j + 4] = e.slice(yb, k * nb, nb)
+        return out
+
+    def encrypt_aes128(self, bits, keys, bs, timings: dict | None = None, pairs_per_call: int = 8):
+        """AES-128 encryption of the bit state under the 11 encrypted round keys `keys`
+        (FIPS-197 section 5.1), bootstrapping with `bs` (a bootstrap.Bootstrapper) as the level
+        budget requires.  Returns the state and the number of refreshes."""
+        import time
+        stc = len(bs.stc_bits)
+        S = self.add_round_key(bits, keys[0])
+        refreshes = 0
+        for rnd in range(1, 11):
+            final = rnd == 10
+            need = self.FINAL_DEPTH if final else self.ROUND_DEPTH
+            lvl = min(c.level for row in S for c in row)
+            if lvl < need or (not final and lvl - need < stc):
+                t0 = time.perf_counter()
+                S = self.refresh(S, bs, pairs_per_call)
+                refreshes += 1
+                if timings is not None:
+                    self.e.synchronize()
+                    timings["bootstrap"] = timings.get("bootstrap", 0.0) + time.perf_counter() - t0
+            t0 = time.perf_counter()
+            S = self.final_round(S, keys[rnd]) if final else self.round(S, keys[rnd])
+            if timings is not None:
+                self.e.synchronize()
+                timings["rounds"] = timings.get("rounds", 0.0) + time.perf_counter() - t0
+        return S, refreshes
 
     def round(self, bits, key, timings: dict | None = None):
         """SubBytes -> ShiftRows -> MixColumns -> AddRoundKey on the row-sliced +-1 bit state."""

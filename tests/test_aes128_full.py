@@ -1,0 +1,57 @@
+"""Full AES-128 (10 rounds, FIPS-197 section 5.1) on the row-sliced bit state with bit-mode
+bootstrapping (AESRowRound.encrypt_aes128; BASELINE configs 4-5).
+
+CPU: the oracle engine at N = 2^10 (128 blocks per ciphertext) encrypts random blocks (block 0 =
+the FIPS-197 C.1 plaintext) under the C.1 key, checked block by block against aes_tables.encrypt_block (pinned by the FIPS-197
+appendix vectors in test_aes_tables.py), and block 0 against the published C.1 ciphertext.
+GPU: the same at BASELINE's N = 2^16, L = 30 (8192 blocks per ciphertext)."""
+import numpy as np
+import pytest
+
+from aes_xor_fhe import aes_tables as T
+from aes_xor_fhe.aes_round_bits import AESRowRound
+from aes_xor_fhe.bootstrap import Bootstrapper
+from aes_xor_fhe.fhe import Engine
+
+SCALE_BITS = 41
+FIPS_C1_KEY = bytes(range(16))
+FIPS_C1_PT = bytes.fromhex("00112233445566778899aabbccddeeff")
+FIPS_C1_CT = bytes.fromhex("69c4e0d86a7b0430d8cdb78070b4c55a")
+
+
+def _run(lib, log_n, nb=1, seed=3):
+    e = Engine(log_n=log_n, max_level=30, special_primes=8 if log_n >= 14 else 4,
+               scale_bits=SCALE_BITS, seed=seed, _lib=lib)
+    sk = e.create_secret_key(1)
+    rlk = e.create_relinearization_key(sk)
+    R = AESRowRound(e, sk, e.create_public_key(sk), rlk)
+    bs = Bootstrapper(e, sk, rlk)
+    rng = np.random.default_rng(seed)
+    key = np.frombuffer(FIPS_C1_KEY, dtype=np.uint8)
+    blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
+    blocks[0, 0] = np.frombuffer(FIPS_C1_PT, dtype=np.uint8)
+    rks = T.expand_key(key)
+    keys = [R.encrypt_round_key(rk) for rk in rks]
+    out, nref = R.encrypt_aes128(R.encrypt_blocks(blocks), keys, bs)
+    got = R.decrypt_blocks(out)
+    want = np.stack([[T.encrypt_block(b, key) for b in blk] for blk in blocks])
+    return got, want, nref, out
+
+
+def test_aes128_fips_vector_plain():
+    assert bytes(T.encrypt_block(np.frombuffer(FIPS_C1_PT, np.uint8), FIPS_C1_KEY)) == FIPS_C1_CT
+
+
+def test_aes128_ten_rounds_oracle(oracle_lib):
+    got, want, nref, out = _run(oracle_lib, 10)
+    assert nref == 4
+    assert np.array_equal(got, want)
+    assert bytes(got[0, 0]) == FIPS_C1_CT
+
+
+@pytest.mark.gpu
+def test_aes128_ten_rounds_full_params(product_lib, gpu_available):
+    got, want, nref, out = _run(product_lib, 16)
+    assert nref == 4 and out[0][0].level == 12
+    assert np.array_equal(got, want)
+    assert bytes(got[0, 0]) == FIPS_C1_CT

@@ -12,7 +12,8 @@ from aes_xor_fhe.fhe import Engine  # noqa: E402
 
 layout = sys.argv[1] if len(sys.argv) > 1 else "rows"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-e = Engine(log_n=16, max_level=30, special_primes=8)
+import os
+e = Engine(log_n=16, max_level=30, special_primes=8, scale_bits=int(os.environ.get("SCALE_BITS", 40)))
 sk = e.create_secret_key(1)
 args = (e, sk, e.create_public_key(sk), e.create_relinearization_key(sk), e.create_conjugation_key(sk))
 if layout == "rows":
@@ -33,4 +34,4 @@ tm.pop("start", None)
 tot = sum(tm.values())
 for k, v in tm.items():
     print(f"{k:18s} {v/2*1e3:8.1f} ms  {100*v/tot:5.1f}%")
-print(f"{layout}: total {tot/2*1e3:.1f} ms/round, B={B}, {B*R.n_blk/(tot/2):.0f} blocks/s")
+print(f"{layout} scale {e.scales[-1]:.3g}: total {tot/2*1e3:.1f} ms/round, B={B}, {B*R.n_blk/(tot/2):.0f} blocks/s")
