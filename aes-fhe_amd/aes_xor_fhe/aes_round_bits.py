@@ -207,10 +207,13 @@ class AESRowRound:
                     self.e.synchronize()
                     timings["bootstrap"] = timings.get("bootstrap", 0.0) + time.perf_counter() - t0
             t0 = time.perf_counter()
+            lvl = min(c.level for row in S for c in row)
             S = self.final_round(S, keys[rnd]) if final else self.round(S, keys[rnd])
             if timings is not None:
                 self.e.synchronize()
-                timings["rounds"] = timings.get("rounds", 0.0) + time.perf_counter() - t0
+                dt = time.perf_counter() - t0
+                timings["rounds"] = timings.get("rounds", 0.0) + dt
+                timings.setdefault("per_round", []).append((rnd, lvl, round(1e3 * dt, 1)))
         return S, refreshes
 
     def round(self, bits, key, timings: dict | None = None):

@@ -184,20 +184,54 @@ class Bootstrapper:
         return out
 
     def chebyshev(self, x: Ciphertext) -> Ciphertext:
-        """sum_k c_k T_k(x): T_{a+b} = 2 T_a T_b - T_{|a-b|}, a the largest power of two < k."""
+        """sum_k c_k T_k(x) by recursive Chebyshev division (baby steps T_1..T_b, giants
+        T_2b, T_4b, ...): for d >= g (g the largest giant <= d),
+        p = q T_g + r with T_{g+j} = 2 T_g T_j - T_{g-j}, so q_0 = c_g, q_j = 2 c_{g+j},
+        r_{g-j} -= c_{g+j}; leaves (degree < b) are one lincomb of T_1..T_{b-1}.  For deg 31,
+        b = 8: 11 ciphertext products (T_2..T_8, T_16, three splits) instead of 30, same depth
+        ceil(log2(deg + 1)) + 1."""
         e = self.e
         T = {1: x}
-        for k in range(2, self.deg + 1):
-            a = 1 << (k.bit_length() - 1)
-            if a == k:
-                a = k // 2
-            b = k - a
-            prod = e.multiply(T[a], T[b], self.rlk)
-            t2 = e.add(prod, prod)
-            T[k] = e.add(t2, -1.0) if a == b else e.subtract(t2, T[a - b])
-        ks = [k for k in range(1, self.deg + 1) if abs(self.cheb[k]) > 1e-13]
-        out = e.lincomb([T[k] for k in ks], [complex(self.cheb[k]) for k in ks])
-        return e.add(out, complex(self.cheb[0]))
+
+        def tk(k):
+            if k not in T:
+                a = 1 << (k.bit_length() - 1)
+                if a == k:
+                    a = k // 2
+                b = k - a
+                prod = e.multiply(tk(a), tk(b), self.rlk)
+                t2 = e.add(prod, prod)
+                T[k] = e.add(t2, -1.0) if a == b else e.subtract(t2, tk(a - b))
+            return T[k]
+
+        baby = 1 << max(1, (self.deg + 1).bit_length() // 2)  # 8 for deg 31
+
+        def ev(c):
+            d = len(c) - 1
+            while d > 0 and abs(c[d]) < 1e-14:
+                d -= 1
+            if d < baby:
+                ks = [k for k in range(1, d + 1) if abs(c[k]) > 1e-14]
+                out = e.lincomb([tk(k) for k in ks], [complex(c[k]) for k in ks]) if ks else None
+                return out, complex(c[0])
+            g = baby
+            while 2 * g <= d:
+                g *= 2
+            q = np.zeros(d - g + 1)
+            r = np.array(c[:g], dtype=float)
+            q[0] = c[g]
+            for jj in range(1, d - g + 1):
+                q[jj] = 2.0 * c[g + jj]
+                r[g - jj] -= c[g + jj]
+            qc, q0 = ev(q)
+            rc, r0 = ev(r)
+            qt = e.add(qc, q0) if qc is not None else None
+            prod = e.multiply(qt, tk(g), self.rlk) if qt is not None else e.multiply(tk(g), q0)
+            return (prod if rc is None else e.add(prod, rc)), r0
+
+        out, c0 = ev(list(self.cheb))
+        T.clear()  # ev / tk form a closure cycle: release the T_k now, not at the next gc pass
+        return e.add(out, c0)
 
     def evalmod(self, x: Ciphertext) -> Ciphertext:
         e = self.e
@@ -225,7 +259,9 @@ class Bootstrapper:
         e = self.e
         c = ct if ct.level == 0 else e.level_down(ct, 0)
         x_re, x_im = self._raise_to_slots(c)
-        y = e.add(self.evalmod(x_re), e.multiply_i(self.evalmod(x_im), 1))
+        nb = x_re.batch
+        ys = self.evalmod(e.concat([x_re, x_im]))  # one batched evaluation for both halves
+        y = e.add(e.slice(ys, 0, nb), e.multiply_i(e.slice(ys, nb, nb), 1))
         for plan in self.stc:
             y = self.linear(y, plan)
         return y
@@ -250,6 +286,8 @@ class Bootstrapper:
         for plan in self.stc_bits:
             x = self.linear(x, plan)
         x_re, x_im = self._raise_to_slots(x)
-        ya = self.evalmod(x_re)
-        yb = self.evalmod(x_im) if b is not None else None
-        return ya, yb
+        if b is None:
+            return self.evalmod(x_re), None
+        nb = x_re.batch
+        ys = self.evalmod(e.concat([x_re, x_im]))  # one batched evaluation for both halves
+        return e.slice(ys, 0, nb), e.slice(ys, nb, nb)

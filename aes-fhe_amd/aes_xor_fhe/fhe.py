@@ -67,19 +67,23 @@ class _Handle:
 
 # ------------------------------------------------------------------------------------------
 # keys
-class SecretKey(_Handle):
-    __slots__ = ("engine",)
+class _Key(_Handle):
+    __slots__ = ("engine",)  # keeps the engine (and its device pool) alive
 
 
-class PublicKey(_Handle):
+class SecretKey(_Key):
     __slots__ = ()
 
 
-class RelinearizationKey(_Handle):
+class PublicKey(_Key):
     __slots__ = ()
 
 
-class GaloisKey(_Handle):
+class RelinearizationKey(_Key):
+    __slots__ = ()
+
+
+class GaloisKey(_Key):
     __slots__ = ("galois_elt",)
 
 
@@ -278,27 +282,32 @@ class Engine:
     def _galois_key(self, sk: SecretKey, g: int, cls):
         out = C.c_void_p()
         self._check(self._lib.key_galois(self._h, sk._h, g, C.byref(out)))
-        k = cls(self._lib, out.value, self._lib.key_free)
+        k = self._key(cls, out.value)
         k.galois_elt = g
         return k
 
     # -- keys (engine_context.py:62-73) -------------------------------------------------------
+    def _key(self, cls, h):
+        """Key handles hold the engine: the C key's free returns its buffer to the engine's
+        device pool, so the engine must outlive every key."""
+        k = cls(self._lib, h, self._lib.key_free)
+        k.engine = self
+        return k
+
     def create_secret_key(self, seed: int = 0) -> SecretKey:
         out = C.c_void_p()
         self._check(self._lib.key_secret(self._h, seed, C.byref(out)))
-        sk = SecretKey(self._lib, out.value, self._lib.key_free)
-        sk.engine = self
-        return sk
+        return self._key(SecretKey, out.value)
 
     def create_public_key(self, sk: SecretKey) -> PublicKey:
         out = C.c_void_p()
         self._check(self._lib.key_public(self._h, sk._h, C.byref(out)))
-        return PublicKey(self._lib, out.value, self._lib.key_free)
+        return self._key(PublicKey, out.value)
 
     def create_relinearization_key(self, sk: SecretKey) -> RelinearizationKey:
         out = C.c_void_p()
         self._check(self._lib.key_relin(self._h, sk._h, C.byref(out)))
-        return RelinearizationKey(self._lib, out.value, self._lib.key_free)
+        return self._key(RelinearizationKey, out.value)
 
     def create_conjugation_key(self, sk: SecretKey) -> ConjugationKey:
         g = self._lib.galois_elt(self.log_coeff_count, 0, 1)
@@ -317,15 +326,13 @@ class Engine:
         """Ternary secret with exactly hw nonzeros (aesfhe_key_secret_sparse)."""
         out = C.c_void_p()
         self._check(self._lib.key_secret_sparse(self._h, seed, int(hw), C.byref(out)))
-        sk = SecretKey(self._lib, out.value, self._lib.key_free)
-        sk.engine = self
-        return sk
+        return self._key(SecretKey, out.value)
 
     def create_switching_key(self, sk_from: SecretKey, sk_to: SecretKey) -> GaloisKey:
         """Key switching key sk_from -> sk_to, applied with switch_key (aesfhe_key_switch)."""
         out = C.c_void_p()
         self._check(self._lib.key_switch(self._h, sk_from._h, sk_to._h, C.byref(out)))
-        k = GaloisKey(self._lib, out.value, self._lib.key_free)
+        k = self._key(GaloisKey, out.value)
         k.galois_elt = 1
         return k
 
@@ -582,6 +589,13 @@ class Engine:
         a = np.ascontiguousarray(arr, dtype=np.uint64)
         b, p, l1, _ = a.shape
         return self._call_ct(self._lib.ct_import, _as_ptr(a, C.c_uint64), b, p, l1 - 1)
+
+    def pool_stats(self) -> dict:
+        """Device pool counters (aesfhe_engine_pool_stats): bytes held / live, hipMalloc calls,
+        trims, reuses of a larger cached block."""
+        a = (C.c_int64 * 5)()
+        self._check(self._lib.engine_pool_stats(self._h, a))
+        return dict(zip(("held", "live", "mallocs", "trims", "reuse_larger"), [int(x) for x in a]))
 
     def synchronize(self):
         self._check(self._lib.engine_sync(self._h))

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -77,35 +78,64 @@ extern "C" const char* aesfhe_backend_name(void) { return "hip-gfx950"; }
 // -----------------------------------------------------------------------------------------------
 // engine state
 struct Pool {
+    // Size classes: exact (256 B granularity) up to 1 MiB, then 8 classes per octave (<= 12.5%
+    // slack), so ciphertexts of neighbouring levels / batch sizes share blocks.  A failed
+    // hipMalloc first takes a cached block of up to twice the class, then frees cached blocks
+    // from the largest class down until the allocation fits (never the whole cache at once).
     std::map<size_t, std::vector<void*>> free_;
+    std::unordered_map<void*, size_t> cls_;  // live block -> its class
     size_t held = 0, live = 0;
-    void* get(size_t bytes) {
-        bytes = (bytes + 255) & ~(size_t)255;
-        auto it = free_.find(bytes);
-        if (it != free_.end() && !it->second.empty()) {
-            void* p = it->second.back();
-            it->second.pop_back();
-            live += bytes;
-            return p;
-        }
-        void* p = nullptr;
-        hipError_t e = hipMalloc(&p, bytes);
-        if (e != hipSuccess) {
-            // release cached blocks and retry once
-            (void)hipGetLastError();
-            trim();
-            e = hipMalloc(&p, bytes);
-            if (e != hipSuccess) throw_err(AESFHE_ENOMEM, "hipMalloc(%zu) failed", bytes);
-        }
-        held += bytes;
-        live += bytes;
+    int64_t mallocs = 0, trims = 0, reuse_larger = 0;
+    static size_t size_class(size_t b) {
+        b = (b + 255) & ~(size_t)255;
+        if (b <= ((size_t)1 << 20)) return b;
+        const int lg = 63 - __builtin_clzll(b);
+        const size_t step = (size_t)1 << (lg - 3);
+        return (b + step - 1) & ~(step - 1);
+    }
+    void* take(std::map<size_t, std::vector<void*>>::iterator it) {
+        void* p = it->second.back();
+        it->second.pop_back();
+        cls_[p] = it->first;
+        live += it->first;
         return p;
     }
-    void put(void* p, size_t bytes) {
+    void* get(size_t bytes) {
+        const size_t c = size_class(bytes);
+        auto it = free_.find(c);
+        if (it != free_.end() && !it->second.empty()) return take(it);
+        void* p = nullptr;
+        hipError_t e = hipMalloc(&p, c);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            for (auto j = free_.lower_bound(c); j != free_.end() && j->first <= 2 * c; ++j)
+                if (!j->second.empty()) { reuse_larger++; return take(j); }
+            hipDeviceSynchronize();
+            trims++;
+            for (auto j = free_.rbegin(); j != free_.rend() && e != hipSuccess; ++j) {
+                for (void* q : j->second) {
+                    hipFree(q);
+                    held -= j->first;
+                }
+                j->second.clear();
+                e = hipMalloc(&p, c);
+                if (e != hipSuccess) (void)hipGetLastError();
+            }
+            if (e != hipSuccess) throw_err(AESFHE_ENOMEM, "hipMalloc(%zu) failed", c);
+        }
+        mallocs++;
+        held += c;
+        live += c;
+        cls_[p] = c;
+        return p;
+    }
+    void put(void* p, size_t) {
         if (!p) return;
-        bytes = (bytes + 255) & ~(size_t)255;
-        free_[bytes].push_back(p);
-        live -= bytes;
+        auto it = cls_.find(p);
+        if (it == cls_.end()) return;
+        free_[it->second].push_back(p);
+        live -= it->second;
+        cls_.erase(it);
     }
     void trim() {
         hipDeviceSynchronize();
@@ -762,6 +792,15 @@ extern "C" int aesfhe_engine_profile_read(aesfhe_engine* e, const char* fam, int
     API_END
 }
 extern "C" int64_t aesfhe_engine_device_bytes(const aesfhe_engine* e) { return (int64_t)e->pool.held; }
+extern "C" int aesfhe_engine_pool_stats(const aesfhe_engine* e, int64_t* out) {
+    if (!e || !out) return set_err(AESFHE_EARG, "null argument");
+    out[0] = (int64_t)e->pool.held;
+    out[1] = (int64_t)e->pool.live;
+    out[2] = e->pool.mallocs;
+    out[3] = e->pool.trims;
+    out[4] = e->pool.reuse_larger;
+    return AESFHE_OK;
+}
 
 // -----------------------------------------------------------------------------------------------
 // host codec

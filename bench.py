@@ -160,7 +160,8 @@ def aes128_full(args, eng, drv, rank, barrier, dist):
             "bootstrap_share": round(tm.get("bootstrap", 0.0) / max(el, 1e-9), 3),
             "bootstrap_ms_per_bit_ct": round(1e3 * tm.get("bootstrap", 0.0) / max(nref * 32 * nb, 1), 2),
             "bootstrap_setup_s": round(setup_s, 2), "verified": ok,
-            "block_rounds_per_s": round(10 * nb * R.n_blk * world / el, 2)}
+            "block_rounds_per_s": round(10 * nb * R.n_blk * world / el, 2),
+            "per_round_level_ms": tm.get("per_round"), "pool": eng.pool_stats()}
 
 
 def cpu_baseline(args):

@@ -107,6 +107,10 @@ int aesfhe_engine_profile_read(aesfhe_engine *eng, const char *family, int64_t *
                                double *total_ms, double *bytes);
 /* device bytes currently held by the engine (keys + pool); 0 in the oracle */
 int64_t aesfhe_engine_device_bytes(const aesfhe_engine *eng);
+/* device pool counters: out[0] bytes held, [1] bytes live, [2] hipMalloc calls, [3] trims
+ * (cache releases after a failed hipMalloc), [4] reuses of a larger cached block; zeros in the
+ * oracle */
+int aesfhe_engine_pool_stats(const aesfhe_engine *eng, int64_t *out);
 
 /* ---- host codec (no engine / device needed) --------------------------------------------- */
 /* Canonical-embedding encode: n_slots <= N/2 complex values (zero padded) -> N integer

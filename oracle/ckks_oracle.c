@@ -496,6 +496,12 @@ int64_t aesfhe_engine_device_bytes(const aesfhe_engine *e) {
     (void)e;
     return 0;
 }
+int aesfhe_engine_pool_stats(const aesfhe_engine *e, int64_t *out) {
+    (void)e;
+    if (!out) return AESFHE_EARG;
+    for (int i = 0; i < 5; i++) out[i] = 0;
+    return 0;
+}
 
 /* ------------------------------------------------------------------------------------------ */
 /* host codec: HEAAN special FFT.  Explicit re/im arithmetic, no FMA.          */

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--general", action="store_true")
     ap.add_argument("--batch", type=int, default=1, help="ciphertext pairs per call")
+    ap.add_argument("--phases", action="store_true", help="also time each bootstrap phase")
     a = ap.parse_args()
     e = Engine(log_n=a.log_n, max_level=a.max_level, special_primes=8, scale_bits=a.scale_bits, seed=3)
     sk = e.create_secret_key(1)
@@ -51,6 +52,31 @@ def main():
                       "ms_per_ct": round(1e3 * min(ts) / (2 * a.batch), 2),
                       "out_level": ya.level, "max_err": float(err),
                       "rotation_keys": len(bs.rot)}), flush=True)
+    if a.phases:
+        def timed(fn, *xs):
+            e.synchronize()
+            t0 = time.time()
+            r = fn(*xs)
+            e.synchronize()
+            return r, 1e3 * (time.time() - t0)
+        ph = {}
+        x, ph["combine"] = timed(lambda p, q: e.add(p, e.multiply_i(q, 1)), *cts)
+        for i, plan in enumerate(bs.stc_bits):
+            x, ph[f"stc{i}"] = timed(bs.linear, x, plan)
+        c, ph["to_sparse"] = timed(e.switch_key, x, bs.to_sparse)
+        c, ph["mod_raise"] = timed(e.mod_raise, c, bs.L)
+        c, ph["from_sparse"] = timed(e.switch_key, c, bs.from_sparse)
+        c, ph["c_in"] = timed(e.multiply, c, bs.c_in)
+        for i, plan in enumerate(bs.cts):
+            c, ph[f"cts{i}"] = timed(bs.linear, c, plan)
+        (xr, xi), ph["conj"] = timed(lambda v: (lambda cj: (e.add(v, cj), e.multiply_i(e.subtract(v, cj), -1)))(e.conjugate(v, bs.cjk)), c)
+        xx, ph["concat"] = timed(lambda p, q: e.concat([p, q]), xr, xi)
+        ch, ph["chebyshev"] = timed(bs.chebyshev, xx)
+        y = ch
+        for i in range(bs.r):
+            y, ph[f"double{i}"] = timed(lambda v: (lambda sq: e.add(e.add(sq, sq), -1.0))(e.multiply(v, v, bs.rlk)), y)
+        tot = sum(ph.values())
+        print(json.dumps({"phases_ms": {k: round(v, 2) for k, v in ph.items()}, "total_ms": round(tot, 1)}), flush=True)
     if a.general:
         z = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
         c = e.encrypt(z, pk, level=0)
