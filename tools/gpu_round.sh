@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU-box session: GPU tests, smoke, bench (with CPU baseline), rocprof kernel stats.
+# One GPU-box session: GPU tests, smoke, bench (with CPU baseline), rocprof kernel stats of the
+# headline round (the roofline's region; --aes10-batch 0) and of the 10-round AES-128 run.
 # Every GPU step has its own time limit; steps are chained so a failure stops the script.
 set -o pipefail
 mkdir -p gpurun_out
@@ -11,8 +12,10 @@ timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.lo
  && echo "smoke ok" \
  && timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err \
  && echo "bench ok" \
- && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o bench -- python bench.py --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/prof_${TAG}.log 2>&1 \
- && echo "rocprof ok"
+ && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o bench -- python bench.py --no-cpu-baseline --aes10-batch 0 ${BENCH_ARGS} > gpurun_out/prof_${TAG}.log 2>&1 \
+ && echo "rocprof ok" \
+ && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_aes10 -o aes10 -- python bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS} > gpurun_out/prof_${TAG}_aes10.log 2>&1 \
+ && echo "rocprof aes10 ok"
 rc=$?
 tail -3 gpurun_out/pytest_gpu.log; cat gpurun_out/smoke.log 2>/dev/null | tail -2; cat gpurun_out/bench_${TAG}.json 2>/dev/null
 exit $rc
