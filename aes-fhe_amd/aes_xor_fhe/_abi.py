@@ -64,6 +64,7 @@ SIGNATURES = [
     ("aesfhe_key_public", C.c_int, [c_eng_p, c_key_p, _P(c_key_p)]),
     ("aesfhe_key_relin", C.c_int, [c_eng_p, c_key_p, _P(c_key_p)]),
     ("aesfhe_key_galois", C.c_int, [c_eng_p, c_key_p, C.c_uint64, _P(c_key_p)]),
+    ("aesfhe_key_galois_hoisted", C.c_int, [c_eng_p, c_key_p, C.c_uint64, _P(c_key_p)]),
     ("aesfhe_galois_elt", C.c_uint64, [C.c_int32, C.c_int64, C.c_int32]),
     ("aesfhe_key_info", C.c_int, [c_key_p, _P(C.c_int32), _P(C.c_uint64)]),
     ("aesfhe_key_free", None, [c_key_p]),
@@ -94,6 +95,8 @@ SIGNATURES = [
     ("aesfhe_mul", C.c_int, [c_eng_p, c_ct_p, c_ct_p, c_key_p, _P(c_ct_p)]),
     ("aesfhe_level_down", C.c_int, [c_eng_p, c_ct_p, C.c_int32, _P(c_ct_p)]),
     ("aesfhe_galois", C.c_int, [c_eng_p, c_ct_p, c_key_p, _P(c_ct_p)]),
+    ("aesfhe_mul_fma", C.c_int, [c_eng_p, c_ct_p, c_ct_p, c_key_p, C.c_int64, c_ct_p, C.c_double, C.c_double, _P(c_ct_p)]),
+    ("aesfhe_rotate_hoisted", C.c_int, [c_eng_p, c_ct_p, _P(c_key_p), C.c_int32, _P(c_ct_p)]),
     ("aesfhe_power_basis", C.c_int, [c_eng_p, c_ct_p, C.c_int32, c_key_p, _P(c_ct_p)]),
     ("aesfhe_lincomb", C.c_int,
      [c_eng_p, _P(c_ct_p), C.c_int32, _P(C.c_double), _P(C.c_double), _P(c_ct_p)]),

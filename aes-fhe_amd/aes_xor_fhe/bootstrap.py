@@ -137,13 +137,15 @@ class Bootstrapper:
         stc_bits[-1] = {d: v * c_bits for d, v in stc_bits[-1].items()}
         self.cts, self.stc = [self._prepare(M) for M in cts], [self._prepare(M) for M in stc]
         self.stc_bits = [self._prepare(M) for M in stc_bits]
-        # rotation keys for every baby / giant step
-        shifts = set()
+        # rotation keys: hoisted keys for the baby steps (one ModUp per group input), ordinary
+        # keys for the giant steps
+        babies, giants = set(), set()
         for plan in self.cts + self.stc:  # stc_bits has the offsets of stc
             u, g = plan["u"], plan["g"]
-            shifts.update((k1 * u) % n for k1 in range(1, g))
-            shifts.update((g * k2 * u) % n for k2 in plan["giants"] if (g * k2 * u) % n)
-        self.rot = {d: e.create_fixed_rotation_key(sk, -d) for d in sorted(shifts)}
+            babies.update((k1 * u) % n for k2, tl in plan["terms"].items() for k1, _ in tl if k1)
+            giants.update((g * k2 * u) % n for k2 in plan["giants"] if (g * k2 * u) % n)
+        self.hrot = {d: e.create_hoisted_rotation_key(sk, -d) for d in sorted(babies)}
+        self.rot = {d: e.create_fixed_rotation_key(sk, -d) for d in sorted(giants)}
         # EvalMod: Chebyshev coefficients of cos(2 pi (Bnd x - 1/4) / 2^r) on [-1, 1]
         kk = np.arange(deg + 1)
         xs = np.cos(np.pi * (kk + 0.5) / (deg + 1))
@@ -170,12 +172,13 @@ class Bootstrapper:
         return ct if d == 0 else self.e.rotate(ct, self.rot[d])
 
     def linear(self, ct: Ciphertext, plan) -> Ciphertext:
+        """sum_k D_k * rot(x, k u) as BSGS: the baby rotations of x in one hoisted call."""
         e, u, g = self.e, plan["u"], plan["g"]
+        ks = sorted({k1 for tl in plan["terms"].values() for k1, _ in tl if k1})
         baby = {0: ct}
-        for k2, tl in plan["terms"].items():
-            for k1, _ in tl:
-                if k1 not in baby:
-                    baby[k1] = self._rot(ct, k1 * u)
+        if ks:
+            rots = e.rotate_hoisted(ct, [self.hrot[(k1 * u) % self.n] for k1 in ks])
+            baby.update(zip(ks, rots))
         out = None
         for k2, tl in sorted(plan["terms"].items()):
             part = e.dot_plain([baby[k1] for k1, _ in tl], [pt for _, pt in tl])
@@ -199,9 +202,11 @@ class Bootstrapper:
                 if a == k:
                     a = k // 2
                 b = k - a
-                prod = e.multiply(tk(a), tk(b), self.rlk)
-                t2 = e.add(prod, prod)
-                T[k] = e.add(t2, -1.0) if a == b else e.subtract(t2, tk(a - b))
+                # T_{a+b} = 2 T_a T_b - T_{a-b} (T_0 = 1): one fused multiply-add
+                if a == b:
+                    T[k] = e.multiply_fma(tk(a), tk(b), self.rlk, alpha=2, beta=-1.0)
+                else:
+                    T[k] = e.multiply_fma(tk(a), tk(b), self.rlk, alpha=2, c=tk(a - b), gamma=-1.0)
             return T[k]
 
         baby = 1 << max(1, (self.deg + 1).bit_length() // 2)  # 8 for deg 31
@@ -226,7 +231,12 @@ class Bootstrapper:
             qc, q0 = ev(q)
             rc, r0 = ev(r)
             qt = e.add(qc, q0) if qc is not None else None
-            prod = e.multiply(qt, tk(g), self.rlk) if qt is not None else e.multiply(tk(g), q0)
+            if qt is None:
+                prod = e.multiply(tk(g), q0)
+                return (prod if rc is None else e.add(prod, rc)), r0
+            if rc is not None and rc.level >= min(qt.level, tk(g).level):
+                return e.multiply_fma(qt, tk(g), self.rlk, c=rc, gamma=1.0), r0
+            prod = e.multiply(qt, tk(g), self.rlk)
             return (prod if rc is None else e.add(prod, rc)), r0
 
         out, c0 = ev(list(self.cheb))
@@ -237,8 +247,7 @@ class Bootstrapper:
         e = self.e
         c = self.chebyshev(x)
         for _ in range(self.r):
-            sq = e.multiply(c, c, self.rlk)
-            c = e.add(e.add(sq, sq), -1.0)
+            c = e.multiply_fma(c, c, self.rlk, alpha=2, beta=-1.0)  # cos 2t = 2 cos^2 t - 1
         return c  # sin(2 pi Bnd x)
 
     def _raise_to_slots(self, c: Ciphertext):

@@ -22,7 +22,7 @@ from typing import Sequence
 
 import numpy as np
 
-from ._abi import Lib, Params, c_ct_p, c_pt_p, load_product
+from ._abi import Lib, Params, c_ct_p, c_key_p, c_pt_p, load_product
 
 # HomomorphicEncryption.org 128-bit bound on log2(QP) for ternary secrets
 SECURITY_BUDGET = {11: 54, 12: 109, 13: 218, 14: 438, 15: 881, 16: 1772, 17: 3544}
@@ -67,8 +67,14 @@ class _Handle:
 
 # ------------------------------------------------------------------------------------------
 # keys
-class _Key(_Handle):
-    __slots__ = ("engine",)  # keeps the engine (and its device pool) alive
+class _Owned(_Handle):
+    """A handle whose C free returns memory to the engine's device pool: it holds the engine,
+    and its own __del__ (which runs before its slots are cleared) frees the handle first."""
+    __slots__ = ("engine",)
+
+
+class _Key(_Owned):
+    __slots__ = ()
 
 
 class SecretKey(_Key):
@@ -168,7 +174,8 @@ class Plaintext:
             co = eng._encode_coeffs(self.values, scale)
             out = C.c_void_p()
             eng._check(eng._lib.pt_create(eng._h, _as_ptr(co, C.c_int64), level, C.byref(out)))
-            h = _Handle(eng._lib, out.value, eng._lib.pt_free)
+            h = _Owned(eng._lib, out.value, eng._lib.pt_free)
+            h.engine = eng
             self._dev[key] = h
         return h._h
 
@@ -322,6 +329,26 @@ class Engine:
         k.delta = int(delta)
         return k
 
+    def create_hoisted_rotation_key(self, sk: SecretKey, delta: int) -> FixedRotationKey:
+        """Key for rotate_hoisted (aesfhe_key_galois_hoisted): same slots as
+        create_fixed_rotation_key(sk, delta)."""
+        g = self._lib.galois_elt(self.log_coeff_count, int(delta), 0)
+        out = C.c_void_p()
+        self._check(self._lib.key_galois_hoisted(self._h, sk._h, g, C.byref(out)))
+        k = self._key(FixedRotationKey, out.value)
+        k.galois_elt = g
+        k.delta = int(delta)
+        return k
+
+    def rotate_hoisted(self, ct: Ciphertext, keys: Sequence[FixedRotationKey]) -> list:
+        """Rotations of one ciphertext by every key (create_hoisted_rotation_key), the ModUp of
+        c1 shared (aesfhe_rotate_hoisted)."""
+        n = len(keys)
+        arr = (c_key_p * n)(*[k._h for k in keys])
+        outs = (C.c_void_p * n)()
+        self._check(self._lib.rotate_hoisted(self._h, ct._h, arr, n, outs))
+        return [self._ct(h) for h in outs]
+
     def create_sparse_secret_key(self, hw: int, seed: int = 0) -> SecretKey:
         """Ternary secret with exactly hw nonzeros (aesfhe_key_secret_sparse)."""
         out = C.c_void_p()
@@ -430,6 +457,14 @@ class Engine:
             return self._call_ct(self._lib.mul_const, a._h, c.real, c.imag)
         scale = self._lib.engine_mul_scale(self._h, a.level)
         return self._call_ct(self._lib.mul_pt, a._h, pt.device(a.level, scale))
+
+    def multiply_fma(self, a: Ciphertext, b: Ciphertext, relinearization_key: RelinearizationKey,
+                     alpha: int = 1, c: Ciphertext | None = None, gamma: float = 0.0,
+                     beta: float = 0.0) -> Ciphertext:
+        """alpha * a * b + gamma * c + beta with one relinearisation + rescale (aesfhe_mul_fma);
+        c (level >= the product's) is truncated, not level-downed."""
+        return self._call_ct(self._lib.mul_fma, a._h, b._h, relinearization_key._h, int(alpha),
+                             c._h if c is not None else None, float(gamma), float(beta))
 
     def relinearize(self, ct: Ciphertext, relinearization_key: RelinearizationKey) -> Ciphertext:
         return self._call_ct(self._lib.relinearize, ct._h, relinearization_key._h)

@@ -905,13 +905,15 @@ extern "C" int aesfhe_key_public(aesfhe_engine* e, const aesfhe_key* sk, aesfhe_
     API_END
 }
 
-static aesfhe_key* make_ksk(aesfhe_engine* e, const aesfhe_key* sk, const u64* sprime, int kind, u64 g,
-                            u64 salt = 0) {
+// Switching key s' -> s: s = the target secret's residues `starget` (every limb
+// of Q u P), randomness from `keyseed`.
+static aesfhe_key* make_ksk_t(aesfhe_engine* e, const u64* starget, u64 keyseed, const u64* sprime, int kind,
+                              u64 g, u64 salt) {
     const int N = e->N, np = e->np;
     aesfhe_key* k = key_new(e, kind, (size_t)e->dnum * 2 * np * N);
     k->galois = g;
-    k->keyseed = sk->keyseed;
-    u64 base = derive(derive(sk->keyseed, 4 + (u64)kind), g);
+    k->keyseed = keyseed;
+    u64 base = derive(derive(keyseed, 4 + (u64)kind), g);
     if (salt) base = derive(base, salt);
     Tmp et(e, (size_t)np * N);
     for (int d = 0; d < e->dnum; d++) {
@@ -921,10 +923,14 @@ static aesfhe_key* make_ksk(aesfhe_engine* e, const aesfhe_key* sk, const u64* s
         hipLaunchKernelGGL(k_sample_uniform, dim3(N / 256, np), dim3(256), 0, e->stream, sa, derive(base, 2 * (u64)d), e->q, e->logN, e->Lp1);
         sample_small_ntt(e, et.p, np, derive(base, 2 * (u64)d + 1), 1);
         int lo = d * e->K, hi = std::min(lo + e->K, e->Lp1);
-        hipLaunchKernelGGL(k_key_combine, dim3(N / 256, np), dim3(256), 0, e->stream, (const u64*)ka, sk->d, et.p, sprime, e->pmod, lo, hi, kb, e->q, e->qinv, e->logN);
+        hipLaunchKernelGGL(k_key_combine, dim3(N / 256, np), dim3(256), 0, e->stream, (const u64*)ka, starget, et.p, sprime, e->pmod, lo, hi, kb, e->q, e->qinv, e->logN);
     }
     HIPC(hipGetLastError());
     return k;
+}
+static aesfhe_key* make_ksk(aesfhe_engine* e, const aesfhe_key* sk, const u64* sprime, int kind, u64 g,
+                            u64 salt = 0) {
+    return make_ksk_t(e, sk->d, sk->keyseed, sprime, kind, g, salt);
 }
 
 extern "C" int aesfhe_key_relin(aesfhe_engine* e, const aesfhe_key* sk, aesfhe_key** out) {
@@ -944,6 +950,24 @@ extern "C" int aesfhe_key_galois(aesfhe_engine* e, const aesfhe_key* sk, uint64_
     Span src = span_s(sk->d, 0, e->np, e->Lp1, 0, e->Lp1), dst = span_s(sg.p, 0, e->np, e->Lp1, 0, e->Lp1);
     hipLaunchKernelGGL(k_galois, dim3(e->N / 256, e->np), dim3(256), 0, e->stream, src, dst, (u64)g, e->logN, e->Lp1);
     *out = make_ksk(e, sk, sg.p, 3, g);
+    API_END
+}
+
+// Hoisted rotation key for galois element g (kind 5): switches s -> sigma_g^{-1}(s), so that
+// rotate = sigma_g o keyswitch and the ModUp of c1 is shared by every key of one input
+// (aesfhe_rotate_hoisted).
+extern "C" int aesfhe_key_galois_hoisted(aesfhe_engine* e, const aesfhe_key* sk, uint64_t g, aesfhe_key** out) {
+    API_BEGIN
+    if (!sk || sk->kind != 0) throw_err(AESFHE_EARG, "galois key needs a secret key");
+    if (!(g & 1) || g >= 2ULL * e->N) throw_err(AESFHE_EARG, "bad galois element");
+    const u64 M = 2ULL * e->N;
+    u64 ginv = 1;  // g^{-1} mod 2N = g^(ord(g) - 1): walk the powers of g
+    for (u64 x = 1;; x = x * g % M)
+        if (x * g % M == 1) { ginv = x; break; }
+    Tmp st(e, (size_t)e->np * e->N);
+    Span src = span_s(sk->d, 0, e->np, e->Lp1, 0, e->Lp1), dst = span_s(st.p, 0, e->np, e->Lp1, 0, e->Lp1);
+    hipLaunchKernelGGL(k_galois, dim3(e->N / 256, e->np), dim3(256), 0, e->stream, src, dst, ginv, e->logN, e->Lp1);
+    *out = make_ksk_t(e, st.p, sk->keyseed, sk->d, 5, g, 0x4015);
     API_END
 }
 
@@ -1265,6 +1289,14 @@ static void align_to(aesfhe_engine* e, const aesfhe_ct* c, int l, Aligned& a) {
     }
 }
 
+// c seen at level l <= c->level: its first l+1 limbs, no rescale (the scale stays D_level(c);
+// callers compensate it in a constant)
+static View trunc_view(const aesfhe_ct* c, int l) {
+    View v = view_of(c);
+    v.level = l;
+    return v;
+}
+
 static void check_bcast(int a, int b) {
     if (a != b && a != 1 && b != 1) throw_err(AESFHE_EARG, "batch mismatch %d vs %d", a, b);
 }
@@ -1468,23 +1500,27 @@ extern "C" int aesfhe_dot_pt(aesfhe_engine* e, const aesfhe_ct* const* cts, cons
 // |eps| <= 1/2 per coefficient instead of the fast conversion's 0..K overflow.  r >= 1: combined ModDown + rescale -- P * addend joins the
 // accumulators in the inner product and one base conversion from E = {q_{l-r+1}..q_l, P} divides
 // by D = P q_l ... q_{l-r+1} (oracle/ckks_oracle.c moddown_r states the same procedure).
-static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, const aesfhe_key* k,
-                      Opnd addend, aesfhe_ct* o, int r = 0) {
+static int ks_beta(const aesfhe_engine* e, int l) {
+    const int beta = (l + 1 + e->K - 1) / e->K;
+    if (beta > 12) throw_err(AESFHE_EUNSUPPORTED, "more than 12 key-switch digits");
+    return beta;
+}
+
+// Key switch, first half (ModUp): ext[j][b] = the NTT-domain extension of digit j of d to every
+// limb of Q_l u P outside the digit (the digit's own limbs are read from d by the inner product).
+// ext holds ks_beta(l) * B * (l+1+K) limbs.  Shared by every key in aesfhe_rotate_hoisted.
+static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64* ext) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long lN = (long)(l + 1) * N, neN = (long)ne * N;
-    const int beta = (l + 1 + K - 1) / K;
-    if (beta > 12) throw_err(AESFHE_EUNSUPPORTED, "more than 12 key-switch digits");
-    if (r < 0 || r > kMdrMaxR || K + r > kMdrMaxE || l - r < 0) throw_err(AESFHE_EARG, "bad combined rescale depth %d", r);
-    const int lk = l - r;  // output level
-    const long kN = (long)(lk + 1) * N;
-    Tmp dc(e, (size_t)B * lN), ext(e, (size_t)beta * B * neN), acc(e, (size_t)B * 2 * neN);
+    const int beta = ks_beta(e, l);
+    Tmp dc(e, (size_t)B * lN);
     // 1. INTT copy of the input
     Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1), sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
     ntt(e, sd, sdc, B * (l + 1), true);
     for (int j = 0; j < beta; j++) {
         const int lo = j * K, hi = std::min(lo + K, l + 1), alpha = hi - lo;
         const size_t set = (size_t)j * K + (alpha - 1);
-        u64* exj = ext.p + (size_t)j * B * neN;
+        u64* exj = ext + (size_t)j * B * neN;
         // 2. ModUp base conversion of digit j to every other limb, then NTT those limbs
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
@@ -1503,11 +1539,24 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
             ntt(e, s2, s2, B * nrest, false);
         }
     }
+}
+
+// Key switch, second half: inner product of ext (ks_modup of d) with key k, ModDown (fused with
+// r rescales) and the finish into o (+ addend).
+static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, int B, int l,
+                     const aesfhe_key* k, Opnd addend, aesfhe_ct* o, int r) {
+    const int N = e->N, K = e->K, ne = l + 1 + K;
+    const long neN = (long)ne * N;
+    const int beta = ks_beta(e, l);
+    if (r < 0 || r > kMdrMaxR || K + r > kMdrMaxE || l - r < 0) throw_err(AESFHE_EARG, "bad combined rescale depth %d", r);
+    const int lk = l - r;  // output level
+    const long kN = (long)(lk + 1) * N;
+    Tmp acc(e, (size_t)B * 2 * neN);
     // 3. inner product with every key digit in one pass
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B));
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
-        hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, (const u64*)ext.p, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, addend, r ? (const double*)e->pmodf : (const double*)nullptr, e->logN);
+        hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, addend, r ? (const double*)e->pmodf : (const double*)nullptr, e->logN);
     }
     HIPC(hipGetLastError());
     // 4. ModDown: INTT the dropped limbs (top r Q limbs + the special limbs) of both accumulators
@@ -1551,6 +1600,14 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
     ProfScope psf(e, FAM_KS, 8.0 * N * (double)B * 2 * (lk + 1) * 4);
     hipLaunchKernelGGL(k_moddown_finish, dim3(N / 256, lk + 1, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, (const u64*)conv.p, 2 * kN, kN, fin_add, out_of(o), e->q, dinv, dinvf, e->logN);
     HIPC(hipGetLastError());
+}
+
+static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, const aesfhe_key* k,
+                      Opnd addend, aesfhe_ct* o, int r = 0) {
+    const long neN = (long)(l + 1 + e->K) * e->N;
+    Tmp ext(e, (size_t)ks_beta(e, l) * B * neN);
+    ks_modup(e, d, dbs, B, l, ext.p);
+    ks_apply(e, d, dbs, ext.p, B, l, k, addend, o, r);
 }
 
 static aesfhe_ct* relin_ct(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_key* rlk) {
@@ -1639,6 +1696,61 @@ extern "C" int aesfhe_mul(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct*
     API_END
 }
 
+// out = alpha * a * b + gamma * c + beta with one relinearisation + rescale (oracle:
+// aesfhe_mul_fma states the same constants): c truncated to the product level l, its scale
+// compensated in C = llround(gamma * (D_l * (D_l / D_c))); beta as K = llround(beta D_l) *
+// llround(D_l) mod q on d0.
+extern "C" int aesfhe_mul_fma(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* b, const aesfhe_key* rlk,
+                              int64_t alpha, const aesfhe_ct* c, double gamma, double beta, aesfhe_ct** out) {
+    API_BEGIN
+    if (!rlk || rlk->kind != 2) throw_err(AESFHE_EARG, "multiply needs a relinearization key");
+    if (a->np != 2 || b->np != 2) throw_err(AESFHE_EDEGREE, "multiply inputs should have 2 polynomials");
+    const int l = std::min(a->level, b->level);
+    if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a ciphertext multiplication");
+    int B = std::max(a->B, b->B);
+    if (c) {
+        if (c->np != 2) throw_err(AESFHE_EDEGREE, "fma addend should have 2 polynomials");
+        if (c->level < l) throw_err(AESFHE_ELEVEL, "fma addend level %d below the product level %d", c->level, l);
+        B = std::max(B, c->B);
+    }
+    if ((a->B != B && a->B != 1) || (b->B != B && b->B != 1) || (c && c->B != B && c->B != 1))
+        throw_err(AESFHE_EARG, "batch mismatch");
+    Aligned A, Bv;
+    const bool prod = !a->is_zero && !b->is_zero;
+    if (prod) {
+        align_to(e, a, l, A);
+        align_to(e, b, l, Bv);
+    }
+    const bool hasc = c && !c->is_zero;
+    const double* D = e->chain.scale.data();
+    const int64_t Cc = c ? llround(gamma * (D[l] * (D[l] / D[c->level]))) : 0;
+    const int64_t Rb = llround(beta * D[l]), R = llround(D[l]);
+    std::vector<u64> fac(3 * (size_t)(l + 1));
+    for (int i = 0; i <= l; i++) {
+        const u64 q = e->chain.q[i];
+        fac[3 * i] = h_smod(alpha, q);
+        fac[3 * i + 1] = h_smod(Cc, q);
+        fac[3 * i + 2] = h_mulmod(h_smod(Rb, q), h_smod(R, q), q);
+    }
+    u64* dfac = upload_small(e, fac.data(), fac.size());
+    const Opnd none{nullptr, 0, 0, 0};
+    aesfhe_ct* t = ct_new(e, B, 3, l);
+    {
+        ProfScope ps(e, FAM_EW, 0);
+        hipLaunchKernelGGL(k_tensor_fma, ew_grid(e, l + 1, B), dim3(256), 0, e->stream, prod ? opnd(A.v, B) : none, prod ? opnd(Bv.v, B) : none,
+                           hasc ? opnd(trunc_view(c, l), B) : none, out_of(t), (const u64*)dfac, e->q, e->qinv, e->logN);
+    }
+    HIPC(hipGetLastError());
+    try {
+        *out = relin_rescale(e, t, rlk, 1);
+    } catch (...) {
+        aesfhe_ct_free(t);
+        throw;
+    }
+    aesfhe_ct_free(t);
+    API_END
+}
+
 extern "C" int aesfhe_galois(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_key* gk, aesfhe_ct** out) {
     API_BEGIN
     if (!gk || gk->kind != 3) throw_err(AESFHE_EARG, "galois needs a rotation/conjugation key");
@@ -1659,6 +1771,46 @@ extern "C" int aesfhe_galois(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_
         keyswitch(e, p->d + pv.ps, pv.bs, c->B, l, gk, add, r);
         aesfhe_ct_free(p);
         *out = r;
+    }
+    API_END
+}
+
+// n rotations of one ciphertext with hoisted keys (aesfhe_key_galois_hoisted): ModUp of c1 once,
+// then per key the inner product + ModDown into (c0 + KS_0, KS_1) and sigma_g of both polys.
+extern "C" int aesfhe_rotate_hoisted(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_key* const* keys, int32_t n,
+                                     aesfhe_ct** outs) {
+    API_BEGIN
+    if (n < 1) throw_err(AESFHE_EARG, "rotate_hoisted needs at least one key");
+    for (int i = 0; i < n; i++)
+        if (!keys[i] || keys[i]->kind != 5) throw_err(AESFHE_EARG, "rotate_hoisted needs hoisted rotation keys");
+    if (c->np != 2) throw_err(AESFHE_EDEGREE, "Input ciphertext should have 2 polynomials");
+    const int N = e->N, l = c->level, B = c->B;
+    for (int i = 0; i < n; i++) outs[i] = nullptr;
+    try {
+        if (c->is_zero) {
+            for (int i = 0; i < n; i++) outs[i] = ct_zero_new(e, B, 2, l);
+        } else {
+            const long neN = (long)(l + 1 + e->K) * N;
+            View cv = view_of(c);
+            const u64* c1 = c->d + cv.ps;
+            Tmp ext(e, (size_t)ks_beta(e, l) * B * neN);
+            ks_modup(e, c1, cv.bs, B, l, ext.p);
+            for (int i = 0; i < n; i++) {
+                aesfhe_ct* r = ct_new(e, B, 2, l);
+                Opnd add = opnd(cv, B);
+                add.np = 1;  // output 0 gets c0
+                ks_apply(e, c1, cv.bs, ext.p, B, l, keys[i], add, r, 0);
+                aesfhe_ct* o = ct_new(e, B, 2, l);
+                Span src = span_s(r->d, (long)(l + 1) * N, l + 1, l + 1, 0, e->Lp1), dst = span_s(o->d, (long)(l + 1) * N, l + 1, l + 1, 0, e->Lp1);
+                hipLaunchKernelGGL(k_galois, dim3(N / 256, B * 2 * (l + 1)), dim3(256), 0, e->stream, src, dst, (u64)keys[i]->galois, e->logN, e->Lp1);
+                HIPC(hipGetLastError());
+                aesfhe_ct_free(r);
+                outs[i] = o;
+            }
+        }
+    } catch (...) {
+        for (int i = 0; i < n; i++) aesfhe_ct_free(outs[i]), outs[i] = nullptr;
+        throw;
     }
     API_END
 }
@@ -1724,14 +1876,16 @@ extern "C" int aesfhe_lincomb(aesfhe_engine* e, const aesfhe_ct* const* cts, int
     std::vector<int> npi;
     std::vector<u64> f;
     std::vector<double> ff;
+    std::vector<long> pss;
     for (int i = 0; i < n; i++) {
-        int64_t A = llround(re[i] * s), Bc = llround(im[i] * s);
+        // inputs above l are truncated to its limbs, their scale compensated in the constant
+        const double si = s * (e->chain.scale[l] / e->chain.scale[cts[i]->level]);
+        int64_t A = llround(re[i] * si), Bc = llround(im[i] * si);
         if (cts[i]->is_zero || (A == 0 && Bc == 0)) continue;
-        al.emplace_back(new Aligned());
-        align_to(e, cts[i], l, *al.back());
-        const View& v = al.back()->v;
+        const View v = trunc_view(cts[i], l);
         ptrs.push_back(v.d);
         bstr.push_back(v.B == 1 && B > 1 ? 0 : v.bs);
+        pss.push_back(v.ps);
         npi.push_back(v.np);
         std::vector<u64> fi;
         std::vector<double> ffi;
@@ -1743,16 +1897,16 @@ extern "C" int aesfhe_lincomb(aesfhe_engine* e, const aesfhe_ct* const* cts, int
         *out = ct_zero_new(e, B, np, l - 1);
     } else {
         const int m = (int)ptrs.size();
-        const long ps = (long)nl * e->N;
         aesfhe_ct* acc = ct_new(e, B, np, l);
         auto dp = upload_small(e, ptrs.data(), ptrs.size());
         auto db = upload_small(e, bstr.data(), bstr.size());
+        auto dps = upload_small(e, pss.data(), pss.size());
         auto dn = upload_small(e, npi.data(), npi.size());
         auto df = upload_small(e, f.data(), f.size());
         auto dff = upload_small(e, ff.data(), ff.size());
         {
             ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (m + 1));
-            hipLaunchKernelGGL(k_lincomb, ew_grid(e, nl, B * np), dim3(256), 0, e->stream, (const u64* const*)dp, (const long*)db, (const int*)dn, m, ps, (const u64*)df, (const double*)dff, out_of(acc), np, nl, e->q, e->qinv, e->logN);
+            hipLaunchKernelGGL(k_lincomb, ew_grid(e, nl, B * np), dim3(256), 0, e->stream, (const u64* const*)dp, (const long*)db, (const int*)dn, m, (const long*)dps, (const u64*)df, (const double*)dff, out_of(acc), np, nl, e->q, e->qinv, e->logN);
         }
         HIPC(hipGetLastError());
         *out = rescale_view(e, view_of(acc));
@@ -1788,7 +1942,8 @@ extern "C" int aesfhe_lincomb_many(aesfhe_engine* e, const aesfhe_ct* const* cts
     for (int r = 0; r < m; r++) {
         bool any = false;
         for (int i = 0; i < n; i++) {
-            int64_t A = llround(re[(size_t)r * n + i] * s), Bc = llround(im[(size_t)r * n + i] * s);
+            const double si = s * (e->chain.scale[l] / e->chain.scale[cts[i]->level]);
+            int64_t A = llround(re[(size_t)r * n + i] * si), Bc = llround(im[(size_t)r * n + i] * si);
             if (!cts[i]->is_zero && (A || Bc)) any = true, used[i] = 1;
         }
         if (any) live.push_back(r);
@@ -1801,12 +1956,12 @@ extern "C" int aesfhe_lincomb_many(aesfhe_engine* e, const aesfhe_ct* const* cts
     std::vector<const u64*> ptrs;
     std::vector<long> bstr;
     std::vector<int> npi;
-    for (int i : cols) {
-        al.emplace_back(new Aligned());
-        align_to(e, cts[i], l, *al.back());
-        const View& v = al.back()->v;
+    std::vector<long> pss;
+    for (int i : cols) {  // truncated to level l (scale compensated in F below)
+        const View v = trunc_view(cts[i], l);
         ptrs.push_back(v.d);
         bstr.push_back(v.B == 1 && B > 1 ? 0 : v.bs);
+        pss.push_back(v.ps);
         npi.push_back(v.np);
     }
     const int nc = (int)cols.size(), ml = (int)live.size();
@@ -1816,7 +1971,8 @@ extern "C" int aesfhe_lincomb_many(aesfhe_engine* e, const aesfhe_ct* const* cts
         for (int r = 0; r < ml; r++)
             for (int c = 0; c < nc; c++) {
                 const size_t idx = (size_t)live[r] * n + cols[c];
-                int64_t A = llround(re[idx] * s), Bc = llround(im[idx] * s);
+                const double si = s * (e->chain.scale[l] / e->chain.scale[cts[cols[c]]->level]);
+                int64_t A = llround(re[idx] * si), Bc = llround(im[idx] * si);
                 if (cts[cols[c]]->is_zero) A = Bc = 0;
                 std::vector<u64> fi;
                 std::vector<double> ffi;
@@ -1828,12 +1984,13 @@ extern "C" int aesfhe_lincomb_many(aesfhe_engine* e, const aesfhe_ct* const* cts
         Tmp acc(e, (size_t)ml * orow);
         auto dp = upload_small(e, ptrs.data(), ptrs.size());
         auto db = upload_small(e, bstr.data(), bstr.size());
+        auto dps = upload_small(e, pss.data(), pss.size());
         auto dn = upload_small(e, npi.data(), npi.size());
         auto dF = upload_small(e, F.data(), F.size());
         auto dFF = upload_small(e, FF.data(), FF.size());
         {
             ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (nc + ml));
-            hipLaunchKernelGGL(k_lincomb_many, ew_grid(e, nl, B * np), dim3(256), 0, e->stream, (const u64* const*)dp, (const long*)db, (const int*)dn, nc, ps, (const u64*)dF, (const double*)dFF, ml, acc.p, orow, obs, np, nl, e->q, e->qinv, e->logN);
+            hipLaunchKernelGGL(k_lincomb_many, ew_grid(e, nl, B * np), dim3(256), 0, e->stream, (const u64* const*)dp, (const long*)db, (const int*)dn, nc, (const long*)dps, (const u64*)dF, (const double*)dFF, ml, acc.p, orow, obs, np, nl, e->q, e->qinv, e->logN);
         }
         HIPC(hipGetLastError());
         std::vector<aesfhe_ct*> res = rescale_groups(e, acc.p, ml, B, np, l);

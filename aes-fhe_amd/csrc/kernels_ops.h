@@ -111,23 +111,47 @@ __global__ void k_tensor(Opnd a, Opnd b, Out o, const u64* __restrict__ qs,
     }
 }
 
+// Fused multiply-add tensor (aesfhe_mul_fma): (d0, d1, d2) = alpha (a (x) b) + C (c0, c1, 0)
+// + (K, 0, 0), fac[l] = {alpha, C, K} mod q_l; absent operands read as zero.  grid (N/256, nl, B)
+__global__ void k_tensor_fma(Opnd a, Opnd b, Opnd c, Out o, const u64* __restrict__ fac,
+                             const u64* __restrict__ qs, const double* __restrict__ qinv, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z;
+    const u64 q = qs[l];
+    const double qi = qinv[l];
+    const u64 am = fac[3 * l], cm = fac[3 * l + 1], km = fac[3 * l + 2];
+    const u64 a0 = opnd_get(a, bb, 0, l, k, logN), a1 = opnd_get(a, bb, 1, l, k, logN);
+    const u64 b0 = opnd_get(b, bb, 0, l, k, logN), b1 = opnd_get(b, bb, 1, l, k, logN);
+    u64 d0 = mul_m(mul_m(a0, b0, q, qi), am, q, qi);
+    u64 d1 = mul_m(add_m(mul_m(a0, b1, q, qi), mul_m(a1, b0, q, qi), q), am, q, qi);
+    const u64 d2 = mul_m(mul_m(a1, b1, q, qi), am, q, qi);
+    d0 = add_m(d0, mul_m(opnd_get(c, bb, 0, l, k, logN), cm, q, qi), q);
+    d1 = add_m(d1, mul_m(opnd_get(c, bb, 1, l, k, logN), cm, q, qi), q);
+    d0 = add_m(d0, km, q);
+    u64* base = o.ptr + (long)bb * o.bs + ((long)l << logN) + k;
+    base[0] = d0;
+    base[o.ps] = d1;
+    base[2 * o.ps] = d2;
+}
+
 // Fused linear combination: out[b][p][l] = sum_i in_i[b][p][l] * f_i(l, half) (one pass, lazy
 // sum in u64: n <= 64 terms of < 2^51 each).  ptrs/bstr: [n]; f/ff: [n][nl][2].  Inputs with
 // fewer polynomials than np contribute zero to the missing ones (npi[i]).
 // grid (N/256, nl, B*np)
 __global__ void k_lincomb(const u64* const* __restrict__ ptrs, const long* __restrict__ bstr,
-                          const int* __restrict__ npi, int n, long ps, const u64* __restrict__ f,
+                          const int* __restrict__ npi, int n, const long* __restrict__ pss,
+                          const u64* __restrict__ f,
                           const double* __restrict__ ff, Out o, int np, int nl,
                           const u64* __restrict__ qs, const double* __restrict__ qinv, int logN) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int l = blockIdx.y, bb = blockIdx.z / np, p = blockIdx.z - bb * np;
     const u64 q = qs[l];
     const int h = k >> (logN - 1);
-    const long off = (long)p * ps + ((long)l << logN) + k;
+    const long off = ((long)l << logN) + k;
     u64 acc = 0;
     for (int i = 0; i < n; i++) {
         if (p >= npi[i]) continue;
-        const u64 v = ptrs[i][(long)bb * bstr[i] + off];
+        const u64 v = ptrs[i][(long)bb * bstr[i] + (long)p * pss[i] + off];
         const int fi = (i * nl + l) * 2 + h;
         acc += mulw(v, f[fi], ff[fi], q);
     }
@@ -138,7 +162,7 @@ __global__ void k_lincomb(const u64* const* __restrict__ ptrs, const long* __res
 // (row-uniform factors -> scalar loads).  out: [m][B][np][nl][N].  grid (N/256, nl, B*np)
 constexpr int kManyMax = 16;
 __global__ void k_lincomb_many(const u64* const* __restrict__ ptrs, const long* __restrict__ bstr,
-                               const int* __restrict__ npi, int n, long ps,
+                               const int* __restrict__ npi, int n, const long* __restrict__ pss,
                                const u64* __restrict__ F, const double* __restrict__ FF, int m,
                                u64* __restrict__ out, long orow, long obs, int np, int nl,
                                const u64* __restrict__ qs, const double* __restrict__ qinv,
@@ -147,12 +171,12 @@ __global__ void k_lincomb_many(const u64* const* __restrict__ ptrs, const long* 
     const int l = blockIdx.y, bb = blockIdx.z / np, p = blockIdx.z - bb * np;
     const u64 q = qs[l];
     const int h = k >> (logN - 1);
-    const long off = (long)p * ps + ((long)l << logN) + k;
+    const long off = ((long)l << logN) + k;
     u64 v[kManyMax];
 #pragma unroll
     for (int j = 0; j < kManyMax; j++)
-        v[j] = (j < n && p < npi[j]) ? ptrs[j][(long)bb * bstr[j] + off] : 0;
-    u64* o = out + (long)bb * obs + off;
+        v[j] = (j < n && p < npi[j]) ? ptrs[j][(long)bb * bstr[j] + (long)p * pss[j] + off] : 0;
+    u64* o = out + (long)bb * obs + ((long)p * nl << logN) + off;
     for (int i = 0; i < m; i++) {
         u64 acc = 0;
 #pragma unroll

@@ -134,6 +134,11 @@ int aesfhe_key_relin(aesfhe_engine *eng, const aesfhe_key *sk, aesfhe_key **out)
 int aesfhe_key_galois(aesfhe_engine *eng, const aesfhe_key *sk, uint64_t galois_elt,
                       aesfhe_key **out);
 uint64_t aesfhe_galois_elt(int32_t log_n, int64_t rotation, int32_t conjugate);
+/* Hoisted rotation key for galois_elt g: a switching key s -> sigma_g^{-1}(s) (kind 5), for
+ * aesfhe_rotate_hoisted.  (No reference counterpart: desilofhe's bootstrap keys are internal,
+ * engine_context.py:72-73; used by the CoeffToSlot / SlotToCoeff baby steps.) */
+int aesfhe_key_galois_hoisted(aesfhe_engine *eng, const aesfhe_key *sk, uint64_t galois_elt,
+                              aesfhe_key **out);
 /* Sparse ternary secret with exactly hw nonzeros (bootstrapping's ephemeral secret, for the
  * ModRaise overflow bound): key = derive(derive(seed_e, seed), 9); partial Fisher-Yates over
  * 0..N-1 -- step i swaps i with i + rnd(key, i) mod (N - i) and sets that coefficient to -1 if
@@ -208,12 +213,26 @@ int aesfhe_mul(aesfhe_engine *eng, const aesfhe_ct *a, const aesfhe_ct *b,
 int aesfhe_level_down(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t level,
                       aesfhe_ct **out);
 /* automorphism X -> X^g followed by key switching back to s (rotation / conjugation) */
+/* n rotations of one ciphertext with hoisted keys: outs[i] = sigma_{g_i}((c0 + KS_i(c1)_0,
+ * KS_i(c1)_1)), the ModUp of c1 computed once for all n (the same slots as aesfhe_galois with
+ * the ordinary key of g_i; residues differ only in the key-switch noise). */
+int aesfhe_rotate_hoisted(aesfhe_engine *eng, const aesfhe_ct *ct, const aesfhe_key *const *keys,
+                          int32_t n, aesfhe_ct **outs);
+/* out = alpha * a * b + gamma * c + beta, one relinearisation + rescale: level
+ * l - 1 for l = min(level a, level b) (a, b level-downed to l), c (optional, level >= l) truncated
+ * to l with C = llround(gamma * (D_l * (D_l / D_c))), beta added to d0 as
+ * llround(beta * D_l) * llround(D_l) mod q.  (Fused T_{a+b} = 2 T_a T_b - T_{a-b} and double
+ * angles of the bootstrapping's EvalMod; no reference counterpart.) */
+int aesfhe_mul_fma(aesfhe_engine *eng, const aesfhe_ct *a, const aesfhe_ct *b, const aesfhe_key *rlk,
+                   int64_t alpha, const aesfhe_ct *c, double gamma, double beta, aesfhe_ct **out);
 int aesfhe_galois(aesfhe_engine *eng, const aesfhe_ct *ct, const aesfhe_key *gk,
                   aesfhe_ct **out);
 /* outs[0..d-1] = ct^1 .. ct^d, ct^k at level(ct) - ceil(log2 k) */
 int aesfhe_power_basis(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t d,
                        const aesfhe_key *rlk, aesfhe_ct **outs);
-/* sum_i (re_i + i*im_i) * cts[i], aligned to the lowest input level, output at that - 1 */
+/* sum_i (re_i + i*im_i) * cts[i] at the lowest input level l, output at l - 1.  Inputs above l
+ * are truncated to its limbs (no rescale) and their scale D_level compensated in the constant:
+ * A = llround(re * mul_scale(l) * (D_l / D_level)). */
 int aesfhe_lincomb(aesfhe_engine *eng, const aesfhe_ct *const *cts, int32_t n,
                    const double *re, const double *im, aesfhe_ct **out);
 /* m linear combinations of the same n inputs in one pass: outs[r] = lincomb(cts, re/im row r)

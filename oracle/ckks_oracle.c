@@ -763,15 +763,22 @@ static aesfhe_key *make_ksk(aesfhe_engine *e, const aesfhe_key *sk, const u64 *s
                             u64 g) {
     return make_ksk_salt(e, sk, sprime, kind, g, 0);
 }
+static aesfhe_key *make_ksk_t(aesfhe_engine *e, const u64 *starget, u64 keyseed, const u64 *sprime,
+                              int kind, u64 g, u64 salt);
 static aesfhe_key *make_ksk_salt(aesfhe_engine *e, const aesfhe_key *sk, const u64 *sprime, int kind,
                                  u64 g, u64 salt) {
+    return make_ksk_t(e, sk->data, sk->keyseed, sprime, kind, g, salt);
+}
+/* switching key s' -> s: s = `starget` (all limbs of Q u P), stream from keyseed */
+static aesfhe_key *make_ksk_t(aesfhe_engine *e, const u64 *starget, u64 keyseed, const u64 *sprime,
+                              int kind, u64 g, u64 salt) {
     const int N = e->N, np = e->np, nq = e->L + 1;
     aesfhe_key *k = calloc(1, sizeof *k);
     k->kind = kind;
     k->galois = g;
-    k->keyseed = sk->keyseed;
+    k->keyseed = keyseed;
     k->data = malloc(sizeof(u64) * (size_t)e->dnum * 2 * np * N);
-    u64 base = derive(derive(sk->keyseed, 4 + (u64)kind), g);
+    u64 base = derive(derive(keyseed, 4 + (u64)kind), g);
     if (salt) base = derive(base, salt);
     /* P mod q_i */
     u64 Pmod[MAXP];
@@ -789,7 +796,7 @@ static aesfhe_key *make_ksk_salt(aesfhe_engine *e, const aesfhe_key *sk, const u
         for (int p = 0; p < np; p++) {
             u64 *b = k->data + (((size_t)d * 2 + 0) * np + p) * N;
             u64 *a = k->data + (((size_t)d * 2 + 1) * np + p) * N;
-            const u64 *s = sk->data + (size_t)p * N;
+            const u64 *s = starget + (size_t)p * N;
             const u64 q = e->q[p];
             u64 *et = malloc(sizeof(u64) * N);
             coeffs_to_ntt(e, ee, et, p);
@@ -854,6 +861,23 @@ int aesfhe_key_switch(aesfhe_engine *e, const aesfhe_key *sk_from, const aesfhe_
     if (!sk_from || !sk_to || sk_from->kind != 0 || sk_to->kind != 0)
         return fail(AESFHE_EARG, "switching key needs two secret keys");
     *out = make_ksk_salt(e, sk_to, sk_from->data, 3, 1, sk_from->keyseed | 1);
+    return 0;
+}
+
+/* hoisted rotation key for g (kind 5): switches s -> sigma_g^{-1}(s); aesfhe_rotate_hoisted
+ * applies it as rotate = sigma_g o keyswitch (the HIP engine shares the ModUp of c1) */
+int aesfhe_key_galois_hoisted(aesfhe_engine *e, const aesfhe_key *sk, uint64_t g, aesfhe_key **out) {
+    if (!sk || sk->kind != 0) return fail(AESFHE_EARG, "galois key needs a secret key");
+    if (!(g & 1) || g >= 2ULL * e->N) return fail(AESFHE_EARG, "bad galois element");
+    const int N = e->N;
+    const u64 M = 2ULL * (u64)N;
+    u64 ginv = 1;
+    for (u64 x = 1;; x = x * g % M)
+        if (x * g % M == 1) { ginv = x; break; }
+    u64 *st = malloc(sizeof(u64) * (size_t)e->np * N);
+    for (int p = 0; p < e->np; p++) galois_perm(e, sk->data + (size_t)p * N, st + (size_t)p * N, ginv);
+    *out = make_ksk_t(e, st, sk->keyseed, sk->data, 5, g, 0x4015);
+    free(st);
     return 0;
 }
 
@@ -1545,6 +1569,44 @@ int aesfhe_galois(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_key *gk, ae
     return 0;
 }
 
+/* n rotations with hoisted keys: out_i = sigma_g((c0 + KS_0, KS_1)), KS = keyswitch of c1 (not
+ * permuted) with key i; the ModUp of c1 is the same for every key (the HIP engine computes it once) */
+int aesfhe_rotate_hoisted(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_key *const *keys, int32_t n,
+                          aesfhe_ct **outs) {
+    if (n < 1) return fail(AESFHE_EARG, "rotate_hoisted needs at least one key");
+    for (int i = 0; i < n; i++)
+        if (!keys[i] || keys[i]->kind != 5) return fail(AESFHE_EARG, "rotate_hoisted needs hoisted rotation keys");
+    if (c->npoly != 2) return fail(AESFHE_EDEGREE, "Input ciphertext should have 2 polynomials");
+    const int N = e->N, l = c->level;
+    u64 *k0 = malloc(sizeof(u64) * (size_t)(l + 1) * N), *k1 = malloc(sizeof(u64) * (size_t)(l + 1) * N);
+    u64 *t = malloc(sizeof(u64) * (size_t)N);
+    for (int i = 0; i < n; i++) {
+        aesfhe_ct *r = ct_new(e, c->B, 2, l);
+        outs[i] = r;
+        if (c->is_zero) {
+            r->is_zero = 1;
+            continue;
+        }
+        for (int b = 0; b < c->B; b++) {
+            u64 *c1 = malloc(sizeof(u64) * (size_t)(l + 1) * N);
+            for (int p = 0; p <= l; p++) memcpy(c1 + (size_t)p * N, limb(e, c, b, 1, p), sizeof(u64) * N);
+            keyswitch(e, c1, l, keys[i], k0, k1);
+            free(c1);
+            for (int p = 0; p <= l; p++) {
+                const u64 q = e->q[p];
+                const u64 *c0 = limb(e, c, b, 0, p);
+                for (int j = 0; j < N; j++) t[j] = add_mod(c0[j], k0[(size_t)p * N + j], q);
+                galois_perm(e, t, limb(e, r, b, 0, p), keys[i]->galois);
+                galois_perm(e, k1 + (size_t)p * N, limb(e, r, b, 1, p), keys[i]->galois);
+            }
+        }
+    }
+    free(k0);
+    free(k1);
+    free(t);
+    return 0;
+}
+
 int aesfhe_power_basis(aesfhe_engine *e, const aesfhe_ct *c, int32_t d, const aesfhe_key *rlk, aesfhe_ct **outs) {
     if (d < 1) return fail(AESFHE_EARG, "degree must be >= 1");
     int need = 0;
@@ -1578,10 +1640,13 @@ int aesfhe_lincomb(aesfhe_engine *e, const aesfhe_ct *const *cts, int32_t n, con
     aesfhe_ct *acc = ct_new(e, B, np, l);
     int any = 0;
     for (int i = 0; i < n; i++) {
-        i64 A = llround(re[i] * s), Bc = llround(im[i] * s);
+        /* inputs above level l are truncated to its limbs (no rescale) and their scale
+         * D_level is compensated in the constant: si = s * (D_l / D_level) */
+        const double si = s * (e->scales[l] / e->scales[cts[i]->level]);
+        i64 A = llround(re[i] * si), Bc = llround(im[i] * si);
         if (cts[i]->is_zero || (A == 0 && Bc == 0)) continue;
         any = 1;
-        aesfhe_ct *t = level_down_raw(e, cts[i], l);
+        aesfhe_ct *t = truncate_ct(e, cts[i], l);
         mul_int_const_inplace(e, t, A, Bc);
         for (int b = 0; b < B; b++)
             for (int pp = 0; pp < t->npoly; pp++)
@@ -1602,6 +1667,59 @@ int aesfhe_lincomb(aesfhe_engine *e, const aesfhe_ct *const *cts, int32_t n, con
     }
     *out = rescale_raw(e, acc);
     aesfhe_ct_free(acc);
+    return 0;
+}
+
+/* out = alpha * a * b + gamma * c + beta, one relinearisation + rescale (include/aesfhe.h):
+ * (d0, d1, d2) = alpha * tensor(a, b) at l = min(level a, level b) (a, b level-downed to l),
+ * plus C * c truncated to l (C = llround(gamma * (D_l * (D_l / D_c)))), plus the constant
+ * K = (llround(beta * D_l) mod q) * (llround(D_l) mod q) on d0; then relin + rescale -> l - 1 */
+int aesfhe_mul_fma(aesfhe_engine *e, const aesfhe_ct *a, const aesfhe_ct *b, const aesfhe_key *rlk,
+                   int64_t alpha, const aesfhe_ct *c, double gamma, double beta, aesfhe_ct **out) {
+    if (!rlk || rlk->kind != 2) return fail(AESFHE_EARG, "multiply needs a relinearization key");
+    if (a->npoly != 2 || b->npoly != 2) return fail(AESFHE_EDEGREE, "multiply inputs should have 2 polynomials");
+    const int l = a->level < b->level ? a->level : b->level;
+    if (l < 1) return fail(AESFHE_ELEVEL, "no level left for a ciphertext multiplication");
+    int B = a->B > b->B ? a->B : b->B;
+    if (c) {
+        if (c->npoly != 2) return fail(AESFHE_EDEGREE, "fma addend should have 2 polynomials");
+        if (c->level < l) return fail(AESFHE_ELEVEL, "fma addend level %d below the product level %d", c->level, l);
+        if (c->B > B) B = c->B;
+    }
+    if ((a->B != B && a->B != 1) || (b->B != B && b->B != 1) || (c && c->B != B && c->B != 1))
+        return fail(AESFHE_EARG, "batch mismatch");
+    const int N = e->N;
+    aesfhe_ct *t = ct_new(e, B, 3, l);
+    if (!a->is_zero && !b->is_zero) {
+        aesfhe_ct *x = level_down_raw(e, a, l), *y = level_down_raw(e, b, l);
+        tensor_acc(e, x, y, t);
+        aesfhe_ct_free(x);
+        aesfhe_ct_free(y);
+    }
+    const i64 Cc = c ? llround(gamma * (e->scales[l] * (e->scales[l] / e->scales[c->level]))) : 0;
+    const i64 Rb = llround(beta * e->scales[l]), R = llround(e->scales[l]);
+    for (int bb = 0; bb < B; bb++)
+        for (int i = 0; i <= l; i++) {
+            const u64 q = e->q[i];
+            const u64 am = smod(alpha, q), cm = smod(Cc, q);
+            const u64 km = mul_mod_slow(smod(Rb, q), smod(R, q), q);
+            u64 *d0 = limb(e, t, bb, 0, i), *d1 = limb(e, t, bb, 1, i), *d2 = limb(e, t, bb, 2, i);
+            const int cz = !c || c->is_zero;
+            const u64 *c0 = cz ? NULL : limb(e, c, c->B == 1 ? 0 : bb, 0, i);
+            const u64 *c1 = cz ? NULL : limb(e, c, c->B == 1 ? 0 : bb, 1, i);
+            for (int j = 0; j < N; j++) {
+                u64 v0 = mul_mod_slow(d0[j], am, q), v1 = mul_mod_slow(d1[j], am, q);
+                if (c0) {
+                    v0 = add_mod(v0, mul_mod_slow(c0[j], cm, q), q);
+                    v1 = add_mod(v1, mul_mod_slow(c1[j], cm, q), q);
+                }
+                d0[j] = add_mod(v0, km, q);
+                d1[j] = v1;
+                d2[j] = mul_mod_slow(d2[j], am, q);
+            }
+        }
+    *out = relin_rescale_raw(e, t, rlk, 1);
+    aesfhe_ct_free(t);
     return 0;
 }
 

@@ -177,3 +177,38 @@ def test_poly2_int_bit_exact(product_lib, oracle_lib, gpu_available):
         _same(g, o, a, b)
     want = sum(W[0, i, j] / 64 * zx ** i * zy ** j for i in range(4) for j in range(5))
     np.testing.assert_allclose(g.decrypt(res[0][0], kg["sk"]), want, atol=1e-4)
+
+
+def test_rotate_hoisted_bit_exact(product_lib, oracle_lib, gpu_available):
+    """aesfhe_rotate_hoisted (one ModUp shared by every key) against the oracle's per-key
+    restatement; slots equal np.roll like the ordinary rotation."""
+    g, o = _pair(product_lib, oracle_lib, **SMALL)
+    outs = []
+    rng = np.random.default_rng(3)
+    z = rng.uniform(-1, 1, (2, g.slot_count))
+    for eng in (g, o):
+        sk = eng.create_secret_key(7)
+        c = eng.encrypt(z, eng.create_public_key(sk), level=4)
+        keys = [eng.create_hoisted_rotation_key(sk, d) for d in (1, -5, 64)]
+        outs.append((eng.rotate_hoisted(c, keys), sk))
+    for cg, co in zip(outs[0][0], outs[1][0]):
+        _same(g, o, cg, co)
+    for d, cg in zip((1, -5, 64), outs[0][0]):
+        np.testing.assert_allclose(g.decrypt(cg, outs[0][1]), np.roll(z, d, axis=1), atol=1e-6)
+
+
+def test_mul_fma_and_mixed_lincomb_bit_exact(product_lib, oracle_lib, gpu_available):
+    g, o = _pair(product_lib, oracle_lib, **SMALL)
+    res = []
+    rng = np.random.default_rng(4)
+    z = [rng.uniform(-1, 1, (3, g.slot_count)) for _ in range(3)]
+    for eng in (g, o):
+        k = _keys(eng)
+        a, b, c = (eng.encrypt(z[0], k["pk"], level=5), eng.encrypt(z[1][:1], k["pk"], level=4),
+                   eng.encrypt(z[2], k["pk"], level=6))
+        res.append([eng.multiply_fma(a, b, k["rlk"], alpha=2, c=c, gamma=-1.0, beta=-1.0),
+                    eng.multiply_fma(a, a, k["rlk"], alpha=2, beta=-1.0),
+                    eng.lincomb([a, b, c], [0.5, -0.25j, 3.0])]
+                   + eng.lincomb_many([a, b, c], [[1.0, 2.0, -1.0], [0.25, 0.0, 1j]]))
+    for cg, co in zip(*res):
+        _same(g, o, cg, co)

@@ -170,3 +170,46 @@ def test_poly2_int_semantics(env):
         np.testing.assert_allclose(e.decrypt(outs[t], sk), want, atol=1e-4)
     with pytest.raises(RuntimeError, match="exceeds 512"):
         e.poly2_int(xb, yb, np.full((1, 4, 5), 300), 64, rlk)
+
+
+def test_rotate_hoisted_oracle(oracle_lib):
+    """Hoisted rotations (shared ModUp; DESIGN.md 3.16 / include/aesfhe.h) = np.roll, batched,
+    and agree with the ordinary rotation up to key-switch noise."""
+    e = Engine(log_n=10, max_level=6, special_primes=4, seed=3, _lib=oracle_lib)
+    sk = e.create_secret_key(1)
+    pk = e.create_public_key(sk)
+    rng = np.random.default_rng(0)
+    x = rng.uniform(-1, 1, (2, e.slot_count)) + 1j * rng.uniform(-1, 1, (2, e.slot_count))
+    c = e.encrypt(x, pk, level=5)
+    ds = (1, 5, -7, 100)
+    outs = e.rotate_hoisted(c, [e.create_hoisted_rotation_key(sk, d) for d in ds])
+    for d, o in zip(ds, outs):
+        assert o.level == 5
+        np.testing.assert_allclose(e.decrypt(o, sk), np.roll(x, d, axis=1), atol=1e-6)
+        ref = e.rotate(c, e.create_fixed_rotation_key(sk, d))
+        np.testing.assert_allclose(e.decrypt(o, sk), e.decrypt(ref, sk), atol=1e-6)
+    with pytest.raises(RuntimeError):
+        e.rotate_hoisted(c, [e.create_fixed_rotation_key(sk, 1)])
+
+
+def test_mul_fma_and_mixed_level_lincomb_oracle(oracle_lib):
+    """aesfhe_mul_fma = alpha a b + gamma c + beta (one relinearise + rescale, c truncated with
+    its scale compensated) and lincomb over inputs at different levels (truncation, no
+    level-down): values within CKKS noise of the plaintext formulas."""
+    e = Engine(log_n=10, max_level=8, special_primes=4, seed=3, _lib=oracle_lib)
+    sk = e.create_secret_key(1)
+    pk = e.create_public_key(sk)
+    rlk = e.create_relinearization_key(sk)
+    rng = np.random.default_rng(0)
+    x, y, z = [rng.uniform(-1, 1, (2, e.slot_count)) for _ in range(3)]
+    a, b, c = (e.encrypt(x, pk, level=6), e.encrypt(y, pk, level=5), e.encrypt(z, pk, level=7))
+    o = e.multiply_fma(a, b, rlk, alpha=2, c=c, gamma=-1.0, beta=-1.0)
+    assert o.level == 4
+    np.testing.assert_allclose(e.decrypt(o, sk), 2 * x * y - z - 1, atol=1e-6)
+    o = e.multiply_fma(a, a, rlk, alpha=-3, beta=0.5)
+    np.testing.assert_allclose(e.decrypt(o, sk), -3 * x * x + 0.5, atol=1e-6)
+    with pytest.raises(RuntimeError):
+        e.multiply_fma(a, a, rlk, c=b)  # addend below the product level
+    li = e.lincomb([a, b, c], [0.5, -0.25j, 3.0])
+    assert li.level == 4
+    np.testing.assert_allclose(e.decrypt(li, sk), 0.5 * x - 0.25j * y + 3 * z, atol=1e-6)
