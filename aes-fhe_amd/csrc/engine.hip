@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -155,6 +156,10 @@ struct ProfRec {
 };
 
 struct aesfhe_engine {
+    // one reference for the engine handle plus one per live ct / pt / key: the tables, pool and
+    // stream outlive aesfhe_engine_destroy until the last object is freed (Python's cycle
+    // collector finalises an engine and its ciphertexts in arbitrary order)
+    std::atomic<int> refs{1};
     int logN, N, L, K, dnum, np, Lp1;
     int device;
     u64 seed;
@@ -309,6 +314,7 @@ struct Tmp {  // RAII temporary device buffer from the pool
 static aesfhe_ct* ct_new(aesfhe_engine* e, int B, int np, int level) {
     auto* c = new aesfhe_ct;
     c->eng = e;
+    e->refs++;
     c->B = B;
     c->np = np;
     c->level = level;
@@ -713,8 +719,14 @@ extern "C" int aesfhe_chain(const aesfhe_params* pp, uint64_t* primes, double* s
     API_END
 }
 
+static void engine_teardown(aesfhe_engine* e);
+static void engine_unref(aesfhe_engine* e) {
+    if (--e->refs == 0) engine_teardown(e);
+}
 extern "C" void aesfhe_engine_destroy(aesfhe_engine* e) {
-    if (!e) return;
+    if (e) engine_unref(e);
+}
+static void engine_teardown(aesfhe_engine* e) {
     hipSetDevice(e->device);
     hipStreamSynchronize(e->stream);
     for (auto& r : e->recs) {
@@ -842,8 +854,10 @@ extern "C" int aesfhe_decode(int32_t logN, const int64_t* co, double scale, doub
 // keys
 extern "C" void aesfhe_key_free(aesfhe_key* k) {
     if (!k) return;
-    k->eng->pool.put(k->d, k->bytes);
+    aesfhe_engine* e = k->eng;
+    e->pool.put(k->d, k->bytes);
     delete k;
+    engine_unref(e);
 }
 extern "C" int aesfhe_key_info(const aesfhe_key* k, int32_t* kind, uint64_t* g) {
     *kind = k->kind;
@@ -862,6 +876,7 @@ extern "C" uint64_t aesfhe_galois_elt(int32_t logN, int64_t rot, int32_t conj) {
 static aesfhe_key* key_new(aesfhe_engine* e, int kind, size_t words) {
     auto* k = new aesfhe_key;
     k->eng = e;
+    e->refs++;
     k->kind = kind;
     k->galois = 0;
     k->keyseed = 0;
@@ -1013,8 +1028,10 @@ extern "C" int aesfhe_key_switch(aesfhe_engine* e, const aesfhe_key* sk_from, co
 // ciphertext management
 extern "C" void aesfhe_ct_free(aesfhe_ct* c) {
     if (!c) return;
-    c->eng->pool.put(c->d, c->bytes);
+    aesfhe_engine* e = c->eng;
+    e->pool.put(c->d, c->bytes);
     delete c;
+    engine_unref(e);
 }
 extern "C" int aesfhe_ct_info(const aesfhe_ct* c, int32_t info[4]) {
     info[0] = c->B;
@@ -1090,6 +1107,7 @@ extern "C" int aesfhe_pt_create(aesfhe_engine* e, const int64_t* co, int32_t lev
     const int N = e->N, nl = level + 1;
     auto* p = new aesfhe_pt;
     p->eng = e;
+    e->refs++;
     p->level = level;
     p->bytes = (size_t)nl * N * 8;
     p->d = (u64*)e->pool.get(p->bytes);
@@ -1105,8 +1123,10 @@ extern "C" int aesfhe_pt_create(aesfhe_engine* e, const int64_t* co, int32_t lev
 }
 extern "C" void aesfhe_pt_free(aesfhe_pt* p) {
     if (!p) return;
-    p->eng->pool.put(p->d, p->bytes);
+    aesfhe_engine* e = p->eng;
+    e->pool.put(p->d, p->bytes);
     delete p;
+    engine_unref(e);
 }
 
 // -----------------------------------------------------------------------------------------------
