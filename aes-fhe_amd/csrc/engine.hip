@@ -24,6 +24,7 @@
 #include "kernels_ops.h"
 #include "ntt256.h"
 #include "ntt256f.h"
+#include "ks_fused.h"
 
 using namespace aesfhe;
 
@@ -1529,7 +1530,9 @@ static int ks_beta(const aesfhe_engine* e, int l) {
 // Key switch, first half (ModUp): ext[j][b] = the NTT-domain extension of digit j of d to every
 // limb of Q_l u P outside the digit (the digit's own limbs are read from d by the inner product).
 // ext holds ks_beta(l) * B * (l+1+K) limbs.  Shared by every key in aesfhe_rotate_hoisted.
-static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64* ext) {
+// cols_only (fused_ntt engines): the extension limbs get only the NTT column pass; the row pass
+// runs inside k_nttf_rows_ks together with the inner product (ks_fused.h).
+static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64* ext, bool cols_only = false) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long lN = (long)(l + 1) * N, neN = (long)ne * N;
     const int beta = ks_beta(e, l);
@@ -1549,22 +1552,25 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
                                e->np, e->q, e->qinv, e->Lp1, e->logN);
         }
         HIPC(hipGetLastError());
-        if (lo > 0) {
-            Span s1 = span_s(exj, neN, lo, lo, 0, e->Lp1);
-            ntt(e, s1, s1, B * lo, false);
-        }
+        auto fwd = [&](Span sp, int total) {
+            if (!cols_only) return ntt(e, sp, sp, total, false);
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+            hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, sp, sp, e->tabs());
+        };
+        if (lo > 0) fwd(span_s(exj, neN, lo, lo, 0, e->Lp1), B * lo);
         {
             int nrest = ne - hi, nq_rest = (l + 1) - hi;
-            Span s2 = span_s(exj + (long)hi * N, neN, nrest, nq_rest, hi, e->Lp1);
-            ntt(e, s2, s2, B * nrest, false);
+            fwd(span_s(exj + (long)hi * N, neN, nrest, nq_rest, hi, e->Lp1), B * nrest);
         }
     }
 }
 
 // Key switch, second half: inner product of ext (ks_modup of d) with key k, ModDown (fused with
 // r rescales) and the finish into o (+ addend).
+// ext_cols: ext holds column-pass intermediates (ks_modup cols_only): the inner product runs in
+// the fused row pass k_nttf_rows_ks.
 static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, int B, int l,
-                     const aesfhe_key* k, Opnd addend, aesfhe_ct* o, int r) {
+                     const aesfhe_key* k, Opnd addend, aesfhe_ct* o, int r, bool ext_cols = false) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long neN = (long)ne * N;
     const int beta = ks_beta(e, l);
@@ -1573,7 +1579,14 @@ static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, i
     const long kN = (long)(lk + 1) * N;
     Tmp acc(e, (size_t)B * 2 * neN);
     // 3. inner product with every key digit in one pass
-    {
+    if (ext_cols) {
+        // row pass of every extension limb (credited half an NTT per limb: 8 N B) + the inner product
+        // (key read once per call, accumulators written; ext never leaves the chip)
+        const int nown = std::min(l + 1, beta * K);
+        ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown) + (double)ne * (2.0 * beta + 2.0 * B)));
+        const int blocks = 8 * B * (ne * 16 / 8);
+        hipLaunchKernelGGL(k_nttf_rows_ks, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, r ? (const double*)e->pmodf : (const double*)nullptr);
+    } else {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B));
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
         hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, addend, r ? (const double*)e->pmodf : (const double*)nullptr, e->logN);
@@ -1622,12 +1635,14 @@ static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, i
     HIPC(hipGetLastError());
 }
 
+static bool g_no_ks_fuse = getenv("AESFHE_NO_KS_FUSE") != nullptr;  // A/B: unfused inner product
 static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, const aesfhe_key* k,
                       Opnd addend, aesfhe_ct* o, int r = 0) {
     const long neN = (long)(l + 1 + e->K) * e->N;
     Tmp ext(e, (size_t)ks_beta(e, l) * B * neN);
-    ks_modup(e, d, dbs, B, l, ext.p);
-    ks_apply(e, d, dbs, ext.p, B, l, k, addend, o, r);
+    const bool fuse = fused_ntt(e) && !g_no_ks_fuse;
+    ks_modup(e, d, dbs, B, l, ext.p, fuse);
+    ks_apply(e, d, dbs, ext.p, B, l, k, addend, o, r, fuse);
 }
 
 static aesfhe_ct* relin_ct(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_key* rlk) {

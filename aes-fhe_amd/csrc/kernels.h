@@ -76,12 +76,13 @@ __device__ __forceinline__ double fred(double x, double q, double qinv) {
     const double qh = __builtin_rint(x * qinv);
     return __builtin_fma(-qh, q, x);
 }
-// canonical residue in [0, q) of |x| < 2^53, as u64
+// canonical residue in [0, q) of |x| < 2^53, as u64: fred lands in [-q/2 - 1, q/2 + 1], so one
+// conditional +q suffices; the exact integer r < 2^52 is converted by the 2^52 magic number
+// (one add + the mantissa bits) instead of the multi-instruction f64 -> u64 conversion.
 __device__ __forceinline__ u64 fcanon(double x, double q, double qinv) {
     double r = fred(x, q, qinv);
     r = r < 0.0 ? r + q : r;
-    r = r >= q ? r - q : r;
-    return (u64)r;
+    return (u64)__double_as_longlong(r + 4503599627370496.0) & 0xFFFFFFFFFFFFFULL;
 }
 // w from its table entry wq = w/q (w < q < 2^52): rint(wq * q) is exact, |wq*q - w| < 2^-4
 __device__ __forceinline__ double tw_w(double wq, double q) {

@@ -13,6 +13,10 @@
 //   inverse GS   x' = x + y doubles per stage, y' = (x - y) w in (-q, q): primes < 2^42 reach
 //                at most 2^8 q per pass (the column pass starts folded); for larger primes the
 //                sum output is folded in every butterfly (inputs <= q, differences <= 2q).
+// Twiddles come from the per-prime table (cache-resident; the row passes walk N entries per
+// limb).  Generating them as psi^{brv(256 ml + j)} * psi^{brv(row << s)} (brv is additive over
+// disjoint bit fields) halves the table traffic but costs one modular product per twiddle --
+// +26 % VALU on a pass that is VALU-bound as much as HBM-bound: measured slower, dropped.
 // The branch on the prime size is block-uniform (one prime per block).  Between the two passes
 // of a transform the intermediate is stored as raw doubles; final outputs are canonical u64
 // residues in [0, q), so results are identical to ntt256.h and to the oracle residue for residue.
@@ -109,6 +113,58 @@ struct RowFin {
     int nl;
 };
 
+// The forward row pass's 8 stages on the 16 rows of one workgroup: lane (b, rl) loads row
+// row = r0 + rl from rp (raw doubles, stride-16 gather), 4 stages in registers, LDS transpose
+// through sr = s + rl * 16 * kPadF, 4 stages.  On return lane ap = b holds elements
+// ap * 16 + bb (bb = 0..15) of its row, lazily reduced (ranges: file header).
+__device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, double* sr, int b, int row,
+                                            const double* W, double q, double qi, bool big) {
+#pragma unroll
+    for (int a = 0; a < 16; a++) x[a] = ld_d(&rp[a * 16 + b]);
+#pragma unroll
+    for (int st = 0; st < 4; st++) {
+        const int ml = 1 << st, h = 8 >> st;
+        if (big && (st & 1) == 0) {
+#pragma unroll
+            for (int a = 0; a < 16; a++) x[a] = fred(x[a], q, qi);
+        }
+        const int base = ml * (256 + row);  // twiddle psi^{brv(256 ml + ml row + j)}
+#pragma unroll
+        for (int j = 0; j < ml; j++) {  // butterflies of twiddle j: a = j * 2h + k, k < h
+            const double wq = W[base + j];
+#pragma unroll
+            for (int k = 0; k < h; k++) ct_f(x[j * 2 * h + k], x[j * 2 * h + k + h], wq, q);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 16; a++) sr[a * kPadF + b] = x[a];
+    __syncthreads();
+    const int ap = b;
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) x[bb] = sr[ap * kPadF + bb];
+#pragma unroll
+    for (int st = 4; st < 8; st++) {
+        const int ml = 1 << st, h = 128 >> st, nj = ml >> 4;
+        if (big && (st & 1) == 0) {
+#pragma unroll
+            for (int bb = 0; bb < 16; bb++) x[bb] = fred(x[bb], q, qi);
+        }
+        const int base = ml * (256 + row) + ap * nj;
+#pragma unroll
+        for (int j = 0; j < nj; j++) {  // bb = j * 2h + k, k < h
+            const double wq = W[base + j];
+#pragma unroll
+            for (int k = 0; k < h; k++) ct_f(x[j * 2 * h + k], x[j * 2 * h + k + h], wq, q);
+        }
+    }
+}
+// element e = k * 256 + tid (k = 0..15) of the workgroup's 16 x 256 tile, as stored by lane
+// (ap, rl) at sr[ap * kPadF + bb]: the coalesced read-out order of the row passes
+__device__ __forceinline__ int row_tile_idx(int e) {
+    const int r = e >> 8, cc = e & 255;
+    return r * 16 * kPadF + (cc >> 4) * kPadF + (cc & 15);
+}
+
 // Forward, row pass: stages m = 256..32768 within rows of 256 contiguous elements; raw doubles
 // in, canonical u64 out (FIN: the ModDown finish above).  Workgroup = 16 rows [r0, r0+16);
 // lane (b, rl) = (tid & 15, tid >> 4).
@@ -122,45 +178,10 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* W = T.psif + ((long)pid << T.logN);
-    u64* rp = io + (long)row * 256;
     double x[16];
-#pragma unroll
-    for (int a = 0; a < 16; a++) x[a] = ld_d(&rp[a * 16 + b]);
-#pragma unroll
-    for (int st = 0; st < 4; st++) {
-        const int ml = 1 << st, h = 8 >> st;
-        const int base = ml * (256 + row);
-        if (big && (st & 1) == 0) {
-#pragma unroll
-            for (int a = 0; a < 16; a++) x[a] = fred(x[a], q, qi);
-        }
-#pragma unroll
-        for (int a = 0; a < 16; a++) {
-            if (a & h) continue;
-            ct_f(x[a], x[a + h], W[base + (a >> (4 - st))], q);
-        }
-    }
     double* sr = s + rl * 16 * kPadF;
-#pragma unroll
-    for (int a = 0; a < 16; a++) sr[a * kPadF + b] = x[a];
-    __syncthreads();
     const int ap = b;
-#pragma unroll
-    for (int bb = 0; bb < 16; bb++) x[bb] = sr[ap * kPadF + bb];
-#pragma unroll
-    for (int st = 4; st < 8; st++) {
-        const int ml = 1 << st, h = 128 >> st;
-        const int base = ml * (256 + row) + ap * (ml >> 4);
-        if (big && (st & 1) == 0) {
-#pragma unroll
-            for (int bb = 0; bb < 16; bb++) x[bb] = fred(x[bb], q, qi);
-        }
-#pragma unroll
-        for (int bb = 0; bb < 16; bb++) {
-            if (bb & h) continue;
-            ct_f(x[bb], x[bb + h], W[base + (bb >> (8 - st))], q);
-        }
-    }
+    row_ntt_fwd(x, io + (long)row * 256, sr, b, row, W, q, qi, big);
     // coalesced store through LDS: canonical residues, then row-major copy-out
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) sr[ap * kPadF + bb] = __longlong_as_double((long long)fcanon(x[bb], q, qi));
@@ -170,7 +191,7 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
-            base[e] = (u64)__double_as_longlong(s[r * 16 * kPadF + (cc >> 4) * kPadF + (cc & 15)]);
+            base[e] = (u64)__double_as_longlong(s[row_tile_idx(e)]);
         }
     } else {
         const int y = blockIdx.y, p = y / fin.nl, i = y - p * fin.nl, bb = p >> 1, c = p & 1;
@@ -192,7 +213,7 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
 
 // Inverse, row pass (Gentleman-Sande, distances 1..128 within rows): canonical u64 in (src),
 // raw doubles out (dst).
-__global__ __launch_bounds__(256) void k_nttf_inv_rows(Span src, Span dst, Tabs T) {
+__global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Tabs T) {
     __shared__ double s[16 * 16 * kPadF];
     int pid;
     const u64* in = span_ptr(src, blockIdx.y, T.logN, T.Lp1, pid);
@@ -202,7 +223,6 @@ __global__ __launch_bounds__(256) void k_nttf_inv_rows(Span src, Span dst, Tabs 
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* W = T.ipsif + ((long)pid << T.logN);
-    const int N = 1 << T.logN;
     const u64* gb = in + (long)blockIdx.x * 16 * 256;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -215,15 +235,18 @@ __global__ __launch_bounds__(256) void k_nttf_inv_rows(Span src, Span dst, Tabs 
     double x[16];
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) x[bb] = sr[ap * kPadF + bb];
+    const int N = 1 << T.logN;
     auto stages_lo = [&](auto fold) {
 #pragma unroll
         for (int st = 0; st < 4; st++) {
-            const int t = 1 << st;
-            const int base = N / (2 * t) + row * (128 / t) + ap * (8 / t);
+            const int t = 1 << st, nj = 8 / t;
+            const int base = N / (2 * t) + row * (128 / t) + ap * nj;  // psi^{-brv(256 ml + ml row + j)}
 #pragma unroll
-            for (int bb = 0; bb < 16; bb++) {
-                if (bb & t) continue;
-                gs_f<decltype(fold)::value>(x[bb], x[bb + t], W[base + (bb >> (st + 1))], q, qi);
+            for (int j = 0; j < nj; j++) {  // butterflies of twiddle j: bb = j * 2t + k, k < t
+                const double wq = W[base + j];
+#pragma unroll
+                for (int k = 0; k < t; k++)
+                    gs_f<decltype(fold)::value>(x[j * 2 * t + k], x[j * 2 * t + k + t], wq, q, qi);
             }
         }
     };
@@ -237,12 +260,14 @@ __global__ __launch_bounds__(256) void k_nttf_inv_rows(Span src, Span dst, Tabs 
     auto stages_hi = [&](auto fold) {
 #pragma unroll
         for (int st = 4; st < 8; st++) {
-            const int t = 1 << st, ta = t >> 4;
-            const int base = N / (2 * t) + row * (128 / t);
+            const int t = 1 << st, ta = t >> 4, ml = 128 / t;
+            const int base = N / (2 * t) + row * ml;
 #pragma unroll
-            for (int a = 0; a < 16; a++) {
-                if (a & ta) continue;
-                gs_f<decltype(fold)::value>(x[a], x[a + ta], W[base + (a >> (st - 3))], q, qi);
+            for (int j = 0; j < ml; j++) {  // a = j * 2ta + k, k < ta
+                const double wq = W[base + j];
+#pragma unroll
+                for (int k = 0; k < ta; k++)
+                    gs_f<decltype(fold)::value>(x[j * 2 * ta + k], x[j * 2 * ta + k + ta], wq, q, qi);
             }
         }
     };
@@ -311,5 +336,6 @@ __global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T) {
         io[(a * 16 + b) * 256 + c] = fcanon(fmul_rem(r, ni, nif, q), q, qi);
     }
 }
+
 
 }  // namespace aesfhe

@@ -36,8 +36,9 @@ def _same(g, o, cg, co):
         raise AssertionError(f"{len(bad)} residues differ; first at {bad[0].tolist()}")
 
 
-@pytest.mark.parametrize("log_n", [10, 12, 14, 16])
-def test_ntt_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
+@pytest.mark.parametrize("log_n,extreme", [(10, False), (12, False), (14, False), (16, False),
+                                           (16, True), (17, True)])
+def test_ntt_bit_exact(product_lib, oracle_lib, gpu_available, log_n, extreme):
     kw = dict(log_n=log_n, max_level=4, special_primes=2, seed=1)
     g, o = _pair(product_lib, oracle_lib, **kw)
     import ctypes as C
@@ -45,6 +46,10 @@ def test_ntt_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
     npr = len(g.primes)
     rng = np.random.default_rng(log_n)
     limbs = np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in g.primes])
+    if extreme:  # the range bounds of the lazy butterflies: runs of q - 1 and 0
+        for r, q in enumerate(g.primes):
+            limbs[r, : n // 2] = q - 1
+            limbs[r, n // 2 :: 3] = 0
     pids = np.arange(npr, dtype=np.int32)
     for inverse in (0, 1):
         out = []
