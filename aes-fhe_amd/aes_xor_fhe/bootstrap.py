@@ -104,7 +104,8 @@ def _bsgs_plan(offsets: List[int], n: int):
 # ---- the bootstrapper --------------------------------------------------------------------------
 class Bootstrapper:
     def __init__(self, engine: Engine, sk, rlk, cjk=None, *, hw: int = 32, K: float = 12.0,
-                 r: int = 3, deg: int = 31, groups: int = 3, seed: int = 7):
+                 r: int = 3, deg: int = 31, groups: int = 3, seed: int = 7,
+                 bits_deg: int = 31, bits_r: int = 3):
         e = self.e = engine
         self.rlk = rlk
         self.cjk = cjk if cjk is not None else e.create_conjugation_key(sk)
@@ -112,6 +113,7 @@ class Bootstrapper:
         self.n = self.N // 2
         self.L = e.max_level
         self.r, self.deg, self.B = r, deg, K + 1.0
+        self.bits_deg, self.bits_r = bits_deg, bits_r
         # sparse-secret encapsulation keys
         s_sparse = e.create_sparse_secret_key(hw, seed)
         self.to_sparse = e.create_switching_key(sk, s_sparse)
@@ -146,13 +148,22 @@ class Bootstrapper:
             giants.update((g * k2 * u) % n for k2 in plan["giants"] if (g * k2 * u) % n)
         self.hrot = {d: e.create_hoisted_rotation_key(sk, -d) for d in sorted(babies)}
         self.rot = {d: e.create_fixed_rotation_key(sk, -d) for d in sorted(giants)}
-        # EvalMod: Chebyshev coefficients of cos(2 pi (Bnd x - 1/4) / 2^r) on [-1, 1]
+        # EvalMod: Chebyshev coefficients of cos(2 pi (Bnd x - 1/4) / 2^r) on [-1, 1], degree 31
+        # and r = 3 (fit error 1.6e-13) in both modes.  A cheaper bit-mode fit (degree 15, r = 4:
+        # same depth, 11 products instead of 14) leaves a sin error of 5.4e-5 that is the SAME
+        # for every bit of a value, so it adds coherently through the S-box's Walsh polynomial
+        # and the MixColumns products: full AES-128 failed at N = 2^10 with it (random noise of
+        # 2e-4 does not), hence the bits_deg / bits_r knobs default to the general fit.
+        self.cheb = self._cheb_fit(deg, r)
+        self.cheb_bits = self._cheb_fit(bits_deg, bits_r)
+        self.depth = 1 + 2 * groups + math.ceil(math.log2(deg + 1)) + 1 + r
+        self.bits_level = self.L - (1 + groups + math.ceil(math.log2(bits_deg + 1)) + 1 + bits_r)
+
+    def _cheb_fit(self, deg: int, r: int) -> np.ndarray:
         kk = np.arange(deg + 1)
         xs = np.cos(np.pi * (kk + 0.5) / (deg + 1))
         f = np.cos(2 * np.pi * (self.B * xs - 0.25) / (1 << r))
-        self.cheb = np.polynomial.chebyshev.chebfit(xs, f, deg)
-        self.depth = 1 + 2 * groups + math.ceil(math.log2(deg + 1)) + 1 + r
-        self.bits_level = self.L - (1 + groups + math.ceil(math.log2(deg + 1)) + 1 + r)
+        return np.polynomial.chebyshev.chebfit(xs, f, deg)
 
     def _prepare(self, M: Dict[int, np.ndarray]):
         u, ks, g = _bsgs_plan(list(M), self.n)
@@ -186,7 +197,7 @@ class Bootstrapper:
             out = part if out is None else e.add(out, part)
         return out
 
-    def chebyshev(self, x: Ciphertext) -> Ciphertext:
+    def chebyshev(self, x: Ciphertext, coeffs: np.ndarray | None = None) -> Ciphertext:
         """sum_k c_k T_k(x) by recursive Chebyshev division (baby steps T_1..T_b, giants
         T_2b, T_4b, ...): for d >= g (g the largest giant <= d),
         p = q T_g + r with T_{g+j} = 2 T_g T_j - T_{g-j}, so q_0 = c_g, q_j = 2 c_{g+j},
@@ -194,6 +205,8 @@ class Bootstrapper:
         b = 8: 11 ciphertext products (T_2..T_8, T_16, three splits) instead of 30, same depth
         ceil(log2(deg + 1)) + 1."""
         e = self.e
+        cheb = self.cheb if coeffs is None else coeffs
+        deg = len(cheb) - 1
         T = {1: x}
 
         def tk(k):
@@ -209,7 +222,7 @@ class Bootstrapper:
                     T[k] = e.multiply_fma(tk(a), tk(b), self.rlk, alpha=2, c=tk(a - b), gamma=-1.0)
             return T[k]
 
-        baby = 1 << max(1, (self.deg + 1).bit_length() // 2)  # 8 for deg 31
+        baby = 1 << max(1, (deg + 1).bit_length() // 2)  # 8 for deg 31, 4 for deg 15
 
         def ev(c):
             d = len(c) - 1
@@ -239,14 +252,14 @@ class Bootstrapper:
             prod = e.multiply(qt, tk(g), self.rlk)
             return (prod if rc is None else e.add(prod, rc)), r0
 
-        out, c0 = ev(list(self.cheb))
+        out, c0 = ev(list(cheb))
         T.clear()  # ev / tk form a closure cycle: release the T_k now, not at the next gc pass
         return e.add(out, c0)
 
-    def evalmod(self, x: Ciphertext) -> Ciphertext:
+    def evalmod(self, x: Ciphertext, bits: bool = False) -> Ciphertext:
         e = self.e
-        c = self.chebyshev(x)
-        for _ in range(self.r):
+        c = self.chebyshev(x, self.cheb_bits if bits else self.cheb)
+        for _ in range(self.bits_r if bits else self.r):
             c = e.multiply_fma(c, c, self.rlk, alpha=2, beta=-1.0)  # cos 2t = 2 cos^2 t - 1
         return c  # sin(2 pi Bnd x)
 
@@ -296,7 +309,7 @@ class Bootstrapper:
             x = self.linear(x, plan)
         x_re, x_im = self._raise_to_slots(x)
         if b is None:
-            return self.evalmod(x_re), None
+            return self.evalmod(x_re, bits=True), None
         nb = x_re.batch
-        ys = self.evalmod(e.concat([x_re, x_im]))  # one batched evaluation for both halves
+        ys = self.evalmod(e.concat([x_re, x_im]), bits=True)  # one batched evaluation for both halves
         return e.slice(ys, 0, nb), e.slice(ys, nb, nb)

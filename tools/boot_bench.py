@@ -71,9 +71,9 @@ def main():
             c, ph[f"cts{i}"] = timed(bs.linear, c, plan)
         (xr, xi), ph["conj"] = timed(lambda v: (lambda cj: (e.add(v, cj), e.multiply_i(e.subtract(v, cj), -1)))(e.conjugate(v, bs.cjk)), c)
         xx, ph["concat"] = timed(lambda p, q: e.concat([p, q]), xr, xi)
-        ch, ph["chebyshev"] = timed(bs.chebyshev, xx)
+        ch, ph["chebyshev"] = timed(bs.chebyshev, xx, bs.cheb_bits)
         y = ch
-        for i in range(bs.r):
+        for i in range(bs.bits_r):
             y, ph[f"double{i}"] = timed(lambda v: (lambda sq: e.add(e.add(sq, sq), -1.0))(e.multiply(v, v, bs.rlk)), y)
         tot = sum(ph.values())
         print(json.dumps({"phases_ms": {k: round(v, 2) for k, v in ph.items()}, "total_ms": round(tot, 1)}), flush=True)
