@@ -81,6 +81,7 @@ SIGNATURES = [
     ("aesfhe_ct_zero", C.c_int, [c_eng_p, C.c_int32, C.c_int32, _P(c_ct_p)]),
     ("aesfhe_ct_free", None, [c_ct_p]),
     ("aesfhe_pt_create", C.c_int, [c_eng_p, _P(C.c_int64), C.c_int32, _P(c_pt_p)]),
+    ("aesfhe_pt_create_ext", C.c_int, [c_eng_p, _P(C.c_int64), C.c_int32, _P(c_pt_p)]),
     ("aesfhe_pt_free", None, [c_pt_p]),
     ("aesfhe_add", C.c_int, [c_eng_p, c_ct_p, c_ct_p, _P(c_ct_p)]),
     ("aesfhe_sub", C.c_int, [c_eng_p, c_ct_p, c_ct_p, _P(c_ct_p)]),
@@ -114,6 +115,9 @@ SIGNATURES = [
     ("aesfhe_mod_raise", C.c_int, [c_eng_p, c_ct_p, C.c_int32, _P(c_ct_p)]),
     ("aesfhe_mul_i", C.c_int, [c_eng_p, c_ct_p, C.c_int32, _P(c_ct_p)]),
     ("aesfhe_dot_pt", C.c_int, [c_eng_p, _P(c_ct_p), _P(c_pt_p), C.c_int32, _P(c_ct_p)]),
+    ("aesfhe_linear_bsgs", C.c_int,
+     [c_eng_p, c_ct_p, C.c_int32, _P(c_key_p), C.c_int32, _P(c_key_p), _P(C.c_int32),
+      _P(C.c_int32), _P(c_pt_p), _P(c_ct_p)]),
     ("aesfhe_ntt_host", C.c_int,
      [c_eng_p, _P(C.c_uint64), C.c_int32, _P(C.c_int32), C.c_int32]),
     ("aesfhe_bench_ntt", C.c_int,

@@ -105,7 +105,7 @@ def _bsgs_plan(offsets: List[int], n: int):
 class Bootstrapper:
     def __init__(self, engine: Engine, sk, rlk, cjk=None, *, hw: int = 32, K: float = 12.0,
                  r: int = 3, deg: int = 31, groups: int = 3, seed: int = 7,
-                 bits_deg: int = 31, bits_r: int = 3):
+                 bits_deg: int = 31, bits_r: int = 3, lazy: bool = True, baby_scale: int = 2):
         e = self.e = engine
         self.rlk = rlk
         self.cjk = cjk if cjk is not None else e.create_conjugation_key(sk)
@@ -114,6 +114,11 @@ class Bootstrapper:
         self.L = e.max_level
         self.r, self.deg, self.B = r, deg, K + 1.0
         self.bits_deg, self.bits_r = bits_deg, bits_r
+        # lazy: linear maps through aesfhe_linear_bsgs (baby rotations kept in Q u P, one ModDown
+        # per giant + one for all giant key switches); baby steps are then cheap, so the BSGS
+        # split takes baby_scale x more of them (fewer giants)
+        self.lazy = lazy
+        self.baby_scale = baby_scale if lazy else 1
         # sparse-secret encapsulation keys
         s_sparse = e.create_sparse_secret_key(hw, seed)
         self.to_sparse = e.create_switching_key(sk, s_sparse)
@@ -167,6 +172,7 @@ class Bootstrapper:
 
     def _prepare(self, M: Dict[int, np.ndarray]):
         u, ks, g = _bsgs_plan(list(M), self.n)
+        g = min(g * self.baby_scale, 1 << max(0, math.ceil(math.log2(max(ks) - min(ks) + 1))))
         giants = sorted({(k - (k % g)) // g for k in ks})
         terms = {}
         for k in ks:
@@ -185,6 +191,16 @@ class Bootstrapper:
     def linear(self, ct: Ciphertext, plan) -> Ciphertext:
         """sum_k D_k * rot(x, k u) as BSGS: the baby rotations of x in one hoisted call."""
         e, u, g = self.e, plan["u"], plan["g"]
+        if self.lazy:
+            terms = plan["terms"]
+            ks = sorted({k1 for tl in terms.values() for k1, _ in tl})
+            idx = {k1: i for i, k1 in enumerate(ks)}
+            bkeys = [None if k1 == 0 else self.hrot[(k1 * u) % self.n] for k1 in ks]
+            giants = sorted(terms)
+            gkeys = [None if (g * k2 * u) % self.n == 0 else self.rot[(g * k2 * u) % self.n]
+                     for k2 in giants]
+            return e.linear_bsgs(ct, bkeys, gkeys, [[(idx[k1], pt) for k1, pt in terms[k2]]
+                                                    for k2 in giants])
         ks = sorted({k1 for tl in plan["terms"].values() for k1, _ in tl if k1})
         baby = {0: ct}
         if ks:

@@ -166,14 +166,16 @@ class Plaintext:
         self.const = complex(values[0]) if values.size else 0j
         self._dev = {}
 
-    def device(self, level: int, scale: float):
-        key = (level, scale)
+    def device(self, level: int, scale: float, ext: bool = False):
+        """Device encoding at (level, scale); ext: over Q_level u P (aesfhe_pt_create_ext)."""
+        key = (level, scale, ext)
         h = self._dev.get(key)
         if h is None:
             eng = self.engine
             co = eng._encode_coeffs(self.values, scale)
             out = C.c_void_p()
-            eng._check(eng._lib.pt_create(eng._h, _as_ptr(co, C.c_int64), level, C.byref(out)))
+            create = eng._lib.pt_create_ext if ext else eng._lib.pt_create
+            eng._check(create(eng._h, _as_ptr(co, C.c_int64), level, C.byref(out)))
             h = _Owned(eng._lib, out.value, eng._lib.pt_free)
             h.engine = eng
             self._dev[key] = h
@@ -528,6 +530,22 @@ class Engine:
         arr = (c_ct_p * n)(*[c._h for c in cts])
         pts = (c_pt_p * n)(*[p.device(lv, s) for p in plains])
         return self._call_ct(self._lib.dot_pt, arr, pts, n)
+
+    def linear_bsgs(self, ct: Ciphertext, baby_keys: Sequence, giant_keys: Sequence,
+                    terms: Sequence[Sequence]) -> Ciphertext:
+        """sum_j rot_{giant_keys[j]}(sum_{(i, pt) in terms[j]} pt * rot_{baby_keys[i]}(ct)), one
+        level (aesfhe_linear_bsgs: hoisted babies, lazy ModDown).  baby_keys: hoisted rotation
+        keys or None (identity); giant_keys: fixed rotation keys or None; terms[j]: (baby index,
+        Plaintext) pairs, encoded at mul_scale(ct.level) over Q u P."""
+        nb, ng = len(baby_keys), len(giant_keys)
+        s = self._lib.engine_mul_scale(self._h, ct.level)
+        bk = (c_key_p * nb)(*[k._h if k is not None else None for k in baby_keys])
+        gk = (c_key_p * ng)(*[k._h if k is not None else None for k in giant_keys])
+        nterm = (C.c_int32 * ng)(*[len(t) for t in terms])
+        flat = [x for t in terms for x in t]
+        tb = (C.c_int32 * len(flat))(*[i for i, _ in flat])
+        pts = (c_pt_p * len(flat))(*[p.device(ct.level, s, ext=True) for _, p in flat])
+        return self._call_ct(self._lib.linear_bsgs, ct._h, nb, bk, ng, gk, nterm, tb, pts)
 
     def lincomb(self, cts: Sequence[Ciphertext], coeffs: Sequence[complex]) -> Ciphertext:
         n = len(cts)

@@ -233,6 +233,7 @@ struct aesfhe_ct {
 struct aesfhe_pt {
     aesfhe_engine* eng;
     int level;
+    int ext = 0;  // 1: limbs 0..level then the K special limbs (aesfhe_pt_create_ext)
     u64* d;
     size_t bytes;
 };
@@ -1122,6 +1123,27 @@ extern "C" int aesfhe_pt_create(aesfhe_engine* e, const int64_t* co, int32_t lev
     *out = p;
     API_END
 }
+extern "C" int aesfhe_pt_create_ext(aesfhe_engine* e, const int64_t* co, int32_t level, aesfhe_pt** out) {
+    API_BEGIN
+    if (level < 0 || level > e->L) throw_err(AESFHE_EARG, "bad plaintext level");
+    const int N = e->N, nl = level + 1, ne = nl + e->K;
+    auto* p = new aesfhe_pt;
+    p->eng = e;
+    e->refs++;
+    p->level = level;
+    p->ext = 1;
+    p->bytes = (size_t)ne * N * 8;
+    p->d = (u64*)e->pool.get(p->bytes);
+    Tmp dco(e, N);
+    HIPC(hipMemcpyAsync(dco.p, co, (size_t)N * 8, hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, nl, 1), dim3(256), 0, e->stream, (const i64*)dco.p, p->d, nl, e->q, e->logN);
+    hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, e->K, 1), dim3(256), 0, e->stream, (const i64*)dco.p, p->d + (long)nl * N, e->K, e->q + e->Lp1, e->logN);
+    Span s = span_s(p->d, 0, ne, nl, 0, e->Lp1);
+    ntt(e, s, s, ne, false);
+    HIPC(hipStreamSynchronize(e->stream));
+    *out = p;
+    API_END
+}
 extern "C" void aesfhe_pt_free(aesfhe_pt* p) {
     if (!p) return;
     aesfhe_engine* e = p->eng;
@@ -1567,34 +1589,45 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
 
 // Key switch, second half: inner product of ext (ks_modup of d) with key k, ModDown (fused with
 // r rescales) and the finish into o (+ addend).
-// ext_cols: ext holds column-pass intermediates (ks_modup cols_only): the inner product runs in
-// the fused row pass k_nttf_rows_ks.
-static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, int B, int l,
-                     const aesfhe_key* k, Opnd addend, aesfhe_ct* o, int r, bool ext_cols = false) {
+// Key switch, second half, part 1: acc[b][c] (layout [B][2][l+1+K][N], NTT domain over Q_l u P)
+// = sum_j ext_j (x) key_j,c; with pmod, P * addend_c joins the Q limbs (np of addend selects
+// which components), so that a later ModDown by P (q_l ...) returns addend + KS.  accum: add into
+// acc instead of overwriting it (the lazy-ModDown sums of aesfhe_linear_bsgs).  ext_cols: ext
+// holds column-pass intermediates (ks_modup cols_only) and the inner product runs in the fused
+// row pass k_nttf_rows_ks.
+static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, int B, int l,
+                         const aesfhe_key* k, Opnd addend, bool pmod, u64* acc, bool ext_cols, bool accum = false) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long neN = (long)ne * N;
     const int beta = ks_beta(e, l);
-    if (r < 0 || r > kMdrMaxR || K + r > kMdrMaxE || l - r < 0) throw_err(AESFHE_EARG, "bad combined rescale depth %d", r);
-    const int lk = l - r;  // output level
-    const long kN = (long)(lk + 1) * N;
-    Tmp acc(e, (size_t)B * 2 * neN);
-    // 3. inner product with every key digit in one pass
+    const double* pm = pmod ? (const double*)e->pmodf : (const double*)nullptr;
     if (ext_cols) {
         // row pass of every extension limb (credited half an NTT per limb: 8 N B) + the inner product
         // (key read once per call, accumulators written; ext never leaves the chip)
         const int nown = std::min(l + 1, beta * K);
-        ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown) + (double)ne * (2.0 * beta + 2.0 * B)));
+        ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))));
         const int blocks = 8 * B * (ne * 16 / 8);
-        hipLaunchKernelGGL(k_nttf_rows_ks, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, r ? (const double*)e->pmodf : (const double*)nullptr);
+        hipLaunchKernelGGL(k_nttf_rows_ks, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum);
     } else {
-        ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B));
+        ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B * (accum ? 2 : 1)));
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
-        hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc.p, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, addend, r ? (const double*)e->pmodf : (const double*)nullptr, e->logN);
+        hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, addend, pm, e->logN, (int)accum);
     }
     HIPC(hipGetLastError());
+}
+
+// Key switch, second half, part 2: ModDown of acc (2 components, layout [B][2][l+1+K][N]; its
+// dropped limbs are overwritten) by D = P q_l ... q_{l-r+1} (fused with r rescales, DESIGN.md
+// 3.12) into o (level l - r) = (acc - conv) D^{-1} + fin_add.
+static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fin_add, aesfhe_ct* o) {
+    const int N = e->N, K = e->K, ne = l + 1 + K;
+    const long neN = (long)ne * N;
+    if (r < 0 || r > kMdrMaxR || K + r > kMdrMaxE || l - r < 0) throw_err(AESFHE_EARG, "bad combined rescale depth %d", r);
+    const int lk = l - r;  // output level
+    const long kN = (long)(lk + 1) * N;
     // 4. ModDown: INTT the dropped limbs (top r Q limbs + the special limbs) of both accumulators
     {
-        Span ssp = span_s(acc.p + (long)(lk + 1) * N, neN, K + r, r, lk + 1, e->Lp1);
+        Span ssp = span_s(acc + (long)(lk + 1) * N, neN, K + r, r, lk + 1, e->Lp1);
         ntt(e, ssp, ssp, B * 2 * (K + r), true);
     }
     const size_t cell = r ? (size_t)(r - 1) * e->Lp1 + l : 0;
@@ -1605,14 +1638,12 @@ static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, i
     Tmp conv(e, (size_t)B * 2 * kN);
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1));
-        hipLaunchKernelGGL(k_moddown, dim3(N / 256, g_bconv_groups, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, l, r, conv.p, 2 * kN, kN, K,
+        hipLaunchKernelGGL(k_moddown, dim3(N / 256, g_bconv_groups, B * 2), dim3(256), 0, e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN, K,
                            invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv,
                            r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN);
     }
     HIPC(hipGetLastError());
     Span sc = span_s(conv.p, kN, lk + 1, lk + 1, 0, e->Lp1);
-    Opnd fin_add = addend;
-    if (r) fin_add.ptr = nullptr;  // already inside the accumulators (times P)
     if (fused_ntt(e)) {
         // conv NTT with the finish in the row pass's epilogue: conv never reaches HBM
         Tabs T = e->tabs();
@@ -1621,7 +1652,7 @@ static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, i
             ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
             hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, sc, sc, T);
         }
-        RowFin f{(const u64*)acc.p, 2 * neN, neN, Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}, o->d,
+        RowFin f{(const u64*)acc, 2 * neN, neN, Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}, o->d,
                  2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf, lk + 1};
         // the row pass (credited half an NTT) plus the finish: acc read, output written (+ addend)
         ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total * (3.0 + (fin_add.ptr ? 1.0 : 0.0)));
@@ -1631,8 +1662,20 @@ static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, i
     }
     ntt(e, sc, sc, B * 2 * (lk + 1), false);
     ProfScope psf(e, FAM_KS, 8.0 * N * (double)B * 2 * (lk + 1) * 4);
-    hipLaunchKernelGGL(k_moddown_finish, dim3(N / 256, lk + 1, B * 2), dim3(256), 0, e->stream, (const u64*)acc.p, 2 * neN, neN, (const u64*)conv.p, 2 * kN, kN, fin_add, out_of(o), e->q, dinv, dinvf, e->logN);
+    hipLaunchKernelGGL(k_moddown_finish, dim3(N / 256, lk + 1, B * 2), dim3(256), 0, e->stream, (const u64*)acc, 2 * neN, neN, (const u64*)conv.p, 2 * kN, kN, fin_add, out_of(o), e->q, dinv, dinvf, e->logN);
     HIPC(hipGetLastError());
+}
+
+
+// Key switch, second half: inner product of ext (ks_modup of d) with key k, ModDown (fused with
+// r rescales) and the finish into o (+ addend).  ext_cols: see ks_inner_acc.
+static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, int B, int l,
+                     const aesfhe_key* k, Opnd addend, aesfhe_ct* o, int r, bool ext_cols = false) {
+    Tmp acc(e, (size_t)B * 2 * (l + 1 + e->K) * e->N);
+    ks_inner_acc(e, d, dbs, ext, B, l, k, addend, r != 0, acc.p, ext_cols);
+    Opnd fin_add = addend;
+    if (r) fin_add.ptr = nullptr;  // already inside the accumulators (times P)
+    moddown_acc(e, acc.p, B, l, r, fin_add, o);
 }
 
 static bool g_no_ks_fuse = getenv("AESFHE_NO_KS_FUSE") != nullptr;  // A/B: unfused inner product
@@ -1847,6 +1890,134 @@ extern "C" int aesfhe_rotate_hoisted(aesfhe_engine* e, const aesfhe_ct* c, const
         for (int i = 0; i < n; i++) aesfhe_ct_free(outs[i]), outs[i] = nullptr;
         throw;
     }
+    API_END
+}
+
+// Baby-step giant-step linear map with lazy ModDown (include/aesfhe.h): babies E_i in Q_l u P,
+// per giant one ModDown fused with the rescale, the giant key switches summed in Q_{l-1} u P and
+// ModDown'd once.  Against aesfhe_rotate_hoisted + aesfhe_dot_pt + aesfhe_galois it saves one
+// ModDown per baby step, one rescale per giant and all but one of the giants' ModDowns.
+extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t nb, const aesfhe_key* const* bkeys,
+                                  int32_t ng, const aesfhe_key* const* gkeys, const int32_t* nterm,
+                                  const int32_t* tbaby, const aesfhe_pt* const* pts, aesfhe_ct** out) {
+    API_BEGIN
+    if (nb < 1 || ng < 1) throw_err(AESFHE_EARG, "linear_bsgs needs baby and giant steps");
+    if (c->np != 2) throw_err(AESFHE_EDEGREE, "Input ciphertext should have 2 polynomials");
+    const int N = e->N, K = e->K, l = c->level, B = c->B, ne = l + 1 + K;
+    if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a linear map");
+    const long neN = (long)ne * N;
+    int tot = 0;
+    for (int j = 0; j < ng; j++) {
+        if (nterm[j] < 1 || nterm[j] > 256) throw_err(AESFHE_EARG, "giant step with %d terms", nterm[j]);
+        if (gkeys[j] && gkeys[j]->kind != 3) throw_err(AESFHE_EARG, "giant steps need galois keys");
+        tot += nterm[j];
+    }
+    for (int i = 0; i < nb; i++)
+        if (bkeys[i] && bkeys[i]->kind != 5) throw_err(AESFHE_EARG, "baby steps need hoisted rotation keys");
+    for (int t = 0; t < tot; t++) {
+        if (tbaby[t] < 0 || tbaby[t] >= nb) throw_err(AESFHE_EARG, "bad baby index");
+        if (!pts[t] || !pts[t]->ext || pts[t]->level != l) throw_err(AESFHE_EARG, "linear_bsgs needs Q u P plaintexts at the input level");
+    }
+    if (c->is_zero) {
+        *out = ct_zero_new(e, B, 2, l - 1);
+        return 0;
+    }
+    View cv = view_of(c);
+    const u64* c1 = c->d + cv.ps;
+    Opnd c0 = opnd(cv, B);
+    c0.np = 1;  // P * c0 joins accumulator 0 only
+    // 1. babies in Q_l u P
+    std::vector<std::unique_ptr<Tmp>> E;
+    bool any_key = false;
+    for (int i = 0; i < nb; i++) any_key |= bkeys[i] != nullptr;
+    {
+        std::unique_ptr<Tmp> ext;
+        if (any_key) {
+            ext.reset(new Tmp(e, (size_t)ks_beta(e, l) * B * neN));
+            ks_modup(e, c1, cv.bs, B, l, ext->p);
+        }
+        for (int i = 0; i < nb; i++) {
+            E.emplace_back(new Tmp(e, (size_t)B * 2 * neN));
+            if (!bkeys[i]) {
+                hipLaunchKernelGGL(k_scale_p_ext, dim3(N / 256, ne, B * 2), dim3(256), 0, e->stream, opnd(cv, B), E.back()->p, l, ne, e->q, e->qinv, (const double*)e->pmodf, e->Lp1, e->logN);
+                HIPC(hipGetLastError());
+                continue;
+            }
+            Tmp acc(e, (size_t)B * 2 * neN);
+            ks_inner_acc(e, c1, cv.bs, ext->p, B, l, bkeys[i], c0, true, acc.p, false);
+            Span src = span_s(acc.p, neN, ne, l + 1, 0, e->Lp1), dst = span_s(E.back()->p, neN, ne, l + 1, 0, e->Lp1);
+            hipLaunchKernelGGL(k_galois, dim3(N / 256, B * 2 * ne), dim3(256), 0, e->stream, src, dst, (u64)bkeys[i]->galois, e->logN, e->Lp1);
+            HIPC(hipGetLastError());
+        }
+    }
+    // 2. giant parts: sum of plaintext products in Q_l u P, ModDown fused with the rescale
+    std::vector<aesfhe_ct*> parts(ng, nullptr);
+    aesfhe_ct* sumq = nullptr;
+    try {
+        int t0 = 0;
+        for (int j = 0; j < ng; j++) {
+            std::vector<const u64*> ep, pp;
+            for (int t = t0; t < t0 + nterm[j]; t++) {
+                ep.push_back(E[tbaby[t]]->p);
+                pp.push_back(pts[t]->d);
+            }
+            t0 += nterm[j];
+            auto dep = upload_small(e, ep.data(), ep.size());
+            auto dpp = upload_small(e, pp.data(), pp.size());
+            Tmp S(e, (size_t)B * 2 * neN);
+            {
+                ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (ep.size() + 1) + ep.size()));
+                hipLaunchKernelGGL(k_dot_pt_ext, dim3(N / 256, ne, B * 2), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64* const*)dpp, (int)ep.size(), S.p, l, ne, e->q, e->qinv, e->Lp1, e->logN);
+            }
+            HIPC(hipGetLastError());
+            parts[j] = ct_new(e, B, 2, l - 1);
+            moddown_acc(e, S.p, B, l, 1, Opnd{nullptr, 0, 0, 0}, parts[j]);
+        }
+        E.clear();
+        // 3. giants: key switches of sigma_j(part_j) summed in Q_{l-1} u P, one ModDown
+        const int l2 = l - 1, ne2 = l2 + 1 + K;
+        const long ne2N = (long)ne2 * N, l2N = (long)(l2 + 1) * N;
+        std::unique_ptr<Tmp> accg;
+        const bool fuse = fused_ntt(e) && !g_no_ks_fuse;
+        for (int j = 0; j < ng; j++) {
+            if (!gkeys[j]) {
+                if (!sumq) {
+                    sumq = parts[j];
+                    parts[j] = nullptr;
+                } else {
+                    aesfhe_ct* s2 = ct_new(e, B, 2, l2);
+                    hipLaunchKernelGGL(k_addsub, ew_grid(e, l2 + 1, B * 2), dim3(256), 0, e->stream, opnd(view_of(sumq), B), opnd(view_of(parts[j]), B), out_of(s2), 2, e->q, 0, e->logN);
+                    HIPC(hipGetLastError());
+                    aesfhe_ct_free(sumq);
+                    sumq = s2;
+                }
+                continue;
+            }
+            Tmp sg(e, (size_t)B * 2 * l2N);
+            Span src = span_s(parts[j]->d, l2N, l2 + 1, l2 + 1, 0, e->Lp1), dst = span_s(sg.p, l2N, l2 + 1, l2 + 1, 0, e->Lp1);
+            hipLaunchKernelGGL(k_galois, dim3(N / 256, B * 2 * (l2 + 1)), dim3(256), 0, e->stream, src, dst, (u64)gkeys[j]->galois, e->logN, e->Lp1);
+            HIPC(hipGetLastError());
+            Opnd s0{sg.p, 2 * l2N, l2N, 1};
+            Tmp ext(e, (size_t)ks_beta(e, l2) * B * ne2N);
+            ks_modup(e, sg.p + l2N, 2 * l2N, B, l2, ext.p, fuse);
+            const bool first = !accg;
+            if (first) accg.reset(new Tmp(e, (size_t)B * 2 * ne2N));
+            ks_inner_acc(e, sg.p + l2N, 2 * l2N, ext.p, B, l2, gkeys[j], s0, true, accg->p, fuse, !first);
+        }
+        if (accg) {
+            aesfhe_ct* r = ct_new(e, B, 2, l2);
+            Opnd add = sumq ? opnd(view_of(sumq), B) : Opnd{nullptr, 0, 0, 0};
+            moddown_acc(e, accg->p, B, l2, 0, add, r);
+            if (sumq) aesfhe_ct_free(sumq);
+            sumq = r;
+        }
+    } catch (...) {
+        for (auto* p : parts) aesfhe_ct_free(p);
+        if (sumq) aesfhe_ct_free(sumq);
+        throw;
+    }
+    for (auto* p : parts) aesfhe_ct_free(p);
+    *out = sumq;
     API_END
 }
 

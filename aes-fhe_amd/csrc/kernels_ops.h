@@ -345,7 +345,7 @@ __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* _
                                long kcomp, u64* __restrict__ acc, long abs_, long acs, int B,
                                int beta, int K, int l, const u64* __restrict__ qall,
                                const double* __restrict__ qinvall, int Lp1, Opnd addend,
-                               const double* __restrict__ pmodf, int logN) {
+                               const double* __restrict__ pmodf, int logN, int accum) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int t = blockIdx.y;
     const int pid = t <= l ? t : Lp1 + (t - l - 1);
@@ -386,6 +386,10 @@ __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* _
             s1 = fred(s1, q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, k, logN)), w, f, q);
         }
         u64* a0 = acc + (long)bb * abs_ + ((long)t << logN) + k;
+        if (accum) {  // the lazy-ModDown sums of aesfhe_linear_bsgs
+            s0 += u2d(a0[0]);
+            s1 += u2d(a0[acs]);
+        }
         a0[0] = fcanon(s0, q, qi);
         a0[acs] = fcanon(s1, q, qi);
     }
@@ -827,6 +831,43 @@ __global__ void k_dot_pt(const u64* const* __restrict__ cp, const long* __restri
         if ((i & 3) == 3) acc = fred(acc, q, qi);
     }
     o.ptr[(long)bb * o.bs + (long)p * o.ps + off] = fcanon(acc, q, qi);
+}
+
+// ---- lazy-ModDown linear transforms (aesfhe_linear_bsgs) over Q_l u P limbs ---------------------
+// limb t of an extended polynomial (t <= l: q_t, else p_{t-l-1}) has prime index ext_pid
+__device__ __forceinline__ int ext_pid(int t, int l, int Lp1) { return t <= l ? t : Lp1 + (t - l - 1); }
+
+// out[b][c][t] = (P mod q_t) * in[b][c][t] on the Q limbs, 0 on the P limbs (P * x in Q_l u P);
+// in: Opnd (level-l ciphertext), out: [B][2][ne][N].  grid (N/256, ne, B*2)
+__global__ void k_scale_p_ext(Opnd in, u64* __restrict__ out, int l, int ne, const u64* __restrict__ qall,
+                              const double* __restrict__ qinvall, const double* __restrict__ pmodf, int Lp1, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.y, bb = blockIdx.z >> 1, c = blockIdx.z & 1;
+    u64 v = 0;
+    if (t <= l) {
+        const double q = (double)qall[t], qi = qinvall[t], f = pmodf[t];
+        v = fcanon(fmul_rem(u2d(opnd_get(in, bb, c, t, k, logN)), tw_w(f, q), f, q), q, qi);
+    }
+    out[((((long)bb * 2 + c) * ne + t) << logN) + k] = v;
+}
+
+// out[b][c][t] = sum_i pt_i[t] * E_i[b][c][t] over the ne limbs of Q_l u P (E_i, out: [B][2][ne][N];
+// pt_i: ne limbs).  grid (N/256, ne, B*2)
+__global__ void k_dot_pt_ext(const u64* const* __restrict__ ep, const u64* const* __restrict__ pp, int n,
+                             u64* __restrict__ out, int l, int ne, const u64* __restrict__ qall,
+                             const double* __restrict__ qinvall, int Lp1, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.y, bb = blockIdx.z >> 1, c = blockIdx.z & 1;
+    const int pid = ext_pid(t, l, Lp1);
+    const double q = (double)qall[pid], qi = qinvall[pid];
+    const long off = ((((long)bb * 2 + c) * ne + t) << logN) + k, po = ((long)t << logN) + k;
+    double acc = 0.0;
+    for (int i = 0; i < n; i++) {
+        const double w = u2d(pp[i][po]);
+        acc += fmul_rem(u2d(ep[i][off]), w, w * qi, q);
+        if ((i & 3) == 3) acc = fred(acc, q, qi);
+    }
+    out[off] = fcanon(acc, q, qi);
 }
 
 }  // namespace aesfhe

@@ -6,8 +6,8 @@
 // switch.  Here ks_modup stops after the column pass (the raw-double intermediate stays in the
 // ext buffer) and one workgroup per (target limb t, 16-row block, batch element b) runs the row
 // pass of ext[j][b][t] for every digit j in registers, multiplies by the key digit and
-// accumulates, writing only the two accumulators acc[b][0/1][t] -- the same canonical values
-// k_ks_inner_all produces (the arithmetic is exact mod q; only the lazy ranges differ).
+// accumulates, writing only the two accumulators acc[b][0/1][t] (accum: added to what acc holds)
+// -- the same canonical values k_ks_inner_all produces (the arithmetic is exact mod q; only the lazy ranges differ).
 //
 // Ranges: row_ntt_fwd leaves |x| <= 17q for q < 2^42 (folded to q/2 + 1 for larger primes
 // before the product); fmul_rem(x, key) lies in (-1.5q, 1.5q) (on-the-fly key quotient), so the
@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void k_nttf_rows_ks(const u64* __restrict__ d,
                                                       const u64* __restrict__ key, long kdig, long kcomp,
                                                       u64* __restrict__ acc, long abs_, long acs, int B,
                                                       int beta, int K, int l, int ne, Tabs T, Opnd addend,
-                                                      const double* __restrict__ pmodf) {
+                                                      const double* __restrict__ pmodf, int accum) {
     __shared__ double s[16 * 16 * kPadF];
     const int id = blockIdx.x, x8 = id & 7, rest = id >> 3;
     const int bb = rest % B, pair = (rest / B) * 8 + x8;
@@ -92,8 +92,9 @@ __global__ __launch_bounds__(256) void k_nttf_rows_ks(const u64* __restrict__ d,
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const int e = k * 256 + tid;
-        o0[e] = fcanon(a0[k], q, qi);
-        o0[acs + e] = fcanon(a1[k], q, qi);
+        const double p0 = accum ? u2d(o0[e]) : 0.0, p1 = accum ? u2d(o0[acs + e]) : 0.0;
+        o0[e] = fcanon(a0[k] + p0, q, qi);
+        o0[acs + e] = fcanon(a1[k] + p1, q, qi);
     }
 }
 

@@ -180,6 +180,9 @@ void aesfhe_ct_free(aesfhe_ct *ct);
 /* plaintext from N integer coefficients, materialised at `level` (NTT residues) */
 int aesfhe_pt_create(aesfhe_engine *eng, const int64_t *coeffs, int32_t level,
                      aesfhe_pt **out);
+/* the same over Q_level u P (level + 1 + K limbs): operands of aesfhe_linear_bsgs */
+int aesfhe_pt_create_ext(aesfhe_engine *eng, const int64_t *coeffs, int32_t level,
+                         aesfhe_pt **out);
 void aesfhe_pt_free(aesfhe_pt *pt);
 
 /* ---- arithmetic ------------------------------------------------------------------------- */
@@ -274,6 +277,21 @@ int aesfhe_mul_i(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t sign, aesfhe_c
  * encoded at mul_scale(l) with >= l+1 limbs): the diagonal sums of homomorphic linear maps. */
 int aesfhe_dot_pt(aesfhe_engine *eng, const aesfhe_ct *const *cts, const aesfhe_pt *const *pts,
                   int32_t n, aesfhe_ct **out);
+
+/* Baby-step giant-step linear map with hoisted baby steps and lazy ModDown (bootstrapping's
+ * CoeffToSlot / SlotToCoeff; no reference counterpart -- desilofhe's bootstrap is internal):
+ *   out = sum_j rho_{gkeys[j]}( sum_{t in terms of j} pts[t] * rho_{bkeys[tbaby[t]]}(ct) )
+ * rho_k = the rotation of key k (bkeys: hoisted keys, kind 5; gkeys: galois keys, kind 3),
+ * rho_NULL = identity.  Terms of giant j are consecutive, nterm[j] of them.  Arithmetic: the
+ * baby rotations stay in Q_l u P (E_i = sigma_i(P c0 + acc0_i, acc1_i), no ModDown), each giant's
+ * term sum S_j = sum pts * E over Q_l u P (pts from aesfhe_pt_create_ext at level l, encoded at
+ * mul_scale(l)) is ModDown'd together with one rescale (D = P q_l) to level l - 1, and the giant
+ * rotations' key switches are summed in Q_{l-1} u P (acc0 += P sigma_j(part_j0)) with ONE final
+ * ModDown by P; parts with a NULL giant key are added after it.  Output level l - 1. */
+int aesfhe_linear_bsgs(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t nb,
+                       const aesfhe_key *const *bkeys, int32_t ng, const aesfhe_key *const *gkeys,
+                       const int32_t *nterm, const int32_t *tbaby, const aesfhe_pt *const *pts,
+                       aesfhe_ct **out);
 
 /* ---- raw kernels (known-answer tests and roofline measurement) ------------------------- */
 /* In-place forward (inverse=0) / inverse NTT of nlimb host limbs; limb i uses prime pids[i]

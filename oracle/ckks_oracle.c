@@ -211,7 +211,8 @@ struct aesfhe_ct {
 
 struct aesfhe_pt {
     int level;
-    u64 *data; /* [level+1][N] */
+    int ext;   /* 1: K special limbs follow (aesfhe_pt_create_ext) */
+    u64 *data; /* [level+1 (+K)][N] */
 };
 
 static double now_ms(void) {
@@ -1041,6 +1042,19 @@ int aesfhe_pt_create(aesfhe_engine *e, const int64_t *co, int32_t level, aesfhe_
     *out = p;
     return 0;
 }
+/* the same over Q_level u P (level+1+K limbs) */
+int aesfhe_pt_create_ext(aesfhe_engine *e, const int64_t *co, int32_t level, aesfhe_pt **out) {
+    if (level < 0 || level > e->L) return fail(AESFHE_EARG, "bad plaintext level");
+    const int nl = level + 1, ne = nl + e->K;
+    aesfhe_pt *p = calloc(1, sizeof *p);
+    p->level = level;
+    p->ext = 1;
+    p->data = malloc(sizeof(u64) * (size_t)ne * e->N);
+#pragma omp parallel for schedule(static)
+    for (int t = 0; t < ne; t++) coeffs_to_ntt(e, co, p->data + (size_t)t * e->N, t < nl ? t : e->L + 1 + (t - nl));
+    *out = p;
+    return 0;
+}
 void aesfhe_pt_free(aesfhe_pt *p) {
     if (!p) return;
     free(p->data);
@@ -1604,6 +1618,146 @@ int aesfhe_rotate_hoisted(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_key
     free(k0);
     free(k1);
     free(t);
+    return 0;
+}
+
+/* P mod q_i for the Q primes */
+static u64 p_mod(const aesfhe_engine *e, int i) {
+    const u64 qi = e->q[i];
+    u64 P = 1;
+    for (int kk = 0; kk < e->K; kk++) P = mul_mod_slow(P, e->q[e->L + 1 + kk] % qi, qi);
+    return P;
+}
+
+/* Baby-step giant-step linear map with lazy ModDown (include/aesfhe.h).  Per batch
+ * element: E_i = sigma_i(P c0 + acc0_i, acc1_i) over Q_l u P (acc_i = ks_acc(c1, bkey_i); NULL
+ * key: E = (P c0, P c1), zero special limbs); S_j = sum_t pts_t * E_{tbaby_t} over Q_l u P;
+ * part_j = moddown_r(S_j, l, 1); giants: G = sum_{j keyed} [ks_acc(sigma_j(part_j1)) with P
+ * sigma_j(part_j0) added to acc0]; out = moddown_r(G, l-1, 0) + sum_{j unkeyed} part_j. */
+int aesfhe_linear_bsgs(aesfhe_engine *e, const aesfhe_ct *c, int32_t nb, const aesfhe_key *const *bkeys,
+                       int32_t ng, const aesfhe_key *const *gkeys, const int32_t *nterm, const int32_t *tbaby,
+                       const aesfhe_pt *const *pts, aesfhe_ct **out) {
+    if (nb < 1 || ng < 1) return fail(AESFHE_EARG, "linear_bsgs needs baby and giant steps");
+    if (c->npoly != 2) return fail(AESFHE_EDEGREE, "Input ciphertext should have 2 polynomials");
+    const int N = e->N, K = e->K, l = c->level, ne = l + 1 + K, nq = e->L + 1;
+    if (l < 1) return fail(AESFHE_ELEVEL, "no level left for a linear map");
+    int tot = 0;
+    for (int j = 0; j < ng; j++) {
+        if (nterm[j] < 1 || nterm[j] > 256) return fail(AESFHE_EARG, "giant step with %d terms", nterm[j]);
+        if (gkeys[j] && gkeys[j]->kind != 3) return fail(AESFHE_EARG, "giant steps need galois keys");
+        tot += nterm[j];
+    }
+    for (int i = 0; i < nb; i++)
+        if (bkeys[i] && bkeys[i]->kind != 5) return fail(AESFHE_EARG, "baby steps need hoisted rotation keys");
+    for (int t = 0; t < tot; t++) {
+        if (tbaby[t] < 0 || tbaby[t] >= nb) return fail(AESFHE_EARG, "bad baby index");
+        if (!pts[t] || !pts[t]->ext || pts[t]->level != l) return fail(AESFHE_EARG, "linear_bsgs needs Q u P plaintexts at the input level");
+    }
+    aesfhe_ct *r = ct_new(e, c->B, 2, l - 1);
+    if (c->is_zero) {
+        r->is_zero = 1;
+        *out = r;
+        return 0;
+    }
+    int pid[MAXP];
+    for (int t = 0; t < ne; t++) pid[t] = t <= l ? t : nq + (t - l - 1);
+    u64 Pm[MAXP];
+    for (int i = 0; i < nq; i++) Pm[i] = p_mod(e, i);
+    const size_t eN = (size_t)2 * ne * N;
+    u64 *E = malloc(sizeof(u64) * eN * nb), *S = malloc(sizeof(u64) * eN);
+    u64 *c1 = malloc(sizeof(u64) * (size_t)(l + 1) * N);
+    const int l2 = l - 1, ne2 = l2 + 1 + K;
+    aesfhe_ct **parts = calloc((size_t)ng, sizeof *parts);
+    for (int j = 0; j < ng; j++) parts[j] = ct_new(e, 1, 2, l2);
+    for (int b = 0; b < c->B; b++) {
+        /* 1. babies */
+        for (int p = 0; p <= l; p++) memcpy(c1 + (size_t)p * N, limb(e, c, b, 1, p), sizeof(u64) * N);
+        for (int i = 0; i < nb; i++) {
+            u64 *Ei = E + eN * i;
+            if (!bkeys[i]) {
+                memset(Ei, 0, sizeof(u64) * eN);
+                for (int cc = 0; cc < 2; cc++)
+                    for (int t = 0; t <= l; t++) {
+                        const u64 *src = limb(e, c, b, cc, t);
+                        u64 *dst = Ei + ((size_t)cc * ne + t) * N;
+                        for (int x = 0; x < N; x++) dst[x] = mul_mod_slow(src[x], Pm[t], e->q[t]);
+                    }
+                continue;
+            }
+            u64 *acc = ks_acc(e, c1, l, bkeys[i]);
+            for (int t = 0; t <= l; t++) {
+                const u64 *c0 = limb(e, c, b, 0, t);
+                u64 *a0 = acc + (size_t)t * N;
+                for (int x = 0; x < N; x++) a0[x] = add_mod(a0[x], mul_mod_slow(c0[x], Pm[t], e->q[t]), e->q[t]);
+            }
+            for (size_t y = 0; y < (size_t)2 * ne; y++) galois_perm(e, acc + y * N, Ei + y * N, bkeys[i]->galois);
+            free(acc);
+        }
+        /* 2. giant parts */
+        int t0 = 0;
+        for (int j = 0; j < ng; j++) {
+            memset(S, 0, sizeof(u64) * eN);
+            for (int t = t0; t < t0 + nterm[j]; t++) {
+                const u64 *Ei = E + eN * tbaby[t];
+#pragma omp parallel for schedule(static)
+                for (int y = 0; y < 2 * ne; y++) {
+                    const int lt = y % ne, p = pid[lt];
+                    const u64 *pv = pts[t]->data + (size_t)lt * N;
+                    for (int x = 0; x < N; x++)
+                        S[(size_t)y * N + x] = add_mod(S[(size_t)y * N + x], mul_mod(Ei[(size_t)y * N + x], pv[x], &e->mont[p]), e->q[p]);
+                }
+            }
+            t0 += nterm[j];
+            moddown_r(e, S, l, 1, limb(e, parts[j], 0, 0, 0), limb(e, parts[j], 0, 1, 0));
+        }
+        /* 3. giants, one ModDown */
+        u64 *G = NULL, *p1 = malloc(sizeof(u64) * (size_t)(l2 + 1) * N), *p0 = malloc(sizeof(u64) * (size_t)(l2 + 1) * N);
+        for (int j = 0; j < ng; j++) {
+            if (!gkeys[j]) continue;
+            for (int t = 0; t <= l2; t++) {
+                galois_perm(e, limb(e, parts[j], 0, 1, t), p1 + (size_t)t * N, gkeys[j]->galois);
+                galois_perm(e, limb(e, parts[j], 0, 0, t), p0 + (size_t)t * N, gkeys[j]->galois);
+            }
+            u64 *acc = ks_acc(e, p1, l2, gkeys[j]);
+            for (int t = 0; t <= l2; t++) {
+                u64 *a0 = acc + (size_t)t * N;
+                for (int x = 0; x < N; x++) a0[x] = add_mod(a0[x], mul_mod_slow(p0[(size_t)t * N + x], Pm[t], e->q[t]), e->q[t]);
+            }
+            if (!G) {
+                G = acc;
+            } else {
+                for (int y = 0; y < 2 * ne2; y++) {
+                    const u64 q = e->q[y % ne2 <= l2 ? y % ne2 : nq + (y % ne2 - l2 - 1)];
+                    for (int x = 0; x < N; x++) G[(size_t)y * N + x] = add_mod(G[(size_t)y * N + x], acc[(size_t)y * N + x], q);
+                }
+                free(acc);
+            }
+        }
+        free(p0);
+        free(p1);
+        u64 *o0 = limb(e, r, b, 0, 0), *o1 = limb(e, r, b, 1, 0);
+        if (G) moddown_r(e, G, l2, 0, o0, o1);
+        else {
+            memset(o0, 0, sizeof(u64) * (size_t)(l2 + 1) * N);
+            memset(o1, 0, sizeof(u64) * (size_t)(l2 + 1) * N);
+        }
+        free(G);
+        for (int j = 0; j < ng; j++) {
+            if (gkeys[j]) continue;
+            for (int cc = 0; cc < 2; cc++)
+                for (int t = 0; t <= l2; t++) {
+                    u64 *o = limb(e, r, b, cc, t);
+                    const u64 *pv = limb(e, parts[j], 0, cc, t);
+                    for (int x = 0; x < N; x++) o[x] = add_mod(o[x], pv[x], e->q[t]);
+                }
+        }
+    }
+    for (int j = 0; j < ng; j++) aesfhe_ct_free(parts[j]);
+    free(parts);
+    free(E);
+    free(S);
+    free(c1);
+    *out = r;
     return 0;
 }
 

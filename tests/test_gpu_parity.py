@@ -217,3 +217,32 @@ def test_mul_fma_and_mixed_lincomb_bit_exact(product_lib, oracle_lib, gpu_availa
                    + eng.lincomb_many([a, b, c], [[1.0, 2.0, -1.0], [0.25, 0.0, 1j]]))
     for cg, co in zip(*res):
         _same(g, o, cg, co)
+
+
+@pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=3, special_primes=2, seed=5)],
+                         ids=["n4096", "n65536"])
+def test_linear_bsgs_bit_exact(product_lib, oracle_lib, gpu_available, kw):
+    """aesfhe_linear_bsgs (hoisted babies and lazy ModDown; at N = 2^16 the giants go through the
+    fused ext-NTT row pass with accumulation) against the oracle's restatement, and its slots
+    against the plain BSGS sum it computes."""
+    g, o = _pair(product_lib, oracle_lib, **kw)
+    n = g.slot_count
+    rng = np.random.default_rng(6)
+    z = rng.uniform(-1, 1, (2, n))
+    diags = [rng.uniform(-1, 1, n) for _ in range(5)]
+    plan = [(0, [(0, 0), (1, 1), (2, 2)]), (-6, [(0, 3)]), (24, [(1, 4), (2, 0)])]  # (giant, [(baby, diag)])
+    babies = [0, 1, -3]
+    outs = []
+    for eng in (g, o):
+        sk = eng.create_secret_key(7)
+        c = eng.encrypt(z, eng.create_public_key(sk), level=kw["max_level"])
+        bk = [None if d == 0 else eng.create_hoisted_rotation_key(sk, -d) for d in babies]
+        gk = [None if d == 0 else eng.create_fixed_rotation_key(sk, -d) for d, _ in plan]
+        pts = [eng.encode(v) for v in diags]
+        terms = [[(b, pts[i]) for b, i in tl] for _, tl in plan]
+        outs.append((eng.linear_bsgs(c, bk, gk, terms), sk))
+    _same(g, o, outs[0][0], outs[1][0])
+    want = sum(np.roll(sum(diags[i] * np.roll(z, -babies[b], axis=1) for b, i in tl), -d, axis=1)
+               for d, tl in plan)
+    assert outs[0][0].level == kw["max_level"] - 1
+    np.testing.assert_allclose(g.decrypt(outs[0][0], outs[0][1]), want, atol=1e-5)

@@ -25,12 +25,14 @@ def main():
     ap.add_argument("--general", action="store_true")
     ap.add_argument("--batch", type=int, default=1, help="ciphertext pairs per call")
     ap.add_argument("--phases", action="store_true", help="also time each bootstrap phase")
+    ap.add_argument("--baby-scale", type=int, default=2, help="BSGS baby steps x this (lazy mode)")
+    ap.add_argument("--eager", action="store_true", help="rotate_hoisted + dot_pt + galois linear maps")
     a = ap.parse_args()
     e = Engine(log_n=a.log_n, max_level=a.max_level, special_primes=8, scale_bits=a.scale_bits, seed=3)
     sk = e.create_secret_key(1)
     pk = e.create_public_key(sk)
     t = time.time()
-    bs = Bootstrapper(e, sk, e.create_relinearization_key(sk))
+    bs = Bootstrapper(e, sk, e.create_relinearization_key(sk), lazy=not a.eager, baby_scale=a.baby_scale)
     e.synchronize()
     setup = time.time() - t
     n = e.slot_count
