@@ -650,6 +650,10 @@ class Engine:
         self._check(self._lib.engine_pool_stats(self._h, a))
         return dict(zip(("held", "live", "mallocs", "trims", "reuse_larger"), [int(x) for x in a]))
 
+    def pool_trim(self):
+        """Release the cached device blocks (aesfhe_engine_pool_trim), e.g. between workloads."""
+        self._check(self._lib.engine_pool_trim(self._h))
+
     def synchronize(self):
         self._check(self._lib.engine_sync(self._h))
 

@@ -82,10 +82,15 @@ extern "C" const char* aesfhe_backend_name(void) { return "hip-gfx950"; }
 struct Pool {
     // Size classes: exact (256 B granularity) up to 1 MiB, then 8 classes per octave (<= 12.5%
     // slack), so ciphertexts of neighbouring levels / batch sizes share blocks.  A failed
-    // hipMalloc first takes a cached block of up to twice the class, then frees cached blocks
-    // from the largest class down until the allocation fits (never the whole cache at once).
+    // hipMalloc first takes a cached block of up to twice the class, then frees the cached blocks
+    // of the least recently used classes (one device sync) until the allocation fits: the sizes
+    // of a finished phase (bootstrapping's Q u P buffers during the rounds, the rounds' during a
+    // refresh) go first, the working set stays cached.  A soft cap (95 % of the device memory
+    // free at engine creation) keeps the device out of failing hipMallocs, which are slow.
     std::map<size_t, std::vector<void*>> free_;
     std::unordered_map<void*, size_t> cls_;  // live block -> its class
+    std::unordered_map<size_t, uint64_t> used_;  // class -> last get/put tick
+    uint64_t tick = 0;
     size_t held = 0, live = 0;
     int64_t mallocs = 0, trims = 0, reuse_larger = 0;
     static size_t size_class(size_t b) {
@@ -100,26 +105,54 @@ struct Pool {
         it->second.pop_back();
         cls_[p] = it->first;
         live += it->first;
+        used_[it->first] = ++tick;
         return p;
+    }
+    size_t cap = 0;  // soft limit on held bytes (0: none); set from the device size at creation
+    // free the cached blocks of the least recently used classes (one device sync) until held +
+    // need <= target or nothing is cached; returns whether anything was freed
+    bool trim_lru(size_t need, size_t target) {
+        std::vector<std::pair<uint64_t, size_t>> order;  // (last use, class) of cached classes
+        for (auto& kv : free_)
+            if (!kv.second.empty()) order.push_back({used_[kv.first], kv.first});
+        if (order.empty()) return false;
+        std::sort(order.begin(), order.end());
+        hipDeviceSynchronize();
+        trims++;
+        for (size_t k = 0; k < order.size() && held + need > target; k++) {
+            auto& v = free_[order[k].second];
+            for (void* q : v) {
+                hipFree(q);
+                held -= order[k].second;
+            }
+            v.clear();
+        }
+        return true;
     }
     void* get(size_t bytes) {
         const size_t c = size_class(bytes);
         auto it = free_.find(c);
         if (it != free_.end() && !it->second.empty()) return take(it);
+        // a cached block of a slightly larger class (<= 25 % waste) before a new allocation: the
+        // sum of per-class peaks otherwise grows far past the peak live set
+        for (auto j = free_.upper_bound(c); j != free_.end() && j->first <= c + c / 4; ++j)
+            if (!j->second.empty()) { reuse_larger++; return take(j); }
         void* p = nullptr;
-        hipError_t e = hipMalloc(&p, c);
+        hipError_t e = hipErrorOutOfMemory;
+        // near the soft cap a new block would only push the device into failing hipMallocs (slow
+        // under ROCm): reuse a cached block of up to twice the class, else release LRU classes
+        // down to 80 % of the cap in one go
+        if (cap && held + c > cap) {
+            for (auto j = free_.lower_bound(c); j != free_.end() && j->first <= 2 * c; ++j)
+                if (!j->second.empty()) { reuse_larger++; return take(j); }
+            trim_lru(c, cap / 5 * 4);
+        }
+        e = hipMalloc(&p, c);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             for (auto j = free_.lower_bound(c); j != free_.end() && j->first <= 2 * c; ++j)
                 if (!j->second.empty()) { reuse_larger++; return take(j); }
-            hipDeviceSynchronize();
-            trims++;
-            for (auto j = free_.rbegin(); j != free_.rend() && e != hipSuccess; ++j) {
-                for (void* q : j->second) {
-                    hipFree(q);
-                    held -= j->first;
-                }
-                j->second.clear();
+            while (e != hipSuccess && trim_lru(c, held > c ? held - c : 0)) {
                 e = hipMalloc(&p, c);
                 if (e != hipSuccess) (void)hipGetLastError();
             }
@@ -129,6 +162,7 @@ struct Pool {
         held += c;
         live += c;
         cls_[p] = c;
+        used_[c] = ++tick;
         return p;
     }
     void put(void* p, size_t) {
@@ -137,6 +171,7 @@ struct Pool {
         if (it == cls_.end()) return;
         free_[it->second].push_back(p);
         live -= it->second;
+        used_[it->second] = ++tick;
         cls_.erase(it);
     }
     void trim() {
@@ -707,6 +742,12 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
     HIPC(hipSetDevice(e->device));
     HIPC(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     build_tables(e.get());
+    {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) e->pool.cap = fr / 100 * 95;
+        const char* cs = getenv("AESFHE_POOL_CAP_GB");  // override (tests / several engines per device)
+        if (cs) e->pool.cap = (size_t)(atof(cs) * 1e9);
+    }
     HIPC(hipMalloc(&e->ring_d, e->ring_size));
     HIPC(hipHostMalloc((void**)&e->ring_h, e->ring_size, hipHostMallocDefault));
     *out = e.release();
@@ -806,6 +847,13 @@ extern "C" int aesfhe_engine_profile_read(aesfhe_engine* e, const char* fam, int
     API_END
 }
 extern "C" int64_t aesfhe_engine_device_bytes(const aesfhe_engine* e) { return (int64_t)e->pool.held; }
+extern "C" int aesfhe_engine_pool_trim(aesfhe_engine* e) {
+    API_BEGIN
+    HIPC(hipSetDevice(e->device));
+    HIPC(hipStreamSynchronize(e->stream));
+    e->pool.trim();
+    API_END
+}
 extern "C" int aesfhe_engine_pool_stats(const aesfhe_engine* e, int64_t* out) {
     if (!e || !out) return set_err(AESFHE_EARG, "null argument");
     out[0] = (int64_t)e->pool.held;

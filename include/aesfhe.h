@@ -111,6 +111,9 @@ int64_t aesfhe_engine_device_bytes(const aesfhe_engine *eng);
  * (cache releases after a failed hipMalloc), [4] reuses of a larger cached block; zeros in the
  * oracle */
 int aesfhe_engine_pool_stats(const aesfhe_engine *eng, int64_t *out);
+/* release every cached (not live) device block (synchronises the engine's stream): between
+ * workload phases whose buffer sizes differ, so the next phase does not evict in its timed path */
+int aesfhe_engine_pool_trim(aesfhe_engine *eng);
 
 /* ---- host codec (no engine / device needed) --------------------------------------------- */
 /* Canonical-embedding encode: n_slots <= N/2 complex values (zero padded) -> N integer

@@ -497,6 +497,7 @@ int64_t aesfhe_engine_device_bytes(const aesfhe_engine *e) {
     (void)e;
     return 0;
 }
+int aesfhe_engine_pool_trim(aesfhe_engine *e) { return e ? 0 : fail(AESFHE_EARG, "null engine"); }
 int aesfhe_engine_pool_stats(const aesfhe_engine *e, int64_t *out) {
     (void)e;
     if (!out) return AESFHE_EARG;
