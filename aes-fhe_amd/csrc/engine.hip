@@ -1998,28 +1998,43 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             HIPC(hipGetLastError());
         }
     }
-    // 2. giant parts: sum of plaintext products in Q_l u P, ModDown fused with the rescale
+    // 2. giant parts: sum of plaintext products in Q_l u P (every giant in one pass over the
+    // babies, kGM at a time), ModDown fused with the rescale
     std::vector<aesfhe_ct*> parts(ng, nullptr);
     aesfhe_ct* sumq = nullptr;
     try {
-        int t0 = 0;
-        for (int j = 0; j < ng; j++) {
-            std::vector<const u64*> ep, pp;
-            for (int t = t0; t < t0 + nterm[j]; t++) {
-                ep.push_back(E[tbaby[t]]->p);
-                pp.push_back(pts[t]->d);
+        constexpr int kGM = 8;
+        std::vector<int> first(ng + 1, 0);
+        for (int j = 0; j < ng; j++) first[j + 1] = first[j] + nterm[j];
+        std::vector<const u64*> ep(nb);
+        for (int i = 0; i < nb; i++) ep[i] = E[i]->p;
+        auto dep = upload_small(e, ep.data(), ep.size());
+        for (int j0 = 0; j0 < ng; j0 += kGM) {
+            const int gn = std::min(kGM, ng - j0);
+            std::vector<const u64*> pt((size_t)gn * nb, nullptr);
+            std::vector<std::unique_ptr<Tmp>> S;
+            std::vector<u64*> so;
+            double terms = 0;
+            for (int j = 0; j < gn; j++) {
+                for (int t = first[j0 + j]; t < first[j0 + j + 1]; t++) {
+                    if (pt[(size_t)j * nb + tbaby[t]]) throw_err(AESFHE_EARG, "two terms of one giant on the same baby");
+                    pt[(size_t)j * nb + tbaby[t]] = pts[t]->d;
+                    terms++;
+                }
+                S.emplace_back(new Tmp(e, (size_t)B * 2 * neN));
+                so.push_back(S.back()->p);
             }
-            t0 += nterm[j];
-            auto dep = upload_small(e, ep.data(), ep.size());
-            auto dpp = upload_small(e, pp.data(), pp.size());
-            Tmp S(e, (size_t)B * 2 * neN);
+            auto dpt = upload_small(e, pt.data(), pt.size());
+            auto dso = upload_small(e, so.data(), so.size());
             {
-                ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (ep.size() + 1) + ep.size()));
-                hipLaunchKernelGGL(k_dot_pt_ext, dim3(N / 256, ne, B * 2), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64* const*)dpp, (int)ep.size(), S.p, l, ne, e->q, e->qinv, e->Lp1, e->logN);
+                ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (nb + gn) + terms));
+                hipLaunchKernelGGL(k_dot_pt_ext_multi<kGM>, dim3(N / 256, ne, B * 2), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, e->q, e->qinv, e->Lp1, e->logN);
             }
             HIPC(hipGetLastError());
-            parts[j] = ct_new(e, B, 2, l - 1);
-            moddown_acc(e, S.p, B, l, 1, Opnd{nullptr, 0, 0, 0}, parts[j]);
+            for (int j = 0; j < gn; j++) {
+                parts[j0 + j] = ct_new(e, B, 2, l - 1);
+                moddown_acc(e, S[j]->p, B, l, 1, Opnd{nullptr, 0, 0, 0}, parts[j0 + j]);
+            }
         }
         E.clear();
         // 3. giants: key switches of sigma_j(part_j) summed in Q_{l-1} u P, one ModDown

@@ -824,7 +824,21 @@ __global__ void k_dot_pt(const u64* const* __restrict__ cp, const long* __restri
     const double q = (double)qs[l], qi = qinv[l];
     const long off = ((long)l << logN) + k;
     double acc = 0.0;
-    for (int i = 0; i < n; i++) {
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {  // chunks of 8 loads in flight (see k_dot_pt_ext)
+        double cv[8], wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            cv[u] = u2d(cp[i + u][(long)bb * cbs[i + u] + (long)p * cps + off]);
+            wv[u] = u2d(pp[i + u][off]);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            acc += fmul_rem(cv[u], wv[u], wv[u] * qi, q);
+            if ((u & 3) == 3) acc = fred(acc, q, qi);
+        }
+    }
+    for (; i < n; i++) {
         const double c = u2d(cp[i][(long)bb * cbs[i] + (long)p * cps + off]);
         const double w = u2d(pp[i][off]);
         acc += fmul_rem(c, w, w * qi, q);
@@ -861,13 +875,67 @@ __global__ void k_dot_pt_ext(const u64* const* __restrict__ ep, const u64* const
     const int pid = ext_pid(t, l, Lp1);
     const double q = (double)qall[pid], qi = qinvall[pid];
     const long off = ((((long)bb * 2 + c) * ne + t) << logN) + k, po = ((long)t << logN) + k;
+    // terms in chunks of 8 with every load of a chunk issued before its products: one HBM round
+    // trip per chunk instead of per term (the loop was latency-bound at 3-5x below bandwidth)
     double acc = 0.0;
-    for (int i = 0; i < n; i++) {
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {
+        double ev[8], wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            ev[u] = u2d(ep[i + u][off]);
+            wv[u] = u2d(pp[i + u][po]);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            acc += fmul_rem(ev[u], wv[u], wv[u] * qi, q);
+            if ((u & 3) == 3) acc = fred(acc, q, qi);
+        }
+    }
+    for (; i < n; i++) {
         const double w = u2d(pp[i][po]);
         acc += fmul_rem(u2d(ep[i][off]), w, w * qi, q);
         if ((i & 3) == 3) acc = fred(acc, q, qi);
     }
     out[off] = fcanon(acc, q, qi);
+}
+
+// All giants of a BSGS map in one pass over the babies: outs[j][b][c][t] = sum_i pt[j][i][t] *
+// E_i[b][c][t] (pt[j * nb + i] == nullptr: no term), so each baby is read once instead of once
+// per giant (the QP-domain term sums were 18 % of a bootstrap, memory-bound on the re-reads).
+// GM: accumulators held in registers (ng <= GM).  grid (N/256, ne, B*2)
+template <int GM>
+__global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64* const* __restrict__ pt, int nb,
+                                   int ng, u64* const* __restrict__ outs, int l, int ne,
+                                   const u64* __restrict__ qall, const double* __restrict__ qinvall, int Lp1,
+                                   int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.y, bb = blockIdx.z >> 1, c = blockIdx.z & 1;
+    const int pid = ext_pid(t, l, Lp1);
+    const double q = (double)qall[pid], qi = qinvall[pid];
+    const long off = ((((long)bb * 2 + c) * ne + t) << logN) + k, po = ((long)t << logN) + k;
+    double acc[GM];
+#pragma unroll
+    for (int j = 0; j < GM; j++) acc[j] = 0.0;
+    for (int i = 0; i < nb; i++) {
+        const double e = u2d(ep[i][off]);
+#pragma unroll
+        for (int j = 0; j < GM; j++) {
+            if (j >= ng) break;
+            const u64* p = pt[j * nb + i];
+            if (p) {
+                const double w = u2d(p[po]);
+                acc[j] += fmul_rem(e, w, w * qi, q);
+            }
+        }
+        if ((i & 3) == 3) {
+#pragma unroll
+            for (int j = 0; j < GM; j++) acc[j] = fred(acc[j], q, qi);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < GM; j++)
+        if (j < ng) outs[j][off] = fcanon(acc[j], q, qi);
 }
 
 }  // namespace aesfhe

@@ -285,7 +285,8 @@ int aesfhe_dot_pt(aesfhe_engine *eng, const aesfhe_ct *const *cts, const aesfhe_
  * CoeffToSlot / SlotToCoeff; no reference counterpart -- desilofhe's bootstrap is internal):
  *   out = sum_j rho_{gkeys[j]}( sum_{t in terms of j} pts[t] * rho_{bkeys[tbaby[t]]}(ct) )
  * rho_k = the rotation of key k (bkeys: hoisted keys, kind 5; gkeys: galois keys, kind 3),
- * rho_NULL = identity.  Terms of giant j are consecutive, nterm[j] of them.  Arithmetic: the
+ * rho_NULL = identity.  Terms of giant j are consecutive, nterm[j] of them, at most one per
+ * baby (AESFHE_EARG otherwise).  Arithmetic: the
  * baby rotations stay in Q_l u P (E_i = sigma_i(P c0 + acc0_i, acc1_i), no ModDown), each giant's
  * term sum S_j = sum pts * E over Q_l u P (pts from aesfhe_pt_create_ext at level l, encoded at
  * mul_scale(l)) is ModDown'd together with one rescale (D = P q_l) to level l - 1, and the giant

@@ -1654,6 +1654,10 @@ int aesfhe_linear_bsgs(aesfhe_engine *e, const aesfhe_ct *c, int32_t nb, const a
         if (tbaby[t] < 0 || tbaby[t] >= nb) return fail(AESFHE_EARG, "bad baby index");
         if (!pts[t] || !pts[t]->ext || pts[t]->level != l) return fail(AESFHE_EARG, "linear_bsgs needs Q u P plaintexts at the input level");
     }
+    for (int j = 0, t0 = 0; j < ng; t0 += nterm[j], j++)
+        for (int t = t0; t < t0 + nterm[j]; t++)
+            for (int t2 = t0; t2 < t; t2++)
+                if (tbaby[t2] == tbaby[t]) return fail(AESFHE_EARG, "two terms of one giant on the same baby");
     aesfhe_ct *r = ct_new(e, c->B, 2, l - 1);
     if (c->is_zero) {
         r->is_zero = 1;
