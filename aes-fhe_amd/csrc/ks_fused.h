@@ -4,7 +4,7 @@
 // in canonical NTT form (row pass) and reads it straight back in k_ks_inner_all:
 // 2 * beta * B * (l + 1 + K) limbs of HBM traffic per call, the largest single item of a key
 // switch.  Here ks_modup stops after the column pass (the raw-double intermediate stays in the
-// ext buffer) and one workgroup per (target limb t, 16-row block, batch element b) runs the row
+// ext buffer) and one workgroup per (target limb t, 8-row block, batch element b) runs the row
 // pass of ext[j][b][t] for every digit j in registers, multiplies by the key digit and
 // accumulates, writing only the two accumulators acc[b][0/1][t] (accum: added to what acc holds)
 // -- the same canonical values k_ks_inner_all produces (the arithmetic is exact mod q; only the lazy ranges differ).
@@ -18,83 +18,159 @@
 
 namespace aesfhe {
 
-// grid: 8 * B * (ne * 16 / 8) blocks of 256; block id -> (xcd group x = id & 7, b, pair), pair =
-// (t, row block): all B batch elements of one (t, row block) are dealt to one XCD (blocks
-// x, x + 8, ...) so the key rows they share are L2 hits.
+// Row NTT with 8 elements per lane (32 lanes per 256-point row), so that the two accumulators of
+// the inner product fit beside it at 4+ waves per SIMD (16 elements per lane held 232 VGPRs:
+// 2 waves per SIMD, latency-bound).  Layouts of row element e (0..255), lane L (0..31), register r:
+//   A: e = L + 32 r          stages ml = 1, 2, 4     (distances 128, 64, 32)
+//   B: e = 32 (L >> 2) + (L & 3) + 4 r   ml = 8, 16, 32   (16, 8, 4)
+//   C: e = 8 L + r           ml = 64, 128     (2, 1)
+// then back to A for the coalesced inner product.  Twiddle of stage ml, element e:
+// psi^{brv(ml (256 + row) + (e >> (8 - log2 ml)))}.  LDS per row: e -> e + (e >> 3) (288 words),
+// conflict-free for the A / B / C patterns.
+__device__ __forceinline__ int r8p(int e) { return e + (e >> 3); }
+
+__device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, double* sr, int L, int row,
+                                             const double* W, double q, double qi, bool big) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) x[r] = ld_d(&rp[L + 32 * r]);
+    // A: ml = 1, 2, 4 (global stages 0..2 of the pass); twiddle j = r >> (3 - st)
+#pragma unroll
+    for (int st = 0; st < 3; st++) {
+        const int ml = 1 << st, h = 4 >> st;
+        if (big && (st & 1) == 0) {
+#pragma unroll
+            for (int r = 0; r < 8; r++) x[r] = fred(x[r], q, qi);
+        }
+        const int base = ml * (256 + row);
+#pragma unroll
+        for (int j = 0; j < ml; j++) {
+            const double wq = W[base + j];
+#pragma unroll
+            for (int k = 0; k < h; k++) ct_f(x[j * 2 * h + k], x[j * 2 * h + k + h], wq, q);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) sr[r8p(L + 32 * r)] = x[r];
+    __syncthreads();
+    const int eb = 32 * (L >> 2) + (L & 3);
+#pragma unroll
+    for (int r = 0; r < 8; r++) x[r] = sr[r8p(eb + 4 * r)];
+    // B: ml = 8, 16, 32 (stages 3..5); twiddle j = e >> (8 - st) = (L >> 2) * ml / 8 + (r >> (6 - st))
+#pragma unroll
+    for (int st = 3; st < 6; st++) {
+        const int ml = 1 << st, h = 4 >> (st - 3), nj = ml >> 3;
+        if (big && (st & 1) == 0) {
+#pragma unroll
+            for (int r = 0; r < 8; r++) x[r] = fred(x[r], q, qi);
+        }
+        const int base = ml * (256 + row) + (L >> 2) * nj;
+#pragma unroll
+        for (int j = 0; j < nj; j++) {
+            const double wq = W[base + j];
+#pragma unroll
+            for (int k = 0; k < h; k++) ct_f(x[j * 2 * h + k], x[j * 2 * h + k + h], wq, q);
+        }
+    }
+    __syncthreads();  // every lane has read its B elements
+#pragma unroll
+    for (int r = 0; r < 8; r++) sr[r8p(eb + 4 * r)] = x[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; r++) x[r] = sr[r8p(8 * L + r)];
+    // C: ml = 64 (distance 2, j = 2L + (r >> 2)), ml = 128 (distance 1, j = 4L + (r >> 1))
+    if (big) {
+#pragma unroll
+        for (int r = 0; r < 8; r++) x[r] = fred(x[r], q, qi);
+    }
+    {
+        const int base = 64 * (256 + row) + 2 * L;
+        const double w0 = W[base], w1 = W[base + 1];
+        ct_f(x[0], x[2], w0, q);
+        ct_f(x[1], x[3], w0, q);
+        ct_f(x[4], x[6], w1, q);
+        ct_f(x[5], x[7], w1, q);
+    }
+    {
+        const int base = 128 * (256 + row) + 4 * L;
+#pragma unroll
+        for (int j = 0; j < 4; j++) ct_f(x[2 * j], x[2 * j + 1], W[base + j], q);
+    }
+    __syncthreads();  // every lane has read its C elements
+#pragma unroll
+    for (int r = 0; r < 8; r++) sr[r8p(8 * L + r)] = big ? fred(x[r], q, qi) : x[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 8; r++) x[r] = sr[r8p(L + 32 * r)];  // back to A
+    __syncthreads();  // the next digit rewrites sr
+}
+
+// grid: 8 * B * (ne * 32 / 8) blocks of 256 (8 rows x 32 lanes); block id -> (xcd group
+// x = id & 7, b, pair), pair = (t, 8-row block): all B batch elements of one (t, row block) are
+// dealt to one XCD (blocks x, x + 8, ...) so the key rows they share are L2 hits.
 __global__ __launch_bounds__(256) void k_nttf_rows_ks(const u64* __restrict__ d, long dbs,
                                                       const u64* __restrict__ ext, long exs, long exj,
                                                       const u64* __restrict__ key, long kdig, long kcomp,
                                                       u64* __restrict__ acc, long abs_, long acs, int B,
                                                       int beta, int K, int l, int ne, Tabs T, Opnd addend,
                                                       const double* __restrict__ pmodf, int accum) {
-    __shared__ double s[16 * 16 * kPadF];
+    __shared__ double s[8 * 288];
     const int id = blockIdx.x, x8 = id & 7, rest = id >> 3;
     const int bb = rest % B, pair = (rest / B) * 8 + x8;
-    const int t = pair >> 4, rb = pair & 15;
+    const int t = pair >> 5, rb = pair & 31;
     if (t >= ne) return;
     const int pid = t <= l ? t : T.Lp1 + (t - l - 1);
     const int own = t <= l ? t / K : -1;  // the digit whose limbs include t (Q limbs only)
-    const int tid = threadIdx.x, b = tid & 15, rl = tid >> 4;
-    const int row = rb * 16 + rl;
+    const int tid = threadIdx.x, L = tid & 31, rl = tid >> 5;
+    const int row = rb * 8 + rl;
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* W = T.psif + ((long)pid << 16);
-    double* sr = s + rl * 16 * kPadF;
-    const long toff = ((long)t << 16) + (long)rb * 4096;  // this block's tile within a limb
-    double a0[16], a1[16];
+    double* sr = s + rl * 288;
+    const long roff = ((long)t << 16) + (long)row * 256 + L;  // element (row, L + 32 r) at roff + 32 r
+    double a0[8], a1[8];
 #pragma unroll
-    for (int k = 0; k < 16; k++) a0[k] = a1[k] = 0.0;
+    for (int r = 0; r < 8; r++) a0[r] = a1[r] = 0.0;
 #pragma unroll 1
     for (int j = 0; j < beta; j++) {
-        double v[16];
+        double v[8];
         if (j == own) {  // the digit's own limbs: d itself, already in NTT form
-            const u64* dp = d + (long)bb * dbs + toff;
+            const u64* dp = d + (long)bb * dbs + roff;
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = u2d(dp[k * 256 + tid]);
+            for (int r = 0; r < 8; r++) v[r] = u2d(dp[32 * r]);
         } else {
-            double x[16];
-            row_ntt_fwd(x, ext + (long)j * exj + (long)bb * exs + ((long)t << 16) + (long)row * 256, sr, b, row,
-                        W, q, qi, big);
-            __syncthreads();  // every lane has read its transposed column out of s
-#pragma unroll
-            for (int k = 0; k < 16; k++) sr[b * kPadF + k] = big ? fred(x[k], q, qi) : x[k];
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = s[row_tile_idx(k * 256 + tid)];
-            __syncthreads();  // s is rewritten by the next digit's transpose
+            row_ntt8_fwd(v, ext + (long)j * exj + (long)bb * exs + ((long)t << 16) + (long)row * 256, sr, L, row,
+                         W, q, qi, big);
         }
-        const u64* kp = key + (long)j * kdig + ((long)pid << 16) + (long)rb * 4096;
+        const u64* kp = key + (long)j * kdig + ((long)pid << 16) + (long)row * 256 + L;
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int e = k * 256 + tid;
-            const double kb = u2d(kp[e]), ka = u2d(kp[e + kcomp]);
-            a0[k] += fmul_rem(v[k], kb, kb * qi, q);
-            a1[k] += fmul_rem(v[k], ka, ka * qi, q);
+        for (int r = 0; r < 8; r++) {
+            const double kb = u2d(kp[32 * r]), ka = u2d(kp[32 * r + kcomp]);
+            a0[r] += fmul_rem(v[r], kb, kb * qi, q);
+            a1[r] += fmul_rem(v[r], ka, ka * qi, q);
         }
         if (big && (j & 3) == 3) {
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                a0[k] = fred(a0[k], q, qi);
-                a1[k] = fred(a1[k], q, qi);
+            for (int r = 0; r < 8; r++) {
+                a0[r] = fred(a0[r], q, qi);
+                a1[r] = fred(a1[r], q, qi);
             }
         }
     }
-    u64* o0 = acc + (long)bb * abs_ + toff;
+    u64* o0 = acc + (long)bb * abs_ + roff;
     if (pmodf && t <= l) {
         const double f = pmodf[t], w = tw_w(f, q);
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int e = k * 256 + tid, kk = rb * 4096 + e;
-            a0[k] = fred(a0[k], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 0, t, kk, 16)), w, f, q);
-            a1[k] = fred(a1[k], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, kk, 16)), w, f, q);
+        for (int r = 0; r < 8; r++) {
+            const int kk = row * 256 + L + 32 * r;
+            a0[r] = fred(a0[r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 0, t, kk, 16)), w, f, q);
+            a1[r] = fred(a1[r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, kk, 16)), w, f, q);
         }
     }
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int e = k * 256 + tid;
-        const double p0 = accum ? u2d(o0[e]) : 0.0, p1 = accum ? u2d(o0[acs + e]) : 0.0;
-        o0[e] = fcanon(a0[k] + p0, q, qi);
-        o0[acs + e] = fcanon(a1[k] + p1, q, qi);
+    for (int r = 0; r < 8; r++) {
+        const double p0 = accum ? u2d(o0[32 * r]) : 0.0, p1 = accum ? u2d(o0[acs + 32 * r]) : 0.0;
+        o0[32 * r] = fcanon(a0[r] + p0, q, qi);
+        o0[acs + 32 * r] = fcanon(a1[r] + p1, q, qi);
     }
 }
 
