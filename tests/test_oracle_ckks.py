@@ -213,3 +213,27 @@ def test_mul_fma_and_mixed_level_lincomb_oracle(oracle_lib):
     li = e.lincomb([a, b, c], [0.5, -0.25j, 3.0])
     assert li.level == 4
     np.testing.assert_allclose(e.decrypt(li, sk), 0.5 * x - 0.25j * y + 3 * z, atol=1e-6)
+
+
+def test_linear_bsgs_oracle(oracle_lib):
+    """aesfhe_linear_bsgs (include/aesfhe.h): slots equal the plain baby-step giant-step sum,
+    batch and identity steps included; one level used; a giant with two terms on one baby is an
+    argument error (the HIP engine's single-pass term kernel relies on it)."""
+    e = Engine(log_n=11, max_level=5, special_primes=2, seed=9, _lib=oracle_lib)
+    n = e.slot_count
+    rng = np.random.default_rng(8)
+    sk = e.create_secret_key(2)
+    z = rng.uniform(-1, 1, (3, n))
+    c = e.encrypt(z, e.create_public_key(sk), level=4)
+    diags = [rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n) for _ in range(4)]
+    babies, plan = [0, 2, -7], [(0, [(1, 0), (2, 1)]), (5, [(0, 2), (1, 3), (2, 0)])]
+    bk = [None if d == 0 else e.create_hoisted_rotation_key(sk, -d) for d in babies]
+    gk = [None if d == 0 else e.create_fixed_rotation_key(sk, -d) for d, _ in plan]
+    pts = [e.encode(v) for v in diags]
+    out = e.linear_bsgs(c, bk, gk, [[(b, pts[i]) for b, i in tl] for _, tl in plan])
+    want = sum(np.roll(sum(diags[i] * np.roll(z, -babies[b], axis=1) for b, i in tl), -d, axis=1)
+               for d, tl in plan)
+    assert out.level == 3 and out.batch == 3
+    np.testing.assert_allclose(e.decrypt(out, sk), want, atol=1e-6)
+    with pytest.raises(RuntimeError, match="same baby"):
+        e.linear_bsgs(c, bk, gk[:1], [[(1, pts[0]), (1, pts[1])]])
