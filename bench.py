@@ -231,9 +231,12 @@ def main():
 
     from aes_xor_fhe import aes_tables as T
 
-    eng, R = setup_engine(args, local)
+    # one rank per GPU; more ranks than GPUs (a multi-rank rehearsal on a 1-GPU box) share them
+    ndev = torch.cuda.device_count() or 1
+    device = local % ndev
+    eng, R = setup_engine(args, device)
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(device)
     rng = np.random.default_rng(1000 + rank)
     blocks = rng.integers(0, 256, (args.batch, R.n_blk, 16), dtype=np.uint8)
     rk = np.random.default_rng(25073102).integers(0, 256, 16, dtype=np.uint8)
