@@ -132,6 +132,14 @@ __global__ __launch_bounds__(256) void k_nttf_rows_ks(const u64* __restrict__ d,
     for (int r = 0; r < 8; r++) a0[r] = a1[r] = 0.0;
 #pragma unroll 1
     for (int j = 0; j < beta; j++) {
+        // the key digit's words are loaded first: they arrive while the row NTT computes
+        const u64* kp = key + (long)j * kdig + ((long)pid << 16) + (long)row * 256 + L;
+        u64 kbw[8], kaw[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            kbw[r] = kp[32 * r];
+            kaw[r] = kp[32 * r + kcomp];
+        }
         double v[8];
         if (j == own) {  // the digit's own limbs: d itself, already in NTT form
             const u64* dp = d + (long)bb * dbs + roff;
@@ -141,10 +149,9 @@ __global__ __launch_bounds__(256) void k_nttf_rows_ks(const u64* __restrict__ d,
             row_ntt8_fwd(v, ext + (long)j * exj + (long)bb * exs + ((long)t << 16) + (long)row * 256, sr, L, row,
                          W, q, qi, big);
         }
-        const u64* kp = key + (long)j * kdig + ((long)pid << 16) + (long)row * 256 + L;
 #pragma unroll
         for (int r = 0; r < 8; r++) {
-            const double kb = u2d(kp[32 * r]), ka = u2d(kp[32 * r + kcomp]);
+            const double kb = u2d(kbw[r]), ka = u2d(kaw[r]);
             a0[r] += fmul_rem(v[r], kb, kb * qi, q);
             a1[r] += fmul_rem(v[r], ka, ka * qi, q);
         }
