@@ -205,6 +205,7 @@ struct aesfhe_engine {
     // device tables
     u64 *q, *psi, *ipsi, *ninv;
     double *qinv, *psif, *ipsif, *ninvf;
+    double *rtwf = nullptr, *irtwf = nullptr;  // N = 2^16 row-pass twiddle factors [np][256][8] (ntt256f.h)
     Tw *tw, *itw;
     u64* iroot;  // host copy only needed
     std::vector<u64> h_iroot;
@@ -239,6 +240,8 @@ struct aesfhe_engine {
         t.psif = psif;
         t.ipsi = ipsi;
         t.ipsif = ipsif;
+        t.rtwf = rtwf;
+        t.irtwf = irtwf;
         t.ninv = ninv;
         t.ninvf = ninvf;
         t.tw = tw;
@@ -567,6 +570,17 @@ static void build_tables(aesfhe_engine* e) {
     up(hipsif, &e->ipsif);
     up(hninv, &e->ninv);
     up(hninvf, &e->ninvf);
+    if (e->logN == 16) {  // row factors psi^{+-brv(row << s)} / q, s = 0..7 (ntt256f.h tw_row)
+        std::vector<double> hr((size_t)np * 2048), hir((size_t)np * 2048);
+        for (int p = 0; p < np; p++)
+            for (int row = 0; row < 256; row++)
+                for (int sh = 0; sh < 8; sh++) {
+                    hr[(size_t)p * 2048 + row * 8 + sh] = hpsif[(size_t)p * N + (row << sh)];
+                    hir[(size_t)p * 2048 + row * 8 + sh] = hipsif[(size_t)p * N + (row << sh)];
+                }
+        up(hr, &e->rtwf);
+        up(hir, &e->irtwf);
+    }
     {
         std::vector<Tw> htw((size_t)np * N), hitw((size_t)np * N);
         for (size_t i = 0; i < htw.size(); i++) {
@@ -778,7 +792,7 @@ static void engine_teardown(aesfhe_engine* e) {
     }
     for (auto ev : e->spare) hipEventDestroy(ev);
     e->pool.trim();
-    void* ptrs[] = {e->q, e->psi, e->ipsi, e->ninv, e->qinv, e->psif, e->ipsif, e->ninvf,
+    void* ptrs[] = {e->q, e->psi, e->ipsi, e->ninv, e->qinv, e->psif, e->ipsif, e->ninvf, e->rtwf, e->irtwf,
                     e->mu_hatinv, e->mu_hat, e->md_phatinv, e->md_phat, e->md_pinv, e->rs_inv,
                     e->rs_mod, e->pmod, e->mu_hatinvf, e->mu_hatf, e->md_phatinvf, e->md_phatf,
                     e->md_pinvf, e->rs_invf, e->ring_d, e->tw, e->itw, e->mdr_invf, e->mdr_hatf,

@@ -124,6 +124,8 @@ struct Tabs {
     const double* psif;  // psi/q
     const u64* ipsi;     // [np][N] psi^{-brv(k)}
     const double* ipsif;
+    const double* rtwf;   // N = 2^16 only: [np][256][8] psi^{brv(row << s)} / q (ntt256f.h)
+    const double* irtwf;  // the same for psi^{-1}
     const u64* ninv;
     const double* ninvf;
     const struct Tw* tw;   // [np][N] {psi^{brv(k)}, psi^{brv(k)}/q} interleaved (16 B)

@@ -9,7 +9,7 @@
 // accumulates, writing only the two accumulators acc[b][0/1][t] (accum: added to what acc holds)
 // -- the same canonical values k_ks_inner_all produces (the arithmetic is exact mod q; only the lazy ranges differ).
 //
-// Ranges: row_ntt_fwd leaves |x| <= 17q for q < 2^42 (folded to q/2 + 1 for larger primes
+// Ranges: the row NTT (table twiddles) leaves |x| <= 17q for q < 2^42 (folded to q/2 + 1 for larger primes
 // before the product); fmul_rem(x, key) lies in (-1.5q, 1.5q) (on-the-fly key quotient), so the
 // beta <= 12 products sum below 18q < 2^47 for small primes; big primes fold every 4 digits.
 #pragma once

@@ -7,16 +7,14 @@
 // (8 B, Tabs::psif / ipsif) and w = rint(wq * q) is recovered exactly (|wq*q - w| < 2^-4).
 //
 // Ranges (fmul_rem needs |input| < 2^51, fred needs |x| < 2^53):
-//   forward CT   x' = x + v, y' = x - v with v in (-q, q): +q per stage.  Primes < 2^42 grow
-//                to at most 17q over both passes; larger primes are folded (fred, |x| <= q/2+1)
-//                before every second stage (fmul_rem inputs <= 2q).
-//   inverse GS   x' = x + y doubles per stage, y' = (x - y) w in (-q, q): primes < 2^42 reach
-//                at most 2^8 q per pass (the column pass starts folded); for larger primes the
-//                sum output is folded in every butterfly (inputs <= q, differences <= 2q).
-// Twiddles come from the per-prime table (cache-resident; the row passes walk N entries per
-// limb).  Generating them as psi^{brv(256 ml + j)} * psi^{brv(row << s)} (brv is additive over
-// disjoint bit fields) halves the table traffic but costs one modular product per twiddle --
-// +26 % VALU on a pass that is VALU-bound as much as HBM-bound: measured slower, dropped.
+//   forward CT   x' = x + v, y' = x - v with v in (-q, q) (table twiddles: column passes, the
+//                fused key-switch pass) or (-1.5q, 1.5q) (generated twiddles, tw_row: the
+//                standalone row passes): primes < 2^42 grow to at most 9q + 8 * 1.5q = 21q over
+//                both passes; larger primes are folded (fred, |x| <= q/2+1) before every second
+//                stage (fmul_rem inputs <= 2q).
+//   inverse GS   x' = x + y doubles per stage, y' = (x - y) w in (-1.5q, 1.5q): primes < 2^42
+//                reach at most 2^8 q per pass (the column pass starts folded); for larger primes
+//                the sum output is folded in every butterfly (inputs <= q, differences <= 2.5q).
 // The branch on the prime size is block-uniform (one prime per block).  Between the two passes
 // of a transform the intermediate is stored as raw doubles; final outputs are canonical u64
 // residues in [0, q), so results are identical to ntt256.h and to the oracle residue for residue.
@@ -40,6 +38,34 @@ __device__ __forceinline__ void gs_f(double& x, double& y, double wq, double q, 
     const double s = x + y, d = x - y;
     x = FOLD ? fred(s, q, qi) : s;
     y = fmul_rem(d, tw_w(wq, q), wq, q);
+}
+// CT / GS butterflies with an on-the-fly twiddle (w exact, |w| < q; wq = w * (1/q) rounded
+// twice, so fmul_rem's remainder is within 1.5q instead of q)
+__device__ __forceinline__ void ct_fw(double& x, double& y, double w, double wq, double q) {
+    const double v = fmul_rem(y, w, wq, q);
+    const double t = x;
+    x = t + v;
+    y = t - v;
+}
+template <bool FOLD>
+__device__ __forceinline__ void gs_fw(double& x, double& y, double w, double wq, double q, double qi) {
+    const double s = x + y, d = x - y;
+    x = FOLD ? fred(s, q, qi) : s;
+    y = fmul_rem(d, w, wq, q);
+}
+// Row-pass twiddles without the N-entry table walk.  The row pass's stage with group size
+// ml = 2^s (m = 256 ml) uses psi^{brv(m + i)}, i = ml * row + j (j < ml); the three bit fields
+// of m + i are disjoint, so brv is additive and
+//     psi^{brv(256 ml + ml row + j)} = psi^{brv(256 ml + j)} * psi^{brv(row << s)}
+// = (a table entry shared by every row: 255 per prime, cache-resident) x (a per-row factor,
+// Tabs::rtwf[pid][row][s]).  Walking the N-entry table instead reads as many bytes as the limb
+// (the row passes' reads are 1.5-1.9x their writes): the standalone row passes run 5-16 %
+// faster generated (tools/ntt_q_bench.hip: 87.6 vs 104 us over 468 limbs), at +1 modular
+// product per twiddle.
+__device__ __forceinline__ void tw_row(const double* W, int idx, double rq, double q, double qi,
+                                       double& w, double& wq) {
+    w = fmul_rem(tw_w(W[idx], q), tw_w(rq, q), rq, q);
+    wq = w * qi;
 }
 __device__ __forceinline__ double ld_d(const u64* p) { return __longlong_as_double((long long)*p); }
 __device__ __forceinline__ void st_d(u64* p, double v) { *p = (u64)__double_as_longlong(v); }
@@ -118,7 +144,8 @@ struct RowFin {
 // through sr = s + rl * 16 * kPadF, 4 stages.  On return lane ap = b holds elements
 // ap * 16 + bb (bb = 0..15) of its row, lazily reduced (ranges: file header).
 __device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, double* sr, int b, int row,
-                                            const double* W, double q, double qi, bool big) {
+                                            const double* W, const double* R, double q, double qi,
+                                            bool big) {
 #pragma unroll
     for (int a = 0; a < 16; a++) x[a] = ld_d(&rp[a * 16 + b]);
 #pragma unroll
@@ -128,12 +155,13 @@ __device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, doub
 #pragma unroll
             for (int a = 0; a < 16; a++) x[a] = fred(x[a], q, qi);
         }
-        const int base = ml * (256 + row);  // twiddle psi^{brv(256 ml + ml row + j)}
+        const double rq = R[st];
 #pragma unroll
         for (int j = 0; j < ml; j++) {  // butterflies of twiddle j: a = j * 2h + k, k < h
-            const double wq = W[base + j];
+            double w, wq;
+            tw_row(W, 256 * ml + j, rq, q, qi, w, wq);
 #pragma unroll
-            for (int k = 0; k < h; k++) ct_f(x[j * 2 * h + k], x[j * 2 * h + k + h], wq, q);
+            for (int k = 0; k < h; k++) ct_fw(x[j * 2 * h + k], x[j * 2 * h + k + h], w, wq, q);
         }
     }
 #pragma unroll
@@ -149,12 +177,13 @@ __device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, doub
 #pragma unroll
             for (int bb = 0; bb < 16; bb++) x[bb] = fred(x[bb], q, qi);
         }
-        const int base = ml * (256 + row) + ap * nj;
+        const double rq = R[st];
 #pragma unroll
         for (int j = 0; j < nj; j++) {  // bb = j * 2h + k, k < h
-            const double wq = W[base + j];
+            double w, wq;
+            tw_row(W, 256 * ml + ap * nj + j, rq, q, qi, w, wq);
 #pragma unroll
-            for (int k = 0; k < h; k++) ct_f(x[j * 2 * h + k], x[j * 2 * h + k + h], wq, q);
+            for (int k = 0; k < h; k++) ct_fw(x[j * 2 * h + k], x[j * 2 * h + k + h], w, wq, q);
         }
     }
 }
@@ -178,10 +207,11 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* W = T.psif + ((long)pid << T.logN);
+    const double* R = T.rtwf + ((long)pid << 11) + row * 8;
     double x[16];
     double* sr = s + rl * 16 * kPadF;
     const int ap = b;
-    row_ntt_fwd(x, io + (long)row * 256, sr, b, row, W, q, qi, big);
+    row_ntt_fwd(x, io + (long)row * 256, sr, b, row, W, R, q, qi, big);
     // coalesced store through LDS: canonical residues, then row-major copy-out
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) sr[ap * kPadF + bb] = __longlong_as_double((long long)fcanon(x[bb], q, qi));
@@ -235,18 +265,19 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
     double x[16];
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) x[bb] = sr[ap * kPadF + bb];
-    const int N = 1 << T.logN;
+    const double* R = T.irtwf + ((long)pid << 11) + row * 8;
     auto stages_lo = [&](auto fold) {
 #pragma unroll
         for (int st = 0; st < 4; st++) {
-            const int t = 1 << st, nj = 8 / t;
-            const int base = N / (2 * t) + row * (128 / t) + ap * nj;  // psi^{-brv(256 ml + ml row + j)}
+            const int t = 1 << st, ml = 128 / t, nj = 8 / t;  // group size ml = 2^(7 - st)
+            const double rq = R[7 - st];
 #pragma unroll
             for (int j = 0; j < nj; j++) {  // butterflies of twiddle j: bb = j * 2t + k, k < t
-                const double wq = W[base + j];
+                double w, wq;
+                tw_row(W, 256 * ml + ap * nj + j, rq, q, qi, w, wq);
 #pragma unroll
                 for (int k = 0; k < t; k++)
-                    gs_f<decltype(fold)::value>(x[j * 2 * t + k], x[j * 2 * t + k + t], wq, q, qi);
+                    gs_fw<decltype(fold)::value>(x[j * 2 * t + k], x[j * 2 * t + k + t], w, wq, q, qi);
             }
         }
     };
@@ -261,13 +292,14 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
 #pragma unroll
         for (int st = 4; st < 8; st++) {
             const int t = 1 << st, ta = t >> 4, ml = 128 / t;
-            const int base = N / (2 * t) + row * ml;
+            const double rq = R[7 - st];
 #pragma unroll
             for (int j = 0; j < ml; j++) {  // a = j * 2ta + k, k < ta
-                const double wq = W[base + j];
+                double w, wq;
+                tw_row(W, 256 * ml + j, rq, q, qi, w, wq);
 #pragma unroll
                 for (int k = 0; k < ta; k++)
-                    gs_f<decltype(fold)::value>(x[j * 2 * ta + k], x[j * 2 * ta + k + ta], wq, q, qi);
+                    gs_fw<decltype(fold)::value>(x[j * 2 * ta + k], x[j * 2 * ta + k + ta], w, wq, q, qi);
             }
         }
     };

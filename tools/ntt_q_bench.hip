@@ -417,6 +417,18 @@ __global__ void k_copy(const u64* __restrict__ a, u64* __restrict__ b, long n) {
     long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) b[i] = a[i];
 }
+__global__ void k_copy16(const ulonglong2* __restrict__ a, ulonglong2* __restrict__ b, long n) {
+    long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) b[i] = a[i];
+}
+__global__ void k_copy16x4(const ulonglong2* __restrict__ a, ulonglong2* __restrict__ b, long n) {
+    long i = ((long)blockIdx.x * blockDim.x) * 4 + threadIdx.x;
+    ulonglong2 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = a[i + u * blockDim.x];
+#pragma unroll
+    for (int u = 0; u < 4; u++) b[i + u * blockDim.x] = v[u];
+}
 
 int main(int argc, char** argv) {
     const int logN = 16, N = 1 << logN, L = 30, K = 8;
@@ -424,7 +436,7 @@ int main(int argc, char** argv) {
     Chain ch = make_chain(logN, L, K, 50, 50, 40);
     const int np = (int)ch.q.size();
     std::vector<u64> hq(ch.q);
-    std::vector<double> hqi(np), hpsif((size_t)np * N), hz(np, 0.0);
+    std::vector<double> hqi(np), hpsif((size_t)np * N), hr((size_t)np * 2048), hz(np, 0.0);
     for (int p = 0; p < np; p++) {
         u64 q = hq[p];
         hqi[p] = 1.0 / (double)q;
@@ -433,11 +445,14 @@ int main(int argc, char** argv) {
         pw[0] = 1;
         for (int k = 1; k < N; k++) pw[k] = h_mulmod(pw[k - 1], psi, q);
         for (int k = 0; k < N; k++) hpsif[(size_t)p * N + k] = (double)pw[bit_reverse(k, logN)] / (double)q;
+        for (int row = 0; row < 256; row++)
+            for (int sh = 0; sh < 8; sh++) hr[(size_t)p * 2048 + row * 8 + sh] = hpsif[(size_t)p * N + (row << sh)];
     }
     Tabs T{};
     T.q = up(hq);
     T.qinv = up(hqi);
     T.psif = up(hpsif);
+    T.rtwf = up(hr);
     T.logN = logN;
     T.Lp1 = np;
     // limb y uses prime y % np: one "poly" per np limbs
@@ -521,6 +536,8 @@ int main(int argc, char** argv) {
                16.0 * limbs * N / (us * 1e3) / 8000.0);
     };
     timeit("copy (r+w = 16 B/coef)", [&] { hipLaunchKernelGGL(k_copy, dim3((long)limbs * N / 256), dim3(256), 0, 0, src, d2, (long)limbs * N); });
+    timeit("copy 16 B / lane", [&] { hipLaunchKernelGGL(k_copy16, dim3((long)limbs * N / 512), dim3(256), 0, 0, (const ulonglong2*)src, (ulonglong2*)d2, (long)limbs * N / 2); });
+    timeit("copy 16 B x4 / lane", [&] { hipLaunchKernelGGL(k_copy16x4, dim3((long)limbs * N / 2048), dim3(256), 0, 0, (const ulonglong2*)src, (ulonglong2*)d2, (long)limbs * N / 2); });
     timeit("two-pass forward (cols + rows)", two_pass);
     timeit("one-pass forward (k_nttf_fwd_q2)", one_pass);
     timeit("one-pass v1 (k_nttf_fwd_q)", one_pass_v1);
