@@ -2005,11 +2005,8 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
                 HIPC(hipGetLastError());
                 continue;
             }
-            Tmp acc(e, (size_t)B * 2 * neN);
-            ks_inner_acc(e, c1, cv.bs, ext->p, B, l, bkeys[i], c0, true, acc.p, false);
-            Span src = span_s(acc.p, neN, ne, l + 1, 0, e->Lp1), dst = span_s(E.back()->p, neN, ne, l + 1, 0, e->Lp1);
-            hipLaunchKernelGGL(k_galois, dim3(N / 256, B * 2 * ne), dim3(256), 0, e->stream, src, dst, (u64)bkeys[i]->galois, e->logN, e->Lp1);
-            HIPC(hipGetLastError());
+            // stored unpermuted: the term kernel applies sigma_i as it reads (k_dot_pt_ext_multi)
+            ks_inner_acc(e, c1, cv.bs, ext->p, B, l, bkeys[i], c0, true, E.back()->p, false);
         }
     }
     // 2. giant parts: sum of plaintext products in Q_l u P (every giant in one pass over the
@@ -2021,8 +2018,13 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
         std::vector<int> first(ng + 1, 0);
         for (int j = 0; j < ng; j++) first[j + 1] = first[j] + nterm[j];
         std::vector<const u64*> ep(nb);
-        for (int i = 0; i < nb; i++) ep[i] = E[i]->p;
+        std::vector<u64> gal(nb, 0);
+        for (int i = 0; i < nb; i++) {
+            ep[i] = E[i]->p;
+            gal[i] = bkeys[i] ? bkeys[i]->galois : 0;
+        }
         auto dep = upload_small(e, ep.data(), ep.size());
+        auto dgal = upload_small(e, gal.data(), gal.size());
         for (int j0 = 0; j0 < ng; j0 += kGM) {
             const int gn = std::min(kGM, ng - j0);
             std::vector<const u64*> pt((size_t)gn * nb, nullptr);
@@ -2042,7 +2044,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             auto dso = upload_small(e, so.data(), so.size());
             {
                 ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (nb + gn) + terms));
-                hipLaunchKernelGGL(k_dot_pt_ext_multi<kGM>, dim3(N / 256, ne, B * 2), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, e->q, e->qinv, e->Lp1, e->logN);
+                hipLaunchKernelGGL(k_dot_pt_ext_multi<kGM>, dim3(N / 256, ne, B * 2), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64*)dgal, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, e->q, e->qinv, e->Lp1, e->logN);
             }
             HIPC(hipGetLastError());
             for (int j = 0; j < gn; j++) {

@@ -904,8 +904,11 @@ __global__ void k_dot_pt_ext(const u64* const* __restrict__ ep, const u64* const
 // E_i[b][c][t] (pt[j * nb + i] == nullptr: no term), so each baby is read once instead of once
 // per giant (the QP-domain term sums were 18 % of a bootstrap, memory-bound on the re-reads).
 // GM: accumulators held in registers (ng <= GM).  grid (N/256, ne, B*2)
+// gal[i] > 1: baby i is stored unpermuted and sigma_{gal[i]} is applied by the read (the NTT-slot
+// gather of k_galois), so the permuted copy of each baby is never written.
 template <int GM>
-__global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64* const* __restrict__ pt, int nb,
+__global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64* __restrict__ gal,
+                                   const u64* const* __restrict__ pt, int nb,
                                    int ng, u64* const* __restrict__ outs, int l, int ne,
                                    const u64* __restrict__ qall, const double* __restrict__ qinvall, int Lp1,
                                    int logN) {
@@ -913,12 +916,17 @@ __global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64*
     const int t = blockIdx.y, bb = blockIdx.z >> 1, c = blockIdx.z & 1;
     const int pid = ext_pid(t, l, Lp1);
     const double q = (double)qall[pid], qi = qinvall[pid];
-    const long off = ((((long)bb * 2 + c) * ne + t) << logN) + k, po = ((long)t << logN) + k;
+    const long base = (((long)bb * 2 + c) * ne + t) << logN, off = base + k, po = ((long)t << logN) + k;
+    const u64 M = 2ULL << logN;
+    const u64 ek = 2 * (u64)(__brev((unsigned)k) >> (32 - logN)) + 1;
     double acc[GM];
 #pragma unroll
     for (int j = 0; j < GM; j++) acc[j] = 0.0;
     for (int i = 0; i < nb; i++) {
-        const double e = u2d(ep[i][off]);
+        const u64 g = gal[i];
+        long src = off;
+        if (g > 1) src = base + (__brev((unsigned)((((g * ek) & (M - 1)) - 1) >> 1)) >> (32 - logN));
+        const double e = u2d(ep[i][src]);
 #pragma unroll
         for (int j = 0; j < GM; j++) {
             if (j >= ng) break;
