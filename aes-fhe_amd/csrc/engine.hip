@@ -1998,6 +1998,8 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             ext.reset(new Tmp(e, (size_t)ks_beta(e, l) * B * neN));
             ks_modup(e, c1, cv.bs, B, l, ext->p);
         }
+        std::vector<const u64*> kd;
+        std::vector<u64*> ko;
         for (int i = 0; i < nb; i++) {
             E.emplace_back(new Tmp(e, (size_t)B * 2 * neN));
             if (!bkeys[i]) {
@@ -2005,8 +2007,19 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
                 HIPC(hipGetLastError());
                 continue;
             }
+            kd.push_back((const u64*)bkeys[i]->d);
+            ko.push_back(E.back()->p);
+        }
+        if (!kd.empty()) {
+            // every keyed baby's inner product in one launch (the extension read once from HBM);
             // stored unpermuted: the term kernel applies sigma_i as it reads (k_dot_pt_ext_multi)
-            ks_inner_acc(e, c1, cv.bs, ext->p, B, l, bkeys[i], c0, true, E.back()->p, false);
+            const int beta = ks_beta(e, l);
+            auto dk = upload_small(e, kd.data(), kd.size());
+            auto dko = upload_small(e, ko.data(), ko.size());
+            ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + kd.size() * (2.0 * beta + 2.0 * B)));
+            auto inner = beta <= 4 ? k_ks_inner_multi<4> : beta <= 8 ? k_ks_inner_multi<8> : k_ks_inner_multi<12>;
+            hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, c1, cv.bs, (const u64*)ext->p, neN, (long)B * neN, (const u64* const*)dk, (int)kd.size(), 2L * e->np * N, (long)e->np * N, (u64* const*)dko, 2 * neN, neN, B, beta, e->K, l, e->q, e->qinv, e->Lp1, c0, (const double*)e->pmodf, e->logN);
+            HIPC(hipGetLastError());
         }
     }
     // 2. giant parts: sum of plaintext products in Q_l u P (every giant in one pass over the

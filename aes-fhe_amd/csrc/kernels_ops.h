@@ -395,6 +395,66 @@ __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* _
     }
 }
 
+// Hoisted baby steps (aesfhe_linear_bsgs): the inner products of one extension with nk keys in
+// one launch -- accs[i] = sum_j ext_j (x) keys[i]_j (+ P * addend on the Q limbs, as
+// k_ks_inner_all with pmodf); the extension slice of a workgroup (beta * B words per lane) is
+// re-read per key from L2 instead of once per key launch from HBM.  grid (N/256, ne, 1)
+template <int BM>
+__global__ void k_ks_inner_multi(const u64* __restrict__ d, long dbs, const u64* __restrict__ ext,
+                                 long exs, long exj, const u64* const* __restrict__ keys, int nk, long kdig,
+                                 long kcomp, u64* const* __restrict__ accs, long abs_, long acs, int B,
+                                 int beta, int K, int l, const u64* __restrict__ qall,
+                                 const double* __restrict__ qinvall, int Lp1, Opnd addend,
+                                 const double* __restrict__ pmodf, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = blockIdx.y;
+    const int pid = t <= l ? t : Lp1 + (t - l - 1);
+    const double q = (double)qall[pid];
+    const double qi = qinvall[pid];
+    const int own = t <= l ? t / K : -1;
+    for (int i = 0; i < nk; i++) {
+        const u64* key = keys[i];
+        double kb[BM], ka[BM], kbq[BM], kaq[BM];
+#pragma unroll
+        for (int j = 0; j < BM; j++) {
+            kb[j] = ka[j] = kbq[j] = kaq[j] = 0.0;
+            if (j < beta) {
+                const long ko = (long)j * kdig + ((long)pid << logN) + k;
+                kb[j] = u2d(key[ko]);
+                ka[j] = u2d(key[ko + kcomp]);
+                kbq[j] = kb[j] * qi;
+                kaq[j] = ka[j] * qi;
+            }
+        }
+        u64* acc = accs[i];
+#pragma unroll 2
+        for (int bb = 0; bb < B; bb++) {
+            double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+            for (int j = 0; j < BM; j++) {
+                if (j < beta) {
+                    const double e = u2d((j == own) ? d[(long)bb * dbs + ((long)t << logN) + k]
+                                                    : ext[(long)j * exj + (long)bb * exs + ((long)t << logN) + k]);
+                    s0 += fmul_rem(e, kb[j], kbq[j], q);
+                    s1 += fmul_rem(e, ka[j], kaq[j], q);
+                    if ((j & 3) == 3) {
+                        s0 = fred(s0, q, qi);
+                        s1 = fred(s1, q, qi);
+                    }
+                }
+            }
+            if (pmodf && t <= l) {
+                const double f = pmodf[t], w = tw_w(f, q);
+                s0 = fred(s0, q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 0, t, k, logN)), w, f, q);
+                s1 = fred(s1, q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, k, logN)), w, f, q);
+            }
+            u64* a0 = acc + (long)bb * abs_ + ((long)t << logN) + k;
+            a0[0] = fcanon(s0, q, qi);
+            a0[acs] = fcanon(s1, q, qi);
+        }
+    }
+}
+
 // ModDown base conversion from the dropped limbs E = {q_{l-r+1}..q_l, p_0..p_{K-1}} (acc limbs
 // l-r+1 .. l+K, already in coefficient form) to the kept limbs q_0..q_{l-r}; r = 0 is the plain
 // ModDown by P, r >= 1 the combined ModDown + rescale by D = P q_l ... q_{l-r+1}:
