@@ -2057,7 +2057,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             auto dso = upload_small(e, so.data(), so.size());
             {
                 ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (nb + gn) + terms));
-                hipLaunchKernelGGL(k_dot_pt_ext_multi<kGM>, dim3(N / 256, ne, B * 2), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64*)dgal, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, e->q, e->qinv, e->Lp1, e->logN);
+                hipLaunchKernelGGL(k_dot_pt_ext_multi<kGM>, dim3((ne * B * 2 + 7) / 8 * 8 * (N / 256)), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64*)dgal, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, e->q, e->qinv, e->Lp1, e->logN, ne * B * 2);
             }
             HIPC(hipGetLastError());
             for (int j = 0; j < gn; j++) {

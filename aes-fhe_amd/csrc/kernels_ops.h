@@ -971,9 +971,17 @@ __global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64*
                                    const u64* const* __restrict__ pt, int nb,
                                    int ng, u64* const* __restrict__ outs, int l, int ne,
                                    const u64* __restrict__ qall, const double* __restrict__ qinvall, int Lp1,
-                                   int logN) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int t = blockIdx.y, bb = blockIdx.z >> 1, c = blockIdx.z & 1;
+                                   int logN, int nlimb) {
+    // 1-D grid, XCD-local limbs: block id -> (x = id & 7, w = id >> 3); limb = (w >> kb) * 8 + x,
+    // k-block = w & (2^kb - 1) -- all blocks of one limb run on one XCD (ids x, x + 8, ...), so the
+    // automorphism's gather over the limb stays in that XCD's L2 (dealt over 8 XCDs, every XCD
+    // would fetch the whole limb)
+    const int kbits = logN - 8;
+    const int x8 = blockIdx.x & 7, w = blockIdx.x >> 3;
+    const int limb = ((w >> kbits) << 3) + x8;
+    if (limb >= nlimb) return;  // nlimb = ne * B * 2
+    const int k = ((w & ((1 << kbits) - 1)) << 8) + threadIdx.x;
+    const int t = limb % ne, bc = limb / ne, bb = bc >> 1, c = bc & 1;
     const int pid = ext_pid(t, l, Lp1);
     const double q = (double)qall[pid], qi = qinvall[pid];
     const long base = (((long)bb * 2 + c) * ne + t) << logN, off = base + k, po = ((long)t << logN) + k;
