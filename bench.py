@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=16, help="ciphertext sets per GPU per step")
+    ap.add_argument("--batch", type=int, default=32, help="ciphertext sets per GPU per step (8192 blocks each)")
     ap.add_argument("--layout", choices=("rows", "bytes"), default="rows")
     ap.add_argument("--log-n", type=int, default=16)
     ap.add_argument("--max-level", type=int, default=30)
@@ -277,6 +277,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    round_pool = eng.pool_stats()
     ok = None
     if args.check:
         got = R.decrypt(out)
@@ -319,7 +320,7 @@ def main():
                 "log_n": args.log_n, "max_level": args.max_level, "special_primes": 8,
                 "ciphertext_sets_per_gpu": args.batch, "blocks_per_gpu_per_step": args.batch * R.n_blk,
                 "parallelism": f"ciphertext-batch sharding x{world} (no data-path collective)",
-                "verified": ok,
+                "verified": ok, "pool_after_round": round_pool,
             },
             "roofline": {
                 "bound": "hbm", "kernel": "ntt (k_nttf_*_cols / k_nttf_*_rows pass launches)",
