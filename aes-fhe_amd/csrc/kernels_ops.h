@@ -305,35 +305,6 @@ __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ 
     }
 }
 
-// acc[b][c][t] (+)= e[b][t] * key_c[pid(t)], e = d (own digit limbs, NTT) or ext (others)
-// grid (N/256, ne, 1); loops over the batch so each key word is read once
-__global__ void k_ks_inner(const u64* __restrict__ d, long dbs, const u64* __restrict__ ext,
-                           long exs, const u64* __restrict__ kb, const u64* __restrict__ ka,
-                           u64* __restrict__ acc, long abs_, long acs, int B, int lo, int hi,
-                           int l, const u64* __restrict__ qall, const double* __restrict__ qinvall,
-                           int Lp1, int first, int logN) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int t = blockIdx.y;
-    const int pid = t <= l ? t : Lp1 + (t - l - 1);
-    const u64 q = qall[pid];
-    const double qi = qinvall[pid];
-    const u64 vb = kb[((long)pid << logN) + k], va = ka[((long)pid << logN) + k];
-    const bool own = t >= lo && t < hi;
-    for (int bb = 0; bb < B; bb++) {
-        u64 e = own ? d[(long)bb * dbs + ((long)t << logN) + k] : ext[(long)bb * exs + ((long)t << logN) + k];
-        u64* a0 = acc + (long)bb * abs_ + ((long)t << logN) + k;
-        u64* a1 = a0 + acs;
-        u64 m0 = mul_m(e, vb, q, qi), m1 = mul_m(e, va, q, qi);
-        if (first) {
-            *a0 = m0;
-            *a1 = m1;
-        } else {
-            *a0 = add_m(*a0, m0, q);
-            *a1 = add_m(*a1, m1, q);
-        }
-    }
-}
-
 // All digits at once: acc[b][c][t] = sum_j e_j[b][t] * key_j,c[pid(t)], e_j = d (limbs of digit
 // j, NTT) or ext_j (other limbs).  key layout [dnum][2][np][N]; ext layout [beta][B][ne][N].
 // grid (N/256, ne, 1); loops over the batch so each key word is read once per batch.
@@ -885,7 +856,7 @@ __global__ void k_dot_pt(const u64* const* __restrict__ cp, const long* __restri
     const long off = ((long)l << logN) + k;
     double acc = 0.0;
     int i = 0;
-    for (; i + 8 <= n; i += 8) {  // chunks of 8 loads in flight (see k_dot_pt_ext)
+    for (; i + 8 <= n; i += 8) {  // chunks of 8 loads in flight: one HBM round trip per chunk
         double cv[8], wv[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
@@ -923,41 +894,6 @@ __global__ void k_scale_p_ext(Opnd in, u64* __restrict__ out, int l, int ne, con
         v = fcanon(fmul_rem(u2d(opnd_get(in, bb, c, t, k, logN)), tw_w(f, q), f, q), q, qi);
     }
     out[((((long)bb * 2 + c) * ne + t) << logN) + k] = v;
-}
-
-// out[b][c][t] = sum_i pt_i[t] * E_i[b][c][t] over the ne limbs of Q_l u P (E_i, out: [B][2][ne][N];
-// pt_i: ne limbs).  grid (N/256, ne, B*2)
-__global__ void k_dot_pt_ext(const u64* const* __restrict__ ep, const u64* const* __restrict__ pp, int n,
-                             u64* __restrict__ out, int l, int ne, const u64* __restrict__ qall,
-                             const double* __restrict__ qinvall, int Lp1, int logN) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int t = blockIdx.y, bb = blockIdx.z >> 1, c = blockIdx.z & 1;
-    const int pid = ext_pid(t, l, Lp1);
-    const double q = (double)qall[pid], qi = qinvall[pid];
-    const long off = ((((long)bb * 2 + c) * ne + t) << logN) + k, po = ((long)t << logN) + k;
-    // terms in chunks of 8 with every load of a chunk issued before its products: one HBM round
-    // trip per chunk instead of per term (the loop was latency-bound at 3-5x below bandwidth)
-    double acc = 0.0;
-    int i = 0;
-    for (; i + 8 <= n; i += 8) {
-        double ev[8], wv[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            ev[u] = u2d(ep[i + u][off]);
-            wv[u] = u2d(pp[i + u][po]);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            acc += fmul_rem(ev[u], wv[u], wv[u] * qi, q);
-            if ((u & 3) == 3) acc = fred(acc, q, qi);
-        }
-    }
-    for (; i < n; i++) {
-        const double w = u2d(pp[i][po]);
-        acc += fmul_rem(u2d(ep[i][off]), w, w * qi, q);
-        if ((i & 3) == 3) acc = fred(acc, q, qi);
-    }
-    out[off] = fcanon(acc, q, qi);
 }
 
 // All giants of a BSGS map in one pass over the babies: outs[j][b][c][t] = sum_i pt[j][i][t] *
