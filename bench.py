@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--max-level", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="decrypt and verify against FIPS-197")
+    ap.add_argument("--aes10-ppc", type=int, default=0,
+                    help="bit-ciphertext pairs per bootstrap call (0: 32 / aes10-batch)")
     ap.add_argument("--aes10-batch", type=int, default=8,
                     help="ciphertext sets for the full 10-round AES-128 measurement (0: skip)")
     return ap.parse_args()
@@ -133,7 +135,7 @@ def aes128_full(args, eng, drv, rank, barrier, dist):
     keys = [R.encrypt_round_key(rk) for rk in T.expand_key(key)]
     rng = np.random.default_rng(2000 + rank)
     nb = args.aes10_batch
-    ppc = max(1, 32 // nb)  # ~32 ciphertexts per Bootstrapper call
+    ppc = args.aes10_ppc or max(1, 32 // nb)  # ~32 ciphertexts per Bootstrapper call
     # warm-up of the same shape: materialises the bootstrap plaintexts and fills the device pool
     # with every buffer size of the run, so the timed run makes no hipMalloc
     warm = R.encrypt_aes128(R.encrypt_blocks(rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)),
