@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--layout", choices=("rows", "bytes"), default="rows")
     ap.add_argument("--log-n", type=int, default=16)
     ap.add_argument("--max-level", type=int, default=30)
+    ap.add_argument("--special-primes", type=int, default=10,
+                    help="K special primes = key-switch digit size alpha (dnum = ceil((L+1)/K))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="decrypt and verify against FIPS-197")
     ap.add_argument("--aes10-ppc", type=int, default=0,
@@ -107,7 +109,7 @@ class RoundDriver:
 
 def setup_engine(args, device):
     from aes_xor_fhe.fhe import Engine
-    eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=8, device_id=device)
+    eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes, device_id=device)
     sk = eng.create_secret_key(1)
     pk = eng.create_public_key(sk)
     rlk = eng.create_relinearization_key(sk)
@@ -190,7 +192,7 @@ def cpu_baseline(args):
     threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
     times = {}
     for log_n in (12, args.log_n):
-        eng = Engine(log_n=log_n, max_level=args.max_level, special_primes=8, thread_count=threads, _lib=lib)
+        eng = Engine(log_n=log_n, max_level=args.max_level, special_primes=args.special_primes, thread_count=threads, _lib=lib)
         sk = eng.create_secret_key(1)
         pk = eng.create_public_key(sk)
         R = RoundDriver(args.layout, eng, sk, pk, eng.create_relinearization_key(sk),
@@ -319,7 +321,7 @@ def main():
                              "polynomial over nibble-bit monomials, bit-domain MixColumns/AddRoundKey" if args.layout == "rows"
                              else "nibble-domain Zeta-16 LUTs, byte-major SIMD packing")),
                 "layout": args.layout,
-                "log_n": args.log_n, "max_level": args.max_level, "special_primes": 8,
+                "log_n": args.log_n, "max_level": args.max_level, "special_primes": args.special_primes,
                 "ciphertext_sets_per_gpu": args.batch, "blocks_per_gpu_per_step": args.batch * R.n_blk,
                 "parallelism": f"ciphertext-batch sharding x{world} (no data-path collective)",
                 "verified": ok, "pool_after_round": round_pool,

@@ -127,9 +127,11 @@ def test_batched_ops_bit_exact(product_lib, oracle_lib, gpu_available):
     np.testing.assert_allclose(dec, zb * zb[0], atol=1e-5)
 
 
-def test_full_params_mul_bit_exact(product_lib, oracle_lib, gpu_available):
-    """BASELINE.json's parameter set: N = 2^16, L = 30 (one ct x ct multiply + rotation)."""
-    kw = dict(log_n=16, max_level=30, special_primes=8, seed=99)
+@pytest.mark.parametrize("k", [8, 10], ids=["K8", "K10"])
+def test_full_params_mul_bit_exact(product_lib, oracle_lib, gpu_available, k):
+    """BASELINE.json's parameter set: N = 2^16, L = 30 (one ct x ct multiply + rotation), with
+    K = 8 (dnum 4) and the bench's K = 10 (dnum 3, alpha 10)."""
+    kw = dict(log_n=16, max_level=30, special_primes=k, seed=99)
     g, o = _pair(product_lib, oracle_lib, **kw)
     kg, ko = _keys(g), _keys(o)
     rng = np.random.default_rng(3)
@@ -219,8 +221,9 @@ def test_mul_fma_and_mixed_lincomb_bit_exact(product_lib, oracle_lib, gpu_availa
         _same(g, o, cg, co)
 
 
-@pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=3, special_primes=2, seed=5)],
-                         ids=["n4096", "n65536"])
+@pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=3, special_primes=2, seed=5),
+                                dict(log_n=16, max_level=12, special_primes=10, seed=5)],
+                         ids=["n4096", "n65536", "n65536K10"])
 def test_linear_bsgs_bit_exact(product_lib, oracle_lib, gpu_available, kw):
     """aesfhe_linear_bsgs (hoisted babies and lazy ModDown; at N = 2^16 the giants go through the
     fused ext-NTT row pass with accumulation) against the oracle's restatement, and its slots
