@@ -2017,7 +2017,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             auto dk = upload_small(e, kd.data(), kd.size());
             auto dko = upload_small(e, ko.data(), ko.size());
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + kd.size() * (2.0 * beta + 2.0 * B)));
-            auto inner = beta <= 4 ? k_ks_inner_multi<4> : beta <= 8 ? k_ks_inner_multi<8> : k_ks_inner_multi<12>;
+            auto inner = beta <= 4 ? k_ks_inner_multi<4, 4> : beta <= 8 ? k_ks_inner_multi<8, 2> : k_ks_inner_multi<12, 1>;
             hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, c1, cv.bs, (const u64*)ext->p, neN, (long)B * neN, (const u64* const*)dk, (int)kd.size(), 2L * e->np * N, (long)e->np * N, (u64* const*)dko, 2 * neN, neN, B, beta, e->K, l, e->q, e->qinv, e->Lp1, c0, (const double*)e->pmodf, e->logN);
             HIPC(hipGetLastError());
         }
@@ -2057,7 +2057,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             auto dso = upload_small(e, so.data(), so.size());
             {
                 ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (nb + gn) + terms));
-                hipLaunchKernelGGL(k_dot_pt_ext_multi<kGM>, dim3((ne * B * 2 + 7) / 8 * 8 * (N / 256)), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64*)dgal, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, e->q, e->qinv, e->Lp1, e->logN, ne * B * 2);
+                hipLaunchKernelGGL(k_dot_pt_ext_multi<kGM>, dim3((ne * (N / 256) + 7) / 8 * 8 * (B * 2)), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64*)dgal, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, e->q, e->qinv, e->Lp1, e->logN, B * 2);
             }
             HIPC(hipGetLastError());
             for (int j = 0; j < gn; j++) {

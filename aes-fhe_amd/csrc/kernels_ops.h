@@ -368,9 +368,11 @@ __global__ void k_ks_inner_all(const u64* __restrict__ d, long dbs, const u64* _
 
 // Hoisted baby steps (aesfhe_linear_bsgs): the inner products of one extension with nk keys in
 // one launch -- accs[i] = sum_j ext_j (x) keys[i]_j (+ P * addend on the Q limbs, as
-// k_ks_inner_all with pmodf); the extension slice of a workgroup (beta * B words per lane) is
-// re-read per key from L2 instead of once per key launch from HBM.  grid (N/256, ne, 1)
-template <int BM>
+// k_ks_inner_all with pmodf).  Keys are taken KC at a time into registers and the batch loop
+// runs inside, so the extension slice of a workgroup (beta * B words per lane, 256 KB at B = 32:
+// far beyond what L2 keeps per workgroup) is read ceil(nk / KC) times instead of nk times (it
+// came from HBM every time: 7 ms per CtS call at 15 keys).  grid (N/256, ne, 1)
+template <int BM, int KC>
 __global__ void k_ks_inner_multi(const u64* __restrict__ d, long dbs, const u64* __restrict__ ext,
                                  long exs, long exj, const u64* const* __restrict__ keys, int nk, long kdig,
                                  long kcomp, u64* const* __restrict__ accs, long abs_, long acs, int B,
@@ -383,45 +385,58 @@ __global__ void k_ks_inner_multi(const u64* __restrict__ d, long dbs, const u64*
     const double q = (double)qall[pid];
     const double qi = qinvall[pid];
     const int own = t <= l ? t / K : -1;
-    for (int i = 0; i < nk; i++) {
-        const u64* key = keys[i];
-        double kb[BM], ka[BM], kbq[BM], kaq[BM];
+    const bool pm = pmodf && t <= l;
+    const double f = pm ? pmodf[t] : 0.0, fw = pm ? tw_w(f, q) : 0.0;
+    for (int i0 = 0; i0 < nk; i0 += KC) {
+        double kb[KC][BM], ka[KC][BM];
 #pragma unroll
-        for (int j = 0; j < BM; j++) {
-            kb[j] = ka[j] = kbq[j] = kaq[j] = 0.0;
-            if (j < beta) {
-                const long ko = (long)j * kdig + ((long)pid << logN) + k;
-                kb[j] = u2d(key[ko]);
-                ka[j] = u2d(key[ko + kcomp]);
-                kbq[j] = kb[j] * qi;
-                kaq[j] = ka[j] * qi;
-            }
-        }
-        u64* acc = accs[i];
-#pragma unroll 2
-        for (int bb = 0; bb < B; bb++) {
-            double s0 = 0.0, s1 = 0.0;
+        for (int ii = 0; ii < KC; ii++) {
 #pragma unroll
             for (int j = 0; j < BM; j++) {
-                if (j < beta) {
-                    const double e = u2d((j == own) ? d[(long)bb * dbs + ((long)t << logN) + k]
-                                                    : ext[(long)j * exj + (long)bb * exs + ((long)t << logN) + k]);
-                    s0 += fmul_rem(e, kb[j], kbq[j], q);
-                    s1 += fmul_rem(e, ka[j], kaq[j], q);
-                    if ((j & 3) == 3) {
-                        s0 = fred(s0, q, qi);
-                        s1 = fred(s1, q, qi);
-                    }
+                kb[ii][j] = ka[ii][j] = 0.0;
+                if (i0 + ii < nk && j < beta) {
+                    const long ko = (long)j * kdig + ((long)pid << logN) + k;
+                    kb[ii][j] = u2d(keys[i0 + ii][ko]);
+                    ka[ii][j] = u2d(keys[i0 + ii][ko + kcomp]);
                 }
             }
-            if (pmodf && t <= l) {
-                const double f = pmodf[t], w = tw_w(f, q);
-                s0 = fred(s0, q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 0, t, k, logN)), w, f, q);
-                s1 = fred(s1, q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, k, logN)), w, f, q);
+        }
+#pragma unroll 1
+        for (int bb = 0; bb < B; bb++) {
+            double e[BM];
+#pragma unroll
+            for (int j = 0; j < BM; j++)
+                e[j] = j < beta ? u2d((j == own) ? d[(long)bb * dbs + ((long)t << logN) + k]
+                                                 : ext[(long)j * exj + (long)bb * exs + ((long)t << logN) + k])
+                                : 0.0;
+            double ad0 = 0.0, ad1 = 0.0;
+            if (pm) {
+                ad0 = fmul_rem(u2d(opnd_get(addend, bb, 0, t, k, logN)), fw, f, q);
+                ad1 = fmul_rem(u2d(opnd_get(addend, bb, 1, t, k, logN)), fw, f, q);
             }
-            u64* a0 = acc + (long)bb * abs_ + ((long)t << logN) + k;
-            a0[0] = fcanon(s0, q, qi);
-            a0[acs] = fcanon(s1, q, qi);
+#pragma unroll
+            for (int ii = 0; ii < KC; ii++) {
+                if (i0 + ii >= nk) break;
+                double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+                for (int j = 0; j < BM; j++) {
+                    if (j < beta) {
+                        s0 += fmul_rem(e[j], kb[ii][j], kb[ii][j] * qi, q);
+                        s1 += fmul_rem(e[j], ka[ii][j], ka[ii][j] * qi, q);
+                        if ((j & 3) == 3) {
+                            s0 = fred(s0, q, qi);
+                            s1 = fred(s1, q, qi);
+                        }
+                    }
+                }
+                if (pm) {
+                    s0 = fred(s0, q, qi) + ad0;
+                    s1 = fred(s1, q, qi) + ad1;
+                }
+                u64* a0 = accs[i0 + ii] + (long)bb * abs_ + ((long)t << logN) + k;
+                a0[0] = fcanon(s0, q, qi);
+                a0[acs] = fcanon(s1, q, qi);
+            }
         }
     }
 }
@@ -907,17 +922,19 @@ __global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64*
                                    const u64* const* __restrict__ pt, int nb,
                                    int ng, u64* const* __restrict__ outs, int l, int ne,
                                    const u64* __restrict__ qall, const double* __restrict__ qinvall, int Lp1,
-                                   int logN, int nlimb) {
-    // 1-D grid, XCD-local limbs: block id -> (x = id & 7, w = id >> 3); limb = (w >> kb) * 8 + x,
-    // k-block = w & (2^kb - 1) -- all blocks of one limb run on one XCD (ids x, x + 8, ...), so the
-    // automorphism's gather over the limb stays in that XCD's L2 (dealt over 8 XCDs, every XCD
-    // would fetch the whole limb)
+                                   int logN, int nbc) {
+    // 1-D grid, XCD-local plaintext rows: block id -> (x = id & 7, w = id >> 3); pair (limb t,
+    // 256-word k-block) = (w / nbc) * 8 + x, bc = (b, c) = w % nbc -- the nbc = 2B workgroups that
+    // share one pair's plaintext words (nb * ng rows of 2 KB) run back to back on one XCD, so the
+    // plaintexts come from HBM once instead of once per ciphertext (dealt over XCDs by limb, the
+    // 1.3 GB of CtS plaintexts were re-read from HBM by every bc).  The automorphism gather of a
+    // k-block reads exactly one 2 KB row of the baby (its high index byte is fixed by the block).
     const int kbits = logN - 8;
     const int x8 = blockIdx.x & 7, w = blockIdx.x >> 3;
-    const int limb = ((w >> kbits) << 3) + x8;
-    if (limb >= nlimb) return;  // nlimb = ne * B * 2
-    const int k = ((w & ((1 << kbits) - 1)) << 8) + threadIdx.x;
-    const int t = limb % ne, bc = limb / ne, bb = bc >> 1, c = bc & 1;
+    const int pair = (w / nbc) * 8 + x8, bc = w % nbc;
+    if (pair >= (ne << kbits)) return;
+    const int t = pair >> kbits, k = ((pair & ((1 << kbits) - 1)) << 8) + threadIdx.x;
+    const int bb = bc >> 1, c = bc & 1;
     const int pid = ext_pid(t, l, Lp1);
     const double q = (double)qall[pid], qi = qinvall[pid];
     const long base = (((long)bb * 2 + c) * ne + t) << logN, off = base + k, po = ((long)t << logN) + k;

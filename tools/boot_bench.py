@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--log-n", type=int, default=16)
     ap.add_argument("--max-level", type=int, default=30)
     ap.add_argument("--scale-bits", type=int, default=44)
+    ap.add_argument("--special-primes", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--general", action="store_true")
     ap.add_argument("--batch", type=int, default=1, help="ciphertext pairs per call")
@@ -28,7 +29,7 @@ def main():
     ap.add_argument("--baby-scale", type=int, default=2, help="BSGS baby steps x this (lazy mode)")
     ap.add_argument("--eager", action="store_true", help="rotate_hoisted + dot_pt + galois linear maps")
     a = ap.parse_args()
-    e = Engine(log_n=a.log_n, max_level=a.max_level, special_primes=8, scale_bits=a.scale_bits, seed=3)
+    e = Engine(log_n=a.log_n, max_level=a.max_level, special_primes=a.special_primes, scale_bits=a.scale_bits, seed=3)
     sk = e.create_secret_key(1)
     pk = e.create_public_key(sk)
     t = time.time()
@@ -49,7 +50,7 @@ def main():
         ts.append(time.time() - t)
     err = max(np.abs(np.atleast_2d(e.decrypt(y, sk)) - b).max() for y, b in zip((ya, yb), bits))
     print(json.dumps({"mode": "bits", "log_n": a.log_n, "max_level": a.max_level,
-                      "scale_bits": a.scale_bits, "setup_s": round(setup, 2),
+                      "special_primes": a.special_primes, "scale_bits": a.scale_bits, "setup_s": round(setup, 2),
                       "ms_per_call": round(1e3 * min(ts), 1), "cts_per_call": 2 * a.batch,
                       "ms_per_ct": round(1e3 * min(ts) / (2 * a.batch), 2),
                       "out_level": ya.level, "max_err": float(err),
