@@ -917,54 +917,68 @@ __global__ void k_scale_p_ext(Opnd in, u64* __restrict__ out, int l, int ne, con
 // GM: accumulators held in registers (ng <= GM).  grid (N/256, ne, B*2)
 // gal[i] > 1: baby i is stored unpermuted and sigma_{gal[i]} is applied by the read (the NTT-slot
 // gather of k_galois), so the permuted copy of each baby is never written.
-template <int GM>
+template <int GM, int BCT>
 __global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64* __restrict__ gal,
                                    const u64* const* __restrict__ pt, int nb,
                                    int ng, u64* const* __restrict__ outs, int l, int ne,
                                    const u64* __restrict__ qall, const double* __restrict__ qinvall, int Lp1,
                                    int logN, int nbc) {
     // 1-D grid, XCD-local plaintext rows: block id -> (x = id & 7, w = id >> 3); pair (limb t,
-    // 256-word k-block) = (w / nbc) * 8 + x, bc = (b, c) = w % nbc -- the nbc = 2B workgroups that
-    // share one pair's plaintext words (nb * ng rows of 2 KB) run back to back on one XCD, so the
-    // plaintexts come from HBM once instead of once per ciphertext (dealt over XCDs by limb, the
-    // 1.3 GB of CtS plaintexts were re-read from HBM by every bc).  The automorphism gather of a
-    // k-block reads exactly one 2 KB row of the baby (its high index byte is fixed by the block).
-    const int kbits = logN - 8;
+    // 256-word k-block) = (w / ng_) * 8 + x, bc group = w % ng_ (ng_ = nbc / BCT groups of BCT
+    // (b, c) polynomials) -- the workgroups that share one pair's plaintext words (nb * ng rows of
+    // 2 KB) run back to back on one XCD, so the plaintexts come from HBM once instead of once per
+    // ciphertext (dealt over XCDs by limb, the 1.3 GB of CtS plaintexts were re-read from HBM by
+    // every bc), and each plaintext word loaded serves BCT polynomials (the L2 -> CU load count per
+    // baby word drops from 1 + ng to 1 + ng / BCT).  The automorphism gather of a k-block reads
+    // exactly one 2 KB row of the baby (its high index byte is fixed by the block).
+    const int kbits = logN - 8, ngrp = nbc / BCT;
     const int x8 = blockIdx.x & 7, w = blockIdx.x >> 3;
-    const int pair = (w / nbc) * 8 + x8, bc = w % nbc;
+    const int pair = (w / ngrp) * 8 + x8, bc0 = (w % ngrp) * BCT;
     if (pair >= (ne << kbits)) return;
     const int t = pair >> kbits, k = ((pair & ((1 << kbits) - 1)) << 8) + threadIdx.x;
-    const int bb = bc >> 1, c = bc & 1;
     const int pid = ext_pid(t, l, Lp1);
     const double q = (double)qall[pid], qi = qinvall[pid];
-    const long base = (((long)bb * 2 + c) * ne + t) << logN, off = base + k, po = ((long)t << logN) + k;
+    const long po = ((long)t << logN) + k;
+    long base[BCT];
+#pragma unroll
+    for (int u = 0; u < BCT; u++) base[u] = ((long)(bc0 + u) * ne + t) << logN;  // bc = 2 b + c
     const u64 M = 2ULL << logN;
     const u64 ek = 2 * (u64)(__brev((unsigned)k) >> (32 - logN)) + 1;
-    double acc[GM];
+    double acc[BCT][GM];
 #pragma unroll
-    for (int j = 0; j < GM; j++) acc[j] = 0.0;
+    for (int u = 0; u < BCT; u++)
+#pragma unroll
+        for (int j = 0; j < GM; j++) acc[u][j] = 0.0;
     for (int i = 0; i < nb; i++) {
         const u64 g = gal[i];
-        long src = off;
-        if (g > 1) src = base + (__brev((unsigned)((((g * ek) & (M - 1)) - 1) >> 1)) >> (32 - logN));
-        const double e = u2d(ep[i][src]);
+        long src = k;
+        if (g > 1) src = __brev((unsigned)((((g * ek) & (M - 1)) - 1) >> 1)) >> (32 - logN);
+        double e[BCT];
+#pragma unroll
+        for (int u = 0; u < BCT; u++) e[u] = u2d(ep[i][base[u] + src]);
 #pragma unroll
         for (int j = 0; j < GM; j++) {
             if (j >= ng) break;
             const u64* p = pt[j * nb + i];
             if (p) {
-                const double w = u2d(p[po]);
-                acc[j] += fmul_rem(e, w, w * qi, q);
+                const double wv = u2d(p[po]), wq = wv * qi;
+#pragma unroll
+                for (int u = 0; u < BCT; u++) acc[u][j] += fmul_rem(e[u], wv, wq, q);
             }
         }
         if ((i & 3) == 3) {
 #pragma unroll
-            for (int j = 0; j < GM; j++) acc[j] = fred(acc[j], q, qi);
+            for (int u = 0; u < BCT; u++)
+#pragma unroll
+                for (int j = 0; j < GM; j++) acc[u][j] = fred(acc[u][j], q, qi);
         }
     }
 #pragma unroll
     for (int j = 0; j < GM; j++)
-        if (j < ng) outs[j][off] = fcanon(acc[j], q, qi);
+        if (j < ng) {
+#pragma unroll
+            for (int u = 0; u < BCT; u++) outs[j][base[u] + k] = fcanon(acc[u][j], q, qi);
+        }
 }
 
 }  // namespace aesfhe
