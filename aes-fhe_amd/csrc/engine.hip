@@ -201,6 +201,10 @@ struct aesfhe_engine {
     u64 seed;
     Chain chain;
     hipStream_t stream;
+    // key-switch ModUp pipelining (AESFHE_KS_STREAMS): the ext column passes run on stream2 while
+    // the next digit's base conversion runs on stream (kKsEv fork / join events, no timing)
+    hipStream_t stream2 = nullptr;
+    hipEvent_t kev[16] = {};
     Pool pool;
     // device tables
     u64 *q, *psi, *ipsi, *ninv;
@@ -281,17 +285,27 @@ struct aesfhe_pt {
 static const int FAM_NTT = 0, FAM_KS = 1, FAM_EW = 2;
 static const int kMdrMaxR = 2, kMdrMaxE = 16;  // combined ModDown + rescale: r <= 2, K + r <= 16
 
+static bool ks_streams_on() {
+    static const bool on = [] {
+        const char* s = getenv("AESFHE_KS_STREAMS");
+        return s && atoi(s) > 0;
+    }();
+    return on;
+}
+
 struct ProfScope {
     aesfhe_engine* e;
     int fam;
     double bytes;
     hipEvent_t a = nullptr, b = nullptr;
+    hipStream_t s;
     bool on;
-    ProfScope(aesfhe_engine* e_, int f, double by) : e(e_), fam(f), bytes(by), on((e_->prof >> f) & 1) {
+    ProfScope(aesfhe_engine* e_, int f, double by, hipStream_t s_ = nullptr)
+        : e(e_), fam(f), bytes(by), s(s_ ? s_ : e_->stream), on((e_->prof >> f) & 1) {
         if (!on) return;
         a = take();
         b = take();
-        hipEventRecord(a, e->stream);
+        hipEventRecord(a, s);
     }
     hipEvent_t take() {
         if (!e->spare.empty()) {
@@ -305,7 +319,7 @@ struct ProfScope {
     }
     ~ProfScope() {
         if (!on) return;
-        hipEventRecord(b, e->stream);
+        hipEventRecord(b, s);
         e->recs.push_back({fam, a, b, bytes});
     }
 };
@@ -313,6 +327,11 @@ struct ProfScope {
 static void prof_flush(aesfhe_engine* e) {
     if (e->recs.empty()) return;
     hipStreamSynchronize(e->stream);
+    if (e->stream2) {
+        hipStreamSynchronize(e->stream2);
+        for (auto ev : e->kev) hipEventDestroy(ev);
+        hipStreamDestroy(e->stream2);
+    }
     for (auto& r : e->recs) {
         float ms = 0;
         hipEventElapsedTime(&ms, r.a, r.b);
@@ -755,6 +774,10 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
         if (x >> 50) throw_err(AESFHE_EARG, "prime %llu exceeds 2^50", (unsigned long long)x);
     HIPC(hipSetDevice(e->device));
     HIPC(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    if (ks_streams_on()) {
+        HIPC(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+        for (auto& ev : e->kev) HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
     build_tables(e.get());
     {
         size_t fr = 0, tot = 0;
@@ -786,6 +809,11 @@ extern "C" void aesfhe_engine_destroy(aesfhe_engine* e) {
 static void engine_teardown(aesfhe_engine* e) {
     hipSetDevice(e->device);
     hipStreamSynchronize(e->stream);
+    if (e->stream2) {
+        hipStreamSynchronize(e->stream2);
+        for (auto ev : e->kev) hipEventDestroy(ev);
+        hipStreamDestroy(e->stream2);
+    }
     for (auto& r : e->recs) {
         hipEventDestroy(r.a);
         hipEventDestroy(r.b);
@@ -1624,6 +1652,10 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
     // 1. INTT copy of the input
     Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1), sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
     ntt(e, sd, sdc, B * (l + 1), true);
+    // pipelined (stream2): the column passes of digit j overlap digit j + 1's base conversion
+    // (HBM-bound next to VALU-bound); joined back into e->stream before dc is released
+    const bool two = cols_only && e->stream2 && beta + 1 <= (int)(sizeof(e->kev) / sizeof(e->kev[0]));
+    hipStream_t cs = two ? e->stream2 : e->stream;
     for (int j = 0; j < beta; j++) {
         const int lo = j * K, hi = std::min(lo + K, l + 1), alpha = hi - lo;
         const size_t set = (size_t)j * K + (alpha - 1);
@@ -1636,16 +1668,24 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
                                e->np, e->q, e->qinv, e->Lp1, e->logN);
         }
         HIPC(hipGetLastError());
+        if (two) {
+            HIPC(hipEventRecord(e->kev[j], e->stream));
+            HIPC(hipStreamWaitEvent(e->stream2, e->kev[j], 0));
+        }
         auto fwd = [&](Span sp, int total) {
             if (!cols_only) return ntt(e, sp, sp, total, false);
-            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
-            hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, sp, sp, e->tabs());
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, cs);
+            hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, cs, sp, sp, e->tabs());
         };
         if (lo > 0) fwd(span_s(exj, neN, lo, lo, 0, e->Lp1), B * lo);
         {
             int nrest = ne - hi, nq_rest = (l + 1) - hi;
             fwd(span_s(exj + (long)hi * N, neN, nrest, nq_rest, hi, e->Lp1), B * nrest);
         }
+    }
+    if (two) {
+        HIPC(hipEventRecord(e->kev[beta], e->stream2));
+        HIPC(hipStreamWaitEvent(e->stream, e->kev[beta], 0));
     }
 }
 
@@ -2059,7 +2099,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
                 ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (nb + gn) + terms));
                 // two (b, c) polynomials per workgroup (four measured the same: 153.7 vs 153.3 ms per
                 // B = 16 bit bootstrap, 162.7 with one)
-                hipLaunchKernelGGL(k_dot_pt_ext_multi<kGM, 2>, dim3((ne * (N / 256) + 7) / 8 * 8 * B), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64*)dgal, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, e->q, e->qinv, e->Lp1, e->logN, B * 2);
+                hipLaunchKernelGGL((k_dot_pt_ext_multi<kGM, 2>), dim3((ne * (N / 256) + 7) / 8 * 8 * B), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64*)dgal, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, e->q, e->qinv, e->Lp1, e->logN, B * 2);
             }
             HIPC(hipGetLastError());
             for (int j = 0; j < gn; j++) {
