@@ -430,6 +430,36 @@ __global__ void k_copy16x4(const ulonglong2* __restrict__ a, ulonglong2* __restr
     for (int u = 0; u < 4; u++) b[i + u * blockDim.x] = v[u];
 }
 
+// Infinity-Cache experiment: one workgroup moves a whole limb src -> mid -> dst with a barrier in
+// between (the data movement of a one-workgroup-per-limb NTT whose transpose goes through
+// memory).  MODE 0: mid = a per-workgroup slot (reused, stays on-die if anything does); 1: mid =
+// a separate buffer per limb; 2: mid = dst itself (in place).
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_copy_mid(const ulonglong2* __restrict__ a, ulonglong2* mid,
+                                                   ulonglong2* b, int limbs, int half) {
+    for (int y = blockIdx.x; y < limbs; y += gridDim.x) {
+        const ulonglong2* s = a + (long)y * half;
+        ulonglong2* d = b + (long)y * half;
+        ulonglong2* m = MODE == 0 ? mid + (long)blockIdx.x * half : MODE == 1 ? mid + (long)y * half : d;
+        for (int e = threadIdx.x; e < half; e += 4096) {
+            ulonglong2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = s[e + u * 1024];
+#pragma unroll
+            for (int u = 0; u < 4; u++) m[e + u * 1024] = v[u];
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < half; e += 4096) {
+            ulonglong2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = m[(e + u * 1024) ^ 2048];  // another lane's words
+#pragma unroll
+            for (int u = 0; u < 4; u++) d[e + u * 1024] = v[u];
+        }
+        __syncthreads();
+    }
+}
+
 int main(int argc, char** argv) {
     const int logN = 16, N = 1 << logN, L = 30, K = 8;
     const int limbs = argc > 1 ? atoi(argv[1]) : 468;  // 12 x 39
@@ -538,6 +568,21 @@ int main(int argc, char** argv) {
     timeit("copy (r+w = 16 B/coef)", [&] { hipLaunchKernelGGL(k_copy, dim3((long)limbs * N / 256), dim3(256), 0, 0, src, d2, (long)limbs * N); });
     timeit("copy 16 B / lane", [&] { hipLaunchKernelGGL(k_copy16, dim3((long)limbs * N / 512), dim3(256), 0, 0, (const ulonglong2*)src, (ulonglong2*)d2, (long)limbs * N / 2); });
     timeit("copy 16 B x4 / lane", [&] { hipLaunchKernelGGL(k_copy16x4, dim3((long)limbs * N / 2048), dim3(256), 0, 0, (const ulonglong2*)src, (ulonglong2*)d2, (long)limbs * N / 2); });
+    {
+        ulonglong2* mid;
+        CK(hipMalloc(&mid, bytes));
+        const int half = N / 2;
+        for (int g : {256, 512}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "copy via WG slot, grid %d", g);
+            timeit(nm, [&] { hipLaunchKernelGGL(k_copy_mid<0>, dim3(g), dim3(1024), 0, 0, (const ulonglong2*)src, mid, (ulonglong2*)d2, limbs, half); });
+            snprintf(nm, sizeof nm, "copy via per-limb mid, grid %d", g);
+            timeit(nm, [&] { hipLaunchKernelGGL(k_copy_mid<1>, dim3(g), dim3(1024), 0, 0, (const ulonglong2*)src, mid, (ulonglong2*)d2, limbs, half); });
+            snprintf(nm, sizeof nm, "copy via dst in place, grid %d", g);
+            timeit(nm, [&] { hipLaunchKernelGGL(k_copy_mid<2>, dim3(g), dim3(1024), 0, 0, (const ulonglong2*)src, mid, (ulonglong2*)d2, limbs, half); });
+        }
+        CK(hipFree(mid));
+    }
     timeit("two-pass forward (cols + rows)", two_pass);
     timeit("one-pass forward (k_nttf_fwd_q2)", one_pass);
     timeit("one-pass v1 (k_nttf_fwd_q)", one_pass_v1);
