@@ -1633,6 +1633,16 @@ extern "C" int aesfhe_dot_pt(aesfhe_engine* e, const aesfhe_ct* const* cts, cons
 // |eps| <= 1/2 per coefficient instead of the fast conversion's 0..K overflow.  r >= 1: combined ModDown + rescale -- P * addend joins the
 // accumulators in the inner product and one base conversion from E = {q_{l-r+1}..q_l, P} divides
 // by D = P q_l ... q_{l-r+1} (oracle/ckks_oracle.c moddown_r states the same procedure).
+// template launchers (a template argument list inside hipLaunchKernelGGL would split its macro args)
+template <int A, typename... Args>
+static void launch_modup(dim3 g, hipStream_t s, Args... args) {
+    hipLaunchKernelGGL(k_modup<A>, g, dim3(256), 0, s, args...);
+}
+template <int NE, typename... Args>
+static void launch_moddown(dim3 g, hipStream_t s, Args... args) {
+    hipLaunchKernelGGL(k_moddown<NE>, g, dim3(256), 0, s, args...);
+}
+
 static int ks_beta(const aesfhe_engine* e, int l) {
     const int beta = (l + 1 + e->K - 1) / e->K;
     if (beta > 12) throw_err(AESFHE_EUNSUPPORTED, "more than 12 key-switch digits");
@@ -1663,9 +1673,10 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         // 2. ModUp base conversion of digit j to every other limb, then NTT those limbs
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
-            hipLaunchKernelGGL(k_modup, dim3(N / 256, g_bconv_groups, B), dim3(256), 0, e->stream, (const u64*)dc.p, lN, exj, neN, lo, alpha, l, ne,
-                               (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
-                               e->np, e->q, e->qinv, e->Lp1, e->logN);
+            if (alpha < 1 || alpha > 16) throw_err(AESFHE_EUNSUPPORTED, "ModUp digit width outside 1..16");
+            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 512, g_bconv_groups, B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
+                              (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
+                              e->np, e->q, e->qinv, e->Lp1, e->logN);
         }
         HIPC(hipGetLastError());
         if (two) {
@@ -1740,7 +1751,8 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
     Tmp conv(e, (size_t)B * 2 * kN);
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1));
-        hipLaunchKernelGGL(k_moddown, dim3(N / 256, g_bconv_groups, B * 2), dim3(256), 0, e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN, K,
+        if (K + r < 1 || K + r > 16) throw_err(AESFHE_EUNSUPPORTED, "ModDown source width outside 1..16");
+        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, g_bconv_groups, B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN,
                            invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv,
                            r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN);
     }

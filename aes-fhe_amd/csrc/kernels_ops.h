@@ -269,39 +269,49 @@ __global__ void k_rescale_finish_g(const u64* __restrict__ c, long cps, const u6
 //   conversion adds is the oracle's), ext[t] = sum_i y_i * (qhat_i mod p_t) mod p_t.
 // Constants: hatinv as w/q (w = rint(wq * q) is exact), hat as {w, w/q}.  grid (N/256,
 // ceil(ne/16), B): each thread converts one coefficient into up to 16 target limbs.
+// A = alpha (digit width) as a template parameter: the per-target constant loads are then
+// unconditional and the compiler issues all A of them before the first use (with a runtime
+// alpha every term was a branch, and each scalar load was waited for on its own).
+template <int A>
 __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ ext, long exs,
-                        int lo, int alpha, int l, int ne, const double* __restrict__ hatinvf,
+                        int lo, int l, int ne, const double* __restrict__ hatinvf,
                         const TwD* __restrict__ hat, int np, const u64* __restrict__ qall,
                         const double* __restrict__ qinvall, int Lp1, int logN) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    // two coefficients per thread (k, k + 256): every constant fetched serves both
+    const int k = blockIdx.x * 512 + threadIdx.x;
     const int bb = blockIdx.z;
-    double y[16];
+    double y[A], z[A];
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-        y[i] = 0.0;
-        if (i < alpha) {
-            const int pi = lo + i;
-            const double qp = (double)qall[pi];
-            const double f = hatinvf[i];
-            double r = fmul_rem(u2d(dc[(long)bb * dcs + ((long)pi << logN) + k]), tw_w(f, qp), f, qp);
-            y[i] = r < 0.0 ? r + qp : r;
-        }
+    for (int i = 0; i < A; i++) {
+        const int pi = lo + i;
+        const double qp = (double)qall[pi];
+        const double f = hatinvf[i], w = tw_w(f, qp);
+        const u64* src = dc + (long)bb * dcs + ((long)pi << logN) + k;
+        double r = fmul_rem(u2d(src[0]), w, f, qp), r2 = fmul_rem(u2d(src[256]), w, f, qp);
+        y[i] = r < 0.0 ? r + qp : r;
+        z[i] = r2 < 0.0 ? r2 + qp : r2;
     }
     const int tg = (ne + gridDim.y - 1) / gridDim.y, t0 = blockIdx.y * tg;  // targets per thread
     for (int t = t0; t < t0 + tg && t < ne; t++) {
-        if (t >= lo && t < lo + alpha) continue;
+        if (t >= lo && t < lo + A) continue;
         const int pid = t <= l ? t : Lp1 + (t - l - 1);
         const double qt = (double)qall[pid], qti = qinvall[pid];
-        double acc = 0.0;
+        TwD f[A];
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            if (i < alpha) {
-                const TwD f = hat[i * np + pid];
-                acc += fmul_rem_r(y[i], f.w, f.wq, qt);
-                if ((i & 3) == 3) acc = fred(acc, qt, qti);
+        for (int i = 0; i < A; i++) f[i] = hat[i * np + pid];
+        double acc = 0.0, acc2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < A; i++) {
+            acc += fmul_rem_r(y[i], f[i].w, f[i].wq, qt);
+            acc2 += fmul_rem_r(z[i], f[i].w, f[i].wq, qt);
+            if ((i & 3) == 3) {
+                acc = fred(acc, qt, qti);
+                acc2 = fred(acc2, qt, qti);
             }
         }
-        ext[(long)bb * exs + ((long)t << logN) + k] = fcanon(acc, qt, qti);
+        u64* o = ext + (long)bb * exs + ((long)t << logN) + k;
+        o[0] = fcanon(acc, qt, qti);
+        o[256] = fcanon(acc2, qt, qti);
     }
 }
 
@@ -449,52 +459,77 @@ __global__ void k_ks_inner_multi(const u64* __restrict__ d, long dbs, const u64*
 // multiples of D in sum_j y_j (D/e_j), and conv[i] -= v * (D mod q_i), so the division rounds to
 // nearest like a plain rescale (einv[j] = 1/e_j, dmodf[i] = (D mod q_i)/q_i).
 // invf[j]: w/q table, hat[j * Lp1 + i]: {w, w/q}.  grid (N/256, ceil((l-r+1)/16), B*2)
+// NE = K + r (dropped limbs) as a template parameter, for the same reason as k_modup's A.
+template <int NE>
 __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int l, int r,
-                          u64* __restrict__ conv, long cbs, long ccs, int K,
+                          u64* __restrict__ conv, long cbs, long ccs,
                           const double* __restrict__ invf, const TwD* __restrict__ hat,
                           const double* __restrict__ einv, const double* __restrict__ dmodf,
                           int Lp1, const u64* __restrict__ qall, const double* __restrict__ qinvall,
                           int logN) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    // two coefficients per thread (k, k + 256), as k_modup
+    const int k = blockIdx.x * 512 + threadIdx.x;
     const int bb = blockIdx.z >> 1, c = blockIdx.z & 1;
     const u64* src = acc + (long)bb * abs_ + (long)c * acs;
-    const int ne = K + r, t0 = l - r + 1;
-    double y[16];
+    const int t0 = l - r + 1;
+    double y[NE], z[NE];
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
-        y[j] = 0.0;
-        if (j < ne) {
-            const int pid = j < r ? t0 + j : Lp1 + (j - r);
-            const double pp = (double)qall[pid];
-            const double f = invf[j];
-            const double v = fmul_rem(u2d(src[((long)(t0 + j) << logN) + k]), tw_w(f, pp), f, pp);
-            y[j] = v < 0.0 ? v + pp : v;  // canonical: the oracle's conversion
-        }
+    for (int j = 0; j < NE; j++) {
+        const int pid = j < r ? t0 + j : Lp1 + (j - r);
+        const double pp = (double)qall[pid];
+        const double f = invf[j], w = tw_w(f, pp);
+        const u64* sp = src + ((long)(t0 + j) << logN) + k;
+        const double v = fmul_rem(u2d(sp[0]), w, f, pp), v2 = fmul_rem(u2d(sp[256]), w, f, pp);
+        y[j] = v < 0.0 ? v + pp : v;  // canonical: the oracle's conversion
+        z[j] = v2 < 0.0 ? v2 + pp : v2;
     }
-    double v = 0.0;
+    double v = 0.0, v2 = 0.0;
     {  // exact conversion (every r): v multiples of D, round-to-nearest division
-        double u = 0.0;
+        double u = 0.0, u2 = 0.0;
 #pragma unroll
-        for (int j = 0; j < 16; j++)
-            if (j < ne) u = u + y[j] * einv[j];
+        for (int j = 0; j < NE; j++) {
+            u = u + y[j] * einv[j];
+            u2 = u2 + z[j] * einv[j];
+        }
         v = __builtin_rint(u);
+        v2 = __builtin_rint(u2);
     }
     const int ig = (l - r + 1 + gridDim.y - 1) / gridDim.y, i0 = blockIdx.y * ig;  // outputs per thread
     for (int i = i0; i < i0 + ig && i <= l - r; i++) {
         const double q = (double)qall[i], qi = qinvall[i];
-        const double f = dmodf[i];
-        double sum = fmul_rem(-v, tw_w(f, q), f, q);
+        const double fd = dmodf[i], wd = tw_w(fd, q);
+        TwD f[NE];
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            if (j < ne) {
-                const TwD f = hat[j * Lp1 + i];
-                sum += fmul_rem_r(y[j], f.w, f.wq, q);
-                if ((j & 3) == 3) sum = fred(sum, q, qi);
+        for (int j = 0; j < NE; j++) f[j] = hat[j * Lp1 + i];
+        double sum = fmul_rem(-v, wd, fd, q), sum2 = fmul_rem(-v2, wd, fd, q);
+#pragma unroll
+        for (int j = 0; j < NE; j++) {
+            sum += fmul_rem_r(y[j], f[j].w, f[j].wq, q);
+            sum2 += fmul_rem_r(z[j], f[j].w, f[j].wq, q);
+            if ((j & 3) == 3) {
+                sum = fred(sum, q, qi);
+                sum2 = fred(sum2, q, qi);
             }
         }
-        conv[(long)bb * cbs + (long)c * ccs + ((long)i << logN) + k] = fcanon(sum, q, qi);
+        u64* o = conv + (long)bb * cbs + (long)c * ccs + ((long)i << logN) + k;
+        o[0] = fcanon(sum, q, qi);
+        o[256] = fcanon(sum2, q, qi);
     }
 }
+
+// launch helper: F<n> for a runtime n in 1..16
+#define AESFHE_DISPATCH16(n, F, ...)                                                     \
+    switch (n) {                                                                         \
+        case 1: F<1>(__VA_ARGS__); break;   case 2: F<2>(__VA_ARGS__); break;             \
+        case 3: F<3>(__VA_ARGS__); break;   case 4: F<4>(__VA_ARGS__); break;             \
+        case 5: F<5>(__VA_ARGS__); break;   case 6: F<6>(__VA_ARGS__); break;             \
+        case 7: F<7>(__VA_ARGS__); break;   case 8: F<8>(__VA_ARGS__); break;             \
+        case 9: F<9>(__VA_ARGS__); break;   case 10: F<10>(__VA_ARGS__); break;           \
+        case 11: F<11>(__VA_ARGS__); break; case 12: F<12>(__VA_ARGS__); break;           \
+        case 13: F<13>(__VA_ARGS__); break; case 14: F<14>(__VA_ARGS__); break;           \
+        case 15: F<15>(__VA_ARGS__); break; case 16: F<16>(__VA_ARGS__); break;           \
+        default: break;                                                                  \
+    }
 
 // out[b][c][i] = addend_c + (acc[b][c][i] - conv[b][c][i]) * D^{-1}  (addend absent: r >= 1) ; grid (N/256, l+1, B*2)
 __global__ void k_moddown_finish(const u64* __restrict__ acc, long abs_, long acs,
