@@ -2670,7 +2670,9 @@ extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, in
                     const bool big = e->chain.q[la] >= (1ULL << 42);
                     int lb = la + 1;
                     while (lb < nl && (e->chain.q[lb] >= (1ULL << 42)) == big) lb++;
-                    hipLaunchKernelGGL(big ? k_poly2_int<true> : k_poly2_int<false>, dim3(N / 256, lb - la, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny,
+                    auto kern = big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max> : k_poly2_int<true, 0>)
+                                    : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max> : k_poly2_int<false, 0>);
+                    hipLaunchKernelGGL(kern, dim3(N / 256, lb - la, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny,
                                        (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, ml, t0, std::min(kPoly2Out, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN);
                     la = lb;
                 }

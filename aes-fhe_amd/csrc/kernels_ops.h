@@ -777,7 +777,9 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
 // remainder products and fold.  Wt: [mtot][nx][ny] doubles (scalar loads), Rt: [nl][cxn][cyn]
 // {w, w/q}, C0: [nl][cxn] = H(c, 0) as doubles, xstart[c]..xstart[c+1]: the i of class c.  BIG: the q >= 2^42 path; the host launches
 // each run of limbs of one size class (limbs l0 .. l0 + gridDim.y - 1 of nl).  grid (N/256, run, B)
-template <bool BIG>
+// NY > 0: ny fixed at compile time (the weight loads are then unconditional and issued together;
+// with a runtime ny each scalar load sat behind its own branch and was waited for alone).
+template <bool BIG, int NY>
 __global__ void __launch_bounds__(256) k_poly2_int(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
                         const long* __restrict__ xps, int nx, const u64* const* __restrict__ yp,
                         const long* __restrict__ ybs, const long* __restrict__ yps, int ny,
@@ -791,6 +793,7 @@ __global__ void __launch_bounds__(256) k_poly2_int(const u64* const* __restrict_
     const double q = (double)qs[l];
     const double qi = qinv[l];
     constexpr bool big = BIG;
+    const int nyv = NY > 0 ? NY : ny;
     const long off = ((long)l << logN) + k;
     double d0[kPoly2Out], d1[kPoly2Out], d2[kPoly2Out];
 #pragma unroll
@@ -803,7 +806,7 @@ __global__ void __launch_bounds__(256) k_poly2_int(const u64* const* __restrict_
 #pragma unroll
         for (int j = 0; j < kPoly2Max - 1; j++) {
             y0[j] = y1[j] = 0.0;
-            if (j < ny - 1) {
+            if (j < nyv - 1) {
                 const u64* p = yp[j] + (long)bb * ybs[j] + off;
                 const TwD r = Rc[ycls[j + 1]];
                 y0[j] = fred(fmul_rem_r(u2d(p[0]), r.w, r.wq, q), q, qi);
@@ -829,7 +832,7 @@ __global__ void __launch_bounds__(256) k_poly2_int(const u64* const* __restrict_
                     a1 = 0.0;
 #pragma unroll
                     for (int j = 1; j < kPoly2Max; j++) {
-                        if (j < ny) {
+                        if (j < nyv) {
                             a0 = __builtin_fma(w[j], y0[j - 1], a0);
                             a1 = __builtin_fma(w[j], y1[j - 1], a1);
                         }
@@ -840,7 +843,7 @@ __global__ void __launch_bounds__(256) k_poly2_int(const u64* const* __restrict_
                     a1 = 0.0;
 #pragma unroll
                     for (int j = 1; j < kPoly2Max; j++) {
-                        if (j < ny) {
+                        if (j < nyv) {
                             const double wj = w[j], wjq = wj * qi;
                             a0 = fred(a0 + fmul_rem(y0[j - 1], wj, wjq, q), q, qi);
                             a1 = fred(a1 + fmul_rem(y1[j - 1], wj, wjq, q), q, qi);
