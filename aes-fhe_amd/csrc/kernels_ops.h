@@ -149,11 +149,22 @@ __global__ void k_lincomb(const u64* const* __restrict__ ptrs, const long* __res
     const int h = k >> (logN - 1);
     const long off = ((long)l << logN) + k;
     u64 acc = 0;
-    for (int i = 0; i < n; i++) {
-        if (p >= npi[i]) continue;
-        const u64 v = ptrs[i][(long)bb * bstr[i] + (long)p * pss[i] + off];
-        const int fi = (i * nl + l) * 2 + h;
-        acc += mulw(v, f[fi], ff[fi], q);
+    // chunks of 8 inputs: the 8 loads are issued before the first product consumes one
+    for (int i0 = 0; i0 < n; i0 += 8) {
+        u64 v[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            const int i = i0 + c;
+            v[c] = (i < n && p < npi[i]) ? ptrs[i][(long)bb * bstr[i] + (long)p * pss[i] + off] : 0;
+        }
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            const int i = i0 + c;
+            if (i < n) {
+                const int fi = (i * nl + l) * 2 + h;
+                acc += mulw(v[c], f[fi], ff[fi], q);
+            }
+        }
     }
     o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)l << logN) + k] = red_m(acc, q, qinv[l]);
 }
@@ -994,14 +1005,20 @@ __global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64*
         double e[BCT];
 #pragma unroll
         for (int u = 0; u < BCT; u++) e[u] = u2d(ep[i][base[u] + src]);
+        // every giant's plaintext word is requested before the first product (a load behind
+        // each pointer test serialised the GM loads)
+        const u64* pj[GM];
+        double wv[GM];
+#pragma unroll
+        for (int j = 0; j < GM; j++) pj[j] = j < ng ? pt[j * nb + i] : nullptr;
+#pragma unroll
+        for (int j = 0; j < GM; j++) wv[j] = pj[j] ? u2d(pj[j][po]) : 0.0;
 #pragma unroll
         for (int j = 0; j < GM; j++) {
-            if (j >= ng) break;
-            const u64* p = pt[j * nb + i];
-            if (p) {
-                const double wv = u2d(p[po]), wq = wv * qi;
+            if (pj[j]) {
+                const double wq = wv[j] * qi;
 #pragma unroll
-                for (int u = 0; u < BCT; u++) acc[u][j] += fmul_rem(e[u], wv, wq, q);
+                for (int u = 0; u < BCT; u++) acc[u][j] += fmul_rem(e[u], wv[j], wq, q);
             }
         }
         if ((i & 3) == 3) {
