@@ -791,7 +791,7 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
 // NY > 0: ny fixed at compile time (the weight loads are then unconditional and issued together;
 // with a runtime ny each scalar load sat behind its own branch and was waited for alone).
 template <bool BIG, int NY>
-__global__ void __launch_bounds__(256) k_poly2_int(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
+__global__ void __launch_bounds__(256, 3) k_poly2_int(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
                         const long* __restrict__ xps, int nx, const u64* const* __restrict__ yp,
                         const long* __restrict__ ybs, const long* __restrict__ yps, int ny,
                         const int* __restrict__ xstart, const int* __restrict__ ycls, int cxn,
