@@ -25,11 +25,13 @@ namespace aesfhe {
 //   B: e = 32 (L >> 2) + (L & 3) + 4 r   ml = 8, 16, 32   (16, 8, 4)
 //   C: e = 8 L + r           ml = 64, 128     (2, 1)
 // then back to A for the coalesced inner product.  Twiddle of stage ml, element e:
-// psi^{brv(ml (256 + row) + (e >> (8 - log2 ml)))}.  LDS per row: e -> e + (e >> 3) (288 words),
+// psi^{brv(ml rt + (e >> (8 - log2 ml)))}.  LDS per row: e -> e + (e >> 3) (288 words),
 // conflict-free for the A / B / C patterns.
 __device__ __forceinline__ int r8p(int e) { return e + (e >> 3); }
 
-__device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, double* sr, int L, int row,
+// rt: 256 + row when W is the limb's global psi table, 1 when W is the row's own LDS copy
+// (entry ml + j = the table's ml rt + j, stages ml = 1 .. 128).
+__device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, double* sr, int L, int rt,
                                              const double* W, double q, double qi, bool big) {
 #pragma unroll
     for (int r = 0; r < 8; r++) x[r] = ld_d(&rp[L + 32 * r]);
@@ -41,7 +43,7 @@ __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, doub
 #pragma unroll
             for (int r = 0; r < 8; r++) x[r] = fred(x[r], q, qi);
         }
-        const int base = ml * (256 + row);
+        const int base = ml * rt;
 #pragma unroll
         for (int j = 0; j < ml; j++) {
             const double wq = W[base + j];
@@ -63,7 +65,7 @@ __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, doub
 #pragma unroll
             for (int r = 0; r < 8; r++) x[r] = fred(x[r], q, qi);
         }
-        const int base = ml * (256 + row) + (L >> 2) * nj;
+        const int base = ml * rt + (L >> 2) * nj;
 #pragma unroll
         for (int j = 0; j < nj; j++) {
             const double wq = W[base + j];
@@ -83,7 +85,7 @@ __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, doub
         for (int r = 0; r < 8; r++) x[r] = fred(x[r], q, qi);
     }
     {
-        const int base = 64 * (256 + row) + 2 * L;
+        const int base = 64 * rt + 2 * L;
         const double w0 = W[base], w1 = W[base + 1];
         ct_f(x[0], x[2], w0, q);
         ct_f(x[1], x[3], w0, q);
@@ -91,7 +93,7 @@ __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, doub
         ct_f(x[5], x[7], w1, q);
     }
     {
-        const int base = 128 * (256 + row) + 4 * L;
+        const int base = 128 * rt + 4 * L;
 #pragma unroll
         for (int j = 0; j < 4; j++) ct_f(x[2 * j], x[2 * j + 1], W[base + j], q);
     }
@@ -107,13 +109,14 @@ __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, doub
 // grid: 8 * B * (ne * 32 / 8) blocks of 256 (8 rows x 32 lanes); block id -> (xcd group
 // x = id & 7, b, pair), pair = (t, 8-row block): all B batch elements of one (t, row block) are
 // dealt to one XCD (blocks x, x + 8, ...) so the key rows they share are L2 hits.
-__global__ __launch_bounds__(256) void k_nttf_rows_ks(const u64* __restrict__ d, long dbs,
+__global__ __launch_bounds__(256, 4) void k_nttf_rows_ks(const u64* __restrict__ d, long dbs,
                                                       const u64* __restrict__ ext, long exs, long exj,
                                                       const u64* __restrict__ key, long kdig, long kcomp,
                                                       u64* __restrict__ acc, long abs_, long acs, int B,
                                                       int beta, int K, int l, int ne, Tabs T, Opnd addend,
                                                       const double* __restrict__ pmodf, int accum) {
-    __shared__ double s[8 * 288];
+    // one LDS array (row transposes, then the 8 rows' twiddles -- see row_ntt8_fwd's rt)
+    __shared__ double s[8 * 288 + 8 * 256];
     const int id = blockIdx.x, x8 = id & 7, rest = id >> 3;
     const int bb = rest % B, pair = (rest / B) * 8 + x8;
     const int t = pair >> 5, rb = pair & 31;
@@ -126,6 +129,17 @@ __global__ __launch_bounds__(256) void k_nttf_rows_ks(const u64* __restrict__ d,
     const bool big = q >= kBigPrime;
     const double* W = T.psif + ((long)pid << 16);
     double* sr = s + rl * 288;
+    // the row's 255 twiddles are the same for every digit: staged in LDS once per workgroup
+    double* tw = s + 8 * 288 + rl * 256;
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+        const int e = L + 32 * m;
+        if (e > 0) {
+            const int ml = 1 << (31 - __clz(e));
+            tw[e] = W[(long)ml * (256 + row) + (e - ml)];
+        }
+    }
+    __syncthreads();
     const long roff = ((long)t << 16) + (long)row * 256 + L;  // element (row, L + 32 r) at roff + 32 r
     double a0[8], a1[8];
 #pragma unroll
@@ -146,8 +160,8 @@ __global__ __launch_bounds__(256) void k_nttf_rows_ks(const u64* __restrict__ d,
 #pragma unroll
             for (int r = 0; r < 8; r++) v[r] = u2d(dp[32 * r]);
         } else {
-            row_ntt8_fwd(v, ext + (long)j * exj + (long)bb * exs + ((long)t << 16) + (long)row * 256, sr, L, row,
-                         W, q, qi, big);
+            row_ntt8_fwd(v, ext + (long)j * exj + (long)bb * exs + ((long)t << 16) + (long)row * 256, sr, L, 1,
+                         tw, q, qi, big);
         }
 #pragma unroll
         for (int r = 0; r < 8; r++) {
