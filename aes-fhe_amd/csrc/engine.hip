@@ -1634,9 +1634,16 @@ extern "C" int aesfhe_dot_pt(aesfhe_engine* e, const aesfhe_ct* const* cts, cons
 // accumulators in the inner product and one base conversion from E = {q_{l-r+1}..q_l, P} divides
 // by D = P q_l ... q_{l-r+1} (oracle/ckks_oracle.c moddown_r states the same procedure).
 // template launchers (a template argument list inside hipLaunchKernelGGL would split its macro args)
+static int g_modup_c = getenv("AESFHE_MODUP_C") ? atoi(getenv("AESFHE_MODUP_C")) : 2;  // A/B knob
 template <int A, typename... Args>
 static void launch_modup(dim3 g, hipStream_t s, Args... args) {
-    hipLaunchKernelGGL(k_modup<A>, g, dim3(256), 0, s, args...);
+    if (g_modup_c == 4 && g.x % 4 == 0) {
+        g.x /= 4;
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_modup<A, 4>), g, dim3(256), 0, s, args...);
+    } else {
+        g.x /= 2;
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_modup<A, 2>), g, dim3(256), 0, s, args...);
+    }
 }
 template <int NE, typename... Args>
 static void launch_moddown(dim3 g, hipStream_t s, Args... args) {
@@ -1674,7 +1681,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
             if (alpha < 1 || alpha > 16) throw_err(AESFHE_EUNSUPPORTED, "ModUp digit width outside 1..16");
-            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 512, g_bconv_groups, B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
+            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, g_bconv_groups, B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
                               (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
                               e->np, e->q, e->qinv, e->Lp1, e->logN);
         }

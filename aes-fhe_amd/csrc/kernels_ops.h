@@ -283,24 +283,25 @@ __global__ void k_rescale_finish_g(const u64* __restrict__ c, long cps, const u6
 // A = alpha (digit width) as a template parameter: the per-target constant loads are then
 // unconditional and the compiler issues all A of them before the first use (with a runtime
 // alpha every term was a branch, and each scalar load was waited for on its own).
-template <int A>
+template <int A, int C>  // C coefficients per thread (k + 256 c): every constant fetched serves C
 __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ ext, long exs,
                         int lo, int l, int ne, const double* __restrict__ hatinvf,
                         const TwD* __restrict__ hat, int np, const u64* __restrict__ qall,
                         const double* __restrict__ qinvall, int Lp1, int logN) {
-    // two coefficients per thread (k, k + 256): every constant fetched serves both
-    const int k = blockIdx.x * 512 + threadIdx.x;
+    const int k = blockIdx.x * (256 * C) + threadIdx.x;
     const int bb = blockIdx.z;
-    double y[A], z[A];
+    double y[C][A];
 #pragma unroll
     for (int i = 0; i < A; i++) {
         const int pi = lo + i;
         const double qp = (double)qall[pi];
         const double f = hatinvf[i], w = tw_w(f, qp);
         const u64* src = dc + (long)bb * dcs + ((long)pi << logN) + k;
-        double r = fmul_rem(u2d(src[0]), w, f, qp), r2 = fmul_rem(u2d(src[256]), w, f, qp);
-        y[i] = r < 0.0 ? r + qp : r;
-        z[i] = r2 < 0.0 ? r2 + qp : r2;
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+            const double r = fmul_rem(u2d(src[256 * c]), w, f, qp);
+            y[c][i] = r < 0.0 ? r + qp : r;
+        }
     }
     const int tg = (ne + gridDim.y - 1) / gridDim.y, t0 = blockIdx.y * tg;  // targets per thread
     for (int t = t0; t < t0 + tg && t < ne; t++) {
@@ -310,19 +311,21 @@ __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ 
         TwD f[A];
 #pragma unroll
         for (int i = 0; i < A; i++) f[i] = hat[i * np + pid];
-        double acc = 0.0, acc2 = 0.0;
+        double acc[C];
+#pragma unroll
+        for (int c = 0; c < C; c++) acc[c] = 0.0;
 #pragma unroll
         for (int i = 0; i < A; i++) {
-            acc += fmul_rem_r(y[i], f[i].w, f[i].wq, qt);
-            acc2 += fmul_rem_r(z[i], f[i].w, f[i].wq, qt);
+#pragma unroll
+            for (int c = 0; c < C; c++) acc[c] += fmul_rem_r(y[c][i], f[i].w, f[i].wq, qt);
             if ((i & 3) == 3) {
-                acc = fred(acc, qt, qti);
-                acc2 = fred(acc2, qt, qti);
+#pragma unroll
+                for (int c = 0; c < C; c++) acc[c] = fred(acc[c], qt, qti);
             }
         }
         u64* o = ext + (long)bb * exs + ((long)t << logN) + k;
-        o[0] = fcanon(acc, qt, qti);
-        o[256] = fcanon(acc2, qt, qti);
+#pragma unroll
+        for (int c = 0; c < C; c++) o[256 * c] = fcanon(acc[c], qt, qti);
     }
 }
 
