@@ -2672,15 +2672,18 @@ extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, in
         aesfhe_ct* d3 = ct_new(e, ml * B, 3, l);
         {
             ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml));
-            for (int t0 = 0; t0 < ml; t0 += kPoly2Out)
+            static const int mo = getenv("AESFHE_POLY2_OUT") && atoi(getenv("AESFHE_POLY2_OUT")) == 8 ? 8 : 4;  // A/B knob
+            for (int t0 = 0; t0 < ml; t0 += mo)
                 for (int la = 0; la < nl;) {  // runs of limbs of one prime-size class
                     const bool big = e->chain.q[la] >= (1ULL << 42);
                     int lb = la + 1;
                     while (lb < nl && (e->chain.q[lb] >= (1ULL << 42)) == big) lb++;
-                    auto kern = big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max> : k_poly2_int<true, 0>)
-                                    : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max> : k_poly2_int<false, 0>);
+                    auto kern = mo == 8 ? (big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max, 8> : k_poly2_int<true, 0, 8>)
+                                               : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max, 8> : k_poly2_int<false, 0, 8>))
+                                        : (big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max, 4> : k_poly2_int<true, 0, 4>)
+                                               : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max, 4> : k_poly2_int<false, 0, 4>));
                     hipLaunchKernelGGL(kern, dim3(N / 256, lb - la, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny,
-                                       (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, ml, t0, std::min(kPoly2Out, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN);
+                                       (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, ml, t0, std::min(mo, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN);
                     la = lb;
                 }
         }

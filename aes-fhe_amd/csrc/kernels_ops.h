@@ -699,7 +699,7 @@ __global__ void k_square(const u64* __restrict__ s, u64* __restrict__ o,
 // registers.  x/y: pointer, batch-stride and poly-stride arrays of 2-poly ciphertexts at level
 // >= nl-1 (only limbs 0..nl-1 are read: truncation).  out: [mtot][B][3][nl][N] (output t at
 // out + t*oos).  grid (N/256, nl, B)
-constexpr int kPoly2Max = 16, kPoly2Out = 4;
+constexpr int kPoly2Max = 16, kPoly2Out = 4, kPoly2OutMax = 8;
 __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
                         const long* __restrict__ xps, int nx, const u64* const* __restrict__ yp,
                         const long* __restrict__ ybs, const long* __restrict__ yps, int ny,
@@ -793,8 +793,8 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
 // each run of limbs of one size class (limbs l0 .. l0 + gridDim.y - 1 of nl).  grid (N/256, run, B)
 // NY > 0: ny fixed at compile time (the weight loads are then unconditional and issued together;
 // with a runtime ny each scalar load sat behind its own branch and was waited for alone).
-template <bool BIG, int NY>
-__global__ void __launch_bounds__(256, 3) k_poly2_int(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
+template <bool BIG, int NY, int MO>  // MO: outputs per launch (<= MOMax)
+__global__ void __launch_bounds__(256, MO > 4 ? 2 : 3) k_poly2_int(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
                         const long* __restrict__ xps, int nx, const u64* const* __restrict__ yp,
                         const long* __restrict__ ybs, const long* __restrict__ yps, int ny,
                         const int* __restrict__ xstart, const int* __restrict__ ycls, int cxn,
@@ -809,9 +809,9 @@ __global__ void __launch_bounds__(256, 3) k_poly2_int(const u64* const* __restri
     constexpr bool big = BIG;
     const int nyv = NY > 0 ? NY : ny;
     const long off = ((long)l << logN) + k;
-    double d0[kPoly2Out], d1[kPoly2Out], d2[kPoly2Out];
+    double d0[MO], d1[MO], d2[MO];
 #pragma unroll
-    for (int t = 0; t < kPoly2Out; t++) d0[t] = d1[t] = d2[t] = 0.0;
+    for (int t = 0; t < MO; t++) d0[t] = d1[t] = d2[t] = 0.0;
     const TwD* Rl = Rt + (size_t)l * cxn * cyn;
 #pragma unroll 1
     for (int c = 0; c < cxn; c++) {  // x classes in order: y' = H(c, cy(j)) * y_j, reloaded
@@ -837,7 +837,7 @@ __global__ void __launch_bounds__(256, 3) k_poly2_int(const u64* const* __restri
             xb = u2d(p[xps[i - 1]]);
         }
 #pragma unroll
-        for (int t = 0; t < kPoly2Out; t++) {
+        for (int t = 0; t < MO; t++) {
             if (t < mc) {
                 const double* w = Wt + ((size_t)(t0 + t) * nx + i) * ny;
                 double a0, a1;
@@ -885,7 +885,7 @@ __global__ void __launch_bounds__(256, 3) k_poly2_int(const u64* const* __restri
     u64* o = out + (long)bb * obs + off;
     const long pstr = (long)nl << logN;
 #pragma unroll
-    for (int t = 0; t < kPoly2Out; t++) {
+    for (int t = 0; t < MO; t++) {
         if (t < mc) {
             u64* ot = o + (long)(t0 + t) * oos;
             ot[0] = fcanon(d0[t], q, qi);
