@@ -504,6 +504,15 @@ static bool g_ntt_generic = getenv("AESFHE_NTT_GENERIC") != nullptr;
 static bool g_no_fuse = getenv("AESFHE_NO_FUSE") != nullptr;  // unfused key-switch epilogues (A/B)
 // base conversions: output-limb groups per coefficient (inputs are re-read once per group)
 static int g_bconv_groups = getenv("AESFHE_BCONV_GROUPS") ? atoi(getenv("AESFHE_BCONV_GROUPS")) : 1;
+// target-limb groups of a base-conversion launch (grid y).  AESFHE_BCONV_GROUPS=0 selects an
+// automatic count for small batches (groups added until ~4096 workgroups are in flight, each
+// re-converting the source limbs): measured neutral on both workloads, so the default is 1.
+static int bconv_groups(long xz_blocks, int targets) {
+    if (g_bconv_groups > 0) return g_bconv_groups;
+    int g = 1;
+    while (g < 8 && xz_blocks * g < 4096 && targets / (2 * g) >= 4) g *= 2;
+    return g;
+}
 // the N = 2^16 fp64 passes with fused epilogues are available
 static bool fused_ntt(const aesfhe_engine* e) { return e->logN == 16 && !g_ntt_generic && !g_ntt_int && !g_no_fuse; }
 
@@ -1681,7 +1690,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
             if (alpha < 1 || alpha > 16) throw_err(AESFHE_EUNSUPPORTED, "ModUp digit width outside 1..16");
-            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, g_bconv_groups, B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
+            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, bconv_groups((long)N / 512 * B, ne - alpha), B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
                               (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
                               e->np, e->q, e->qinv, e->Lp1, e->logN);
         }
@@ -1759,7 +1768,7 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1));
         if (K + r < 1 || K + r > 16) throw_err(AESFHE_EUNSUPPORTED, "ModDown source width outside 1..16");
-        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, g_bconv_groups, B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN,
+        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, bconv_groups((long)N / 512 * B * 2, lk + 1), B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN,
                            invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv,
                            r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN);
     }

@@ -16,6 +16,7 @@
 namespace aesfhe {
 
 constexpr int kMaxPrimes = 96;
+constexpr double kBigPrime = 4398046511104.0;  // 2^42: primes at or above it fold lazily more often
 
 __device__ __forceinline__ u64 add_m(u64 a, u64 b, u64 q) {
     u64 s = a + b;

@@ -314,11 +314,14 @@ __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ 
         double acc[C];
 #pragma unroll
         for (int c = 0; c < C; c++) acc[c] = 0.0;
+        // terms lie in (-1.5 qt, 1.5 qt): below 2^42 the A <= 16 of them sum exactly without
+        // folding; 50-bit targets fold every 4 (uniform branch)
+        const bool fold = qt >= kBigPrime;
 #pragma unroll
         for (int i = 0; i < A; i++) {
 #pragma unroll
             for (int c = 0; c < C; c++) acc[c] += fmul_rem_r(y[c][i], f[i].w, f[i].wq, qt);
-            if ((i & 3) == 3) {
+            if (fold && (i & 3) == 3) {
 #pragma unroll
                 for (int c = 0; c < C; c++) acc[c] = fred(acc[c], qt, qti);
             }
@@ -516,11 +519,12 @@ __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int 
 #pragma unroll
         for (int j = 0; j < NE; j++) f[j] = hat[j * Lp1 + i];
         double sum = fmul_rem(-v, wd, fd, q), sum2 = fmul_rem(-v2, wd, fd, q);
+        const bool fold = q >= kBigPrime;  // as k_modup: small targets sum NE + 1 terms unfolded
 #pragma unroll
         for (int j = 0; j < NE; j++) {
             sum += fmul_rem_r(y[j], f[j].w, f[j].wq, q);
             sum2 += fmul_rem_r(z[j], f[j].w, f[j].wq, q);
-            if ((j & 3) == 3) {
+            if (fold && (j & 3) == 3) {
                 sum = fred(sum, q, qi);
                 sum2 = fred(sum2, q, qi);
             }

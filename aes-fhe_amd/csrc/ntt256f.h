@@ -25,7 +25,7 @@
 
 namespace aesfhe {
 
-constexpr double kBigPrime = 4398046511104.0;  // 2^42
+// kBigPrime (2^42): defined in kernels.h
 
 __device__ __forceinline__ void ct_f(double& x, double& y, double wq, double q) {
     const double v = fmul_rem(y, tw_w(wq, q), wq, q);
