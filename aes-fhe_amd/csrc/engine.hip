@@ -1735,8 +1735,10 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
         // (key read once per call, accumulators written; ext never leaves the chip)
         const int nown = std::min(l + 1, beta * K);
         ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))));
-        const int blocks = 8 * B * (ne * 32 / 8);
-        hipLaunchKernelGGL(k_nttf_rows_ks, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum);
+        static const int G = getenv("AESFHE_KS_G") && atoi(getenv("AESFHE_KS_G")) == 2 ? 2 : 1;  // A/B knob
+        const int blocks = 8 * ((B + G - 1) / G) * (ne * 32 / 8);
+        auto kern = G == 2 ? k_nttf_rows_ks<2> : k_nttf_rows_ks<1>;
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum);
     } else {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B * (accum ? 2 : 1)));
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;

@@ -106,10 +106,13 @@ __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, doub
     __syncthreads();  // the next digit rewrites sr
 }
 
-// grid: 8 * B * (ne * 32 / 8) blocks of 256 (8 rows x 32 lanes); block id -> (xcd group
-// x = id & 7, b, pair), pair = (t, 8-row block): all B batch elements of one (t, row block) are
-// dealt to one XCD (blocks x, x + 8, ...) so the key rows they share are L2 hits.
-__global__ __launch_bounds__(256, 4) void k_nttf_rows_ks(const u64* __restrict__ d, long dbs,
+// grid: 8 * ceil(B / G) * (ne * 32 / 8) blocks of 256 (8 rows x 32 lanes); block id -> (xcd group
+// x = id & 7, batch group, pair), pair = (t, 8-row block): all batch groups of one (t, row block)
+// are dealt to one XCD (blocks x, x + 8, ...) so the key rows they share are L2 hits.  G batch
+// elements per workgroup share each key word loaded (G = 2 halves the key reads, the largest
+// load stream of the kernel, at the price of a second pair of accumulators).
+template <int G>
+__global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64* __restrict__ d, long dbs,
                                                       const u64* __restrict__ ext, long exs, long exj,
                                                       const u64* __restrict__ key, long kdig, long kcomp,
                                                       u64* __restrict__ acc, long abs_, long acs, int B,
@@ -117,8 +120,9 @@ __global__ __launch_bounds__(256, 4) void k_nttf_rows_ks(const u64* __restrict__
                                                       const double* __restrict__ pmodf, int accum) {
     // one LDS array (row transposes, then the 8 rows' twiddles -- see row_ntt8_fwd's rt)
     __shared__ double s[8 * 288 + 8 * 256];
+    const int nbg = (B + G - 1) / G;
     const int id = blockIdx.x, x8 = id & 7, rest = id >> 3;
-    const int bb = rest % B, pair = (rest / B) * 8 + x8;
+    const int b0 = (rest % nbg) * G, pair = (rest / nbg) * 8 + x8;
     const int t = pair >> 5, rb = pair & 31;
     if (t >= ne) return;
     const int pid = t <= l ? t : T.Lp1 + (t - l - 1);
@@ -141,9 +145,11 @@ __global__ __launch_bounds__(256, 4) void k_nttf_rows_ks(const u64* __restrict__
     }
     __syncthreads();
     const long roff = ((long)t << 16) + (long)row * 256 + L;  // element (row, L + 32 r) at roff + 32 r
-    double a0[8], a1[8];
+    double a0[G][8], a1[G][8];
 #pragma unroll
-    for (int r = 0; r < 8; r++) a0[r] = a1[r] = 0.0;
+    for (int g = 0; g < G; g++)
+#pragma unroll
+        for (int r = 0; r < 8; r++) a0[g][r] = a1[g][r] = 0.0;
 #pragma unroll 1
     for (int j = 0; j < beta; j++) {
         // the key digit's words are loaded first: they arrive while the row NTT computes
@@ -154,44 +160,56 @@ __global__ __launch_bounds__(256, 4) void k_nttf_rows_ks(const u64* __restrict__
             kbw[r] = kp[32 * r];
             kaw[r] = kp[32 * r + kcomp];
         }
-        double v[8];
-        if (j == own) {  // the digit's own limbs: d itself, already in NTT form
-            const u64* dp = d + (long)bb * dbs + roff;
 #pragma unroll
-            for (int r = 0; r < 8; r++) v[r] = u2d(dp[32 * r]);
-        } else {
-            row_ntt8_fwd(v, ext + (long)j * exj + (long)bb * exs + ((long)t << 16) + (long)row * 256, sr, L, 1,
-                         tw, q, qi, big);
-        }
+        for (int g = 0; g < G; g++) {
+            const int bb = b0 + g;
+            if (bb >= B) break;  // block-uniform
+            double v[8];
+            if (j == own) {  // the digit's own limbs: d itself, already in NTT form
+                const u64* dp = d + (long)bb * dbs + roff;
 #pragma unroll
-        for (int r = 0; r < 8; r++) {
-            const double kb = u2d(kbw[r]), ka = u2d(kaw[r]);
-            a0[r] += fmul_rem(v[r], kb, kb * qi, q);
-            a1[r] += fmul_rem(v[r], ka, ka * qi, q);
+                for (int r = 0; r < 8; r++) v[r] = u2d(dp[32 * r]);
+            } else {
+                row_ntt8_fwd(v, ext + (long)j * exj + (long)bb * exs + ((long)t << 16) + (long)row * 256, sr, L, 1,
+                             tw, q, qi, big);
+            }
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const double kb = u2d(kbw[r]), ka = u2d(kaw[r]);
+                a0[g][r] += fmul_rem(v[r], kb, kb * qi, q);
+                a1[g][r] += fmul_rem(v[r], ka, ka * qi, q);
+            }
         }
         if (big && (j & 3) == 3) {
 #pragma unroll
+            for (int g = 0; g < G; g++)
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    a0[g][r] = fred(a0[g][r], q, qi);
+                    a1[g][r] = fred(a1[g][r], q, qi);
+                }
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        const int bb = b0 + g;
+        if (bb >= B) break;
+        u64* o0 = acc + (long)bb * abs_ + roff;
+        if (pmodf && t <= l) {
+            const double f = pmodf[t], w = tw_w(f, q);
+#pragma unroll
             for (int r = 0; r < 8; r++) {
-                a0[r] = fred(a0[r], q, qi);
-                a1[r] = fred(a1[r], q, qi);
+                const int kk = row * 256 + L + 32 * r;
+                a0[g][r] = fred(a0[g][r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 0, t, kk, 16)), w, f, q);
+                a1[g][r] = fred(a1[g][r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, kk, 16)), w, f, q);
             }
         }
-    }
-    u64* o0 = acc + (long)bb * abs_ + roff;
-    if (pmodf && t <= l) {
-        const double f = pmodf[t], w = tw_w(f, q);
 #pragma unroll
         for (int r = 0; r < 8; r++) {
-            const int kk = row * 256 + L + 32 * r;
-            a0[r] = fred(a0[r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 0, t, kk, 16)), w, f, q);
-            a1[r] = fred(a1[r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, kk, 16)), w, f, q);
+            const double p0 = accum ? u2d(o0[32 * r]) : 0.0, p1 = accum ? u2d(o0[acs + 32 * r]) : 0.0;
+            o0[32 * r] = fcanon(a0[g][r] + p0, q, qi);
+            o0[acs + 32 * r] = fcanon(a1[g][r] + p1, q, qi);
         }
-    }
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-        const double p0 = accum ? u2d(o0[32 * r]) : 0.0, p1 = accum ? u2d(o0[acs + 32 * r]) : 0.0;
-        o0[32 * r] = fcanon(a0[r] + p0, q, qi);
-        o0[acs + 32 * r] = fcanon(a1[r] + p1, q, qi);
     }
 }
 
