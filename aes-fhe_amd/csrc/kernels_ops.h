@@ -327,8 +327,9 @@ __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ 
             }
         }
         u64* o = ext + (long)bb * exs + ((long)t << logN) + k;
+        // streaming stores: ext of one digit (B ne limbs) is far larger than the caches
 #pragma unroll
-        for (int c = 0; c < C; c++) o[256 * c] = fcanon(acc[c], qt, qti);
+        for (int c = 0; c < C; c++) __builtin_nontemporal_store(fcanon(acc[c], qt, qti), &o[256 * c]);
     }
 }
 
