@@ -531,8 +531,8 @@ __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int 
             }
         }
         u64* o = conv + (long)bb * cbs + (long)c * ccs + ((long)i << logN) + k;
-        o[0] = fcanon(sum, q, qi);
-        o[256] = fcanon(sum2, q, qi);
+        __builtin_nontemporal_store(fcanon(sum, q, qi), &o[0]);  // streaming, as k_modup
+        __builtin_nontemporal_store(fcanon(sum2, q, qi), &o[256]);
     }
 }
 
