@@ -104,10 +104,10 @@ __global__ void k_tensor(Opnd a, Opnd b, Out o, const u64* __restrict__ qs,
         base[0] = add_m(base[0], d0, q);
         base[o.ps] = add_m(base[o.ps], d1, q);
         base[2 * o.ps] = add_m(base[2 * o.ps], d2, q);
-    } else {
-        base[0] = d0;
-        base[o.ps] = d1;
-        base[2 * o.ps] = d2;
+    } else {  // streaming stores: the 3-component product is read back only by the key switch
+        __builtin_nontemporal_store(d0, &base[0]);
+        __builtin_nontemporal_store(d1, &base[o.ps]);
+        __builtin_nontemporal_store(d2, &base[2 * o.ps]);
     }
 }
 
