@@ -68,7 +68,9 @@ __device__ __forceinline__ void tw_row(const double* W, int idx, double rq, doub
     wq = w * qi;
 }
 __device__ __forceinline__ double ld_d(const u64* p) { return __longlong_as_double((long long)*p); }
-__device__ __forceinline__ void st_d(u64* p, double v) { *p = (u64)__double_as_longlong(v); }
+// raw-double intermediates between NTT passes are streamed (nontemporal): one pass writes far more
+// than the caches hold before the next pass reads it back
+__device__ __forceinline__ void st_d(u64* p, double v) { __builtin_nontemporal_store((u64)__double_as_longlong(v), p); }
 
 constexpr int kPadF = 17;  // LDS row stride (8 B words) of the 16 x 16 transpose tiles
 
