@@ -207,8 +207,8 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             const double p0 = accum ? u2d(o0[32 * r]) : 0.0, p1 = accum ? u2d(o0[acs + 32 * r]) : 0.0;
-            o0[32 * r] = fcanon(a0[g][r] + p0, q, qi);
-            o0[acs + 32 * r] = fcanon(a1[g][r] + p1, q, qi);
+            __builtin_nontemporal_store(fcanon(a0[g][r] + p0, q, qi), &o0[32 * r]);  // streaming
+            __builtin_nontemporal_store(fcanon(a1[g][r] + p1, q, qi), &o0[acs + 32 * r]);
         }
     }
 }

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
             const double conv = u2d((u64)__double_as_longlong(s[r * 16 * kPadF + (cc >> 4) * kPadF + (cc & 15)]));
             double v = fmul_rem(u2d(ap[e]) - conv, w, f, q);
             if (dp) v += u2d(dp[e]);
-            op[e] = fcanon(v, q, qi);
+            __builtin_nontemporal_store(fcanon(v, q, qi), &op[e]);  // streaming
         }
     }
 }
