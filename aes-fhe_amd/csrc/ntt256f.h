@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
-            base[e] = (u64)__double_as_longlong(s[row_tile_idx(e)]);
+            __builtin_nontemporal_store((u64)__double_as_longlong(s[row_tile_idx(e)]), &base[e]);
         }
     } else {
         const int y = blockIdx.y, p = y / fin.nl, i = y - p * fin.nl, bb = p >> 1, c = p & 1;
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T) {
 #pragma unroll
     for (int a = 0; a < 16; a++) {
         const double r = fred(x[a], q, qi);
-        io[(a * 16 + b) * 256 + c] = fcanon(fmul_rem(r, ni, nif, q), q, qi);
+        __builtin_nontemporal_store(fcanon(fmul_rem(r, ni, nif, q), q, qi), &io[(a * 16 + b) * 256 + c]);
     }
 }
 
