@@ -69,6 +69,10 @@ SIGNATURES = [
     ("aesfhe_galois_elt", C.c_uint64, [C.c_int32, C.c_int64, C.c_int32]),
     ("aesfhe_key_info", C.c_int, [c_key_p, _P(C.c_int32), _P(C.c_uint64)]),
     ("aesfhe_key_free", None, [c_key_p]),
+    ("aesfhe_key_export", C.c_int,
+     [c_eng_p, c_key_p, _P(C.c_int32), _P(C.c_uint64), _P(C.c_uint64), _P(C.c_int64), _P(C.c_uint64)]),
+    ("aesfhe_key_import", C.c_int,
+     [c_eng_p, C.c_int32, C.c_uint64, C.c_uint64, _P(C.c_uint64), C.c_int64, _P(c_key_p)]),
     ("aesfhe_encrypt", C.c_int,
      [c_eng_p, c_key_p, _P(C.c_int64), C.c_int32, C.c_int32, C.c_uint64, _P(c_ct_p)]),
     ("aesfhe_decrypt", C.c_int, [c_eng_p, c_key_p, c_ct_p, _P(C.c_int64)]),
@@ -76,6 +80,9 @@ SIGNATURES = [
     ("aesfhe_ct_export", C.c_int, [c_eng_p, c_ct_p, _P(C.c_uint64)]),
     ("aesfhe_ct_import", C.c_int,
      [c_eng_p, _P(C.c_uint64), C.c_int32, C.c_int32, C.c_int32, _P(c_ct_p)]),
+    ("aesfhe_ct_export_device", C.c_int, [c_eng_p, c_ct_p, C.c_int32, C.c_int32, C.c_void_p]),
+    ("aesfhe_ct_import_device", C.c_int,
+     [c_eng_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, _P(c_ct_p)]),
     ("aesfhe_ct_copy", C.c_int, [c_eng_p, c_ct_p, _P(c_ct_p)]),
     ("aesfhe_ct_slice", C.c_int, [c_eng_p, c_ct_p, C.c_int32, C.c_int32, _P(c_ct_p)]),
     ("aesfhe_ct_concat", C.c_int, [c_eng_p, _P(c_ct_p), C.c_int32, _P(c_ct_p)]),

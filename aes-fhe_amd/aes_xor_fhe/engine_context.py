@@ -41,8 +41,9 @@ class EngineContext:
         self.bootstrap_key = eng.create_bootstrap_key(self.secret_key)
 
     def __repr__(self) -> str:  # pragma: no cover
-        return (f"FHEContext(engine=Engine(slot_count={self.engine.slot_count}), "
-                f"keys=[sk, pk, rlk, cjk, rot])")
+        e = self.engine
+        return (f"<EngineContext N=2^{e.log_coeff_count} L={e.max_level} "
+                f"slots={e.slot_count} backend={e._lib.backend}>")
 
     def encrypt(self, data):
         return self.engine.encrypt(data, self.public_key)

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from typing import Sequence
 
 import numpy as np
@@ -27,8 +28,18 @@ from ._abi import Lib, Params, c_ct_p, c_key_p, c_pt_p, load_product
 # HomomorphicEncryption.org 128-bit bound on log2(QP) for ternary secrets
 SECURITY_BUDGET = {11: 54, 12: 109, 13: 218, 14: 438, 15: 881, 16: 1772, 17: 3544}
 
+# seed None: a fresh 64-bit engine seed from the OS entropy pool (os.urandom) per engine, so
+# that no two default engines derive the same keys; an explicit seed reproduces every key and
+# encryption (tests, and multi-rank key sharing -- see `nonce_start`).
 DEFAULT_PARAMS = dict(log_n=16, max_level=30, special_primes=8, scale_bits=40, base_bits=50,
-                      special_bits=50, seed=0x5EED5EED)
+                      special_bits=50, seed=None)
+
+
+_MAGIC = b"AESFHE\x01\x00"
+
+
+def _urandom64() -> int:
+    return int.from_bytes(os.urandom(8), "little")
 
 
 def _params_for(log_n=None, max_level=None, special_primes=None, scale_bits=None,
@@ -41,6 +52,8 @@ def _params_for(log_n=None, max_level=None, special_primes=None, scale_bits=None
             p[k] = v
     p["threads"] = threads
     p["device"] = device
+    if p["seed"] is None:
+        p["seed"] = _urandom64()
     return p
 
 
@@ -194,6 +207,12 @@ class Engine:
     ``device_id`` (the product has no CPU path).  Extra keyword overrides (``log_n``,
     ``special_primes``, ``scale_bits``, ``base_bits``, ``special_bits``, ``seed``) select explicit parameters; ``_lib`` injects
     another implementation of the ABI (tests use it for the CPU oracle).
+
+    Randomness: without ``seed`` the engine seed, every secret key created without a seed and
+    the first encryption nonce are drawn from os.urandom.  With an explicit ``seed`` everything
+    is reproducible and nonces count from ``nonce_start`` (default 0); engines that share a seed
+    to share keys (one per rank) must use disjoint nonce ranges (parallel.rank_nonce_start),
+    otherwise two encryptions would reuse the same (a, e) randomness.
     """
 
     def __init__(self, *args, mode: str = "cpu", use_bootstrap: bool = False,
@@ -202,7 +221,8 @@ class Engine:
                  special_prime_count: int | None = None, log_n: int | None = None,
                  special_primes: int | None = None, scale_bits: int | None = None,
                  base_bits: int | None = None, special_bits: int | None = None,
-                 seed: int | None = None, _lib: Lib | None = None):
+                 seed: int | None = None, nonce_start: int | None = None,
+                 _lib: Lib | None = None):
         ints = [a for a in args if isinstance(a, (int, np.integer)) and not isinstance(a, bool)]
         strs = [a for a in args if isinstance(a, str)]
         if strs:
@@ -248,7 +268,10 @@ class Engine:
         scales = (C.c_double * (self.max_level + 1))()
         self._lib.engine_scales(self._h, scales)
         self.scales = [float(x) for x in scales]
-        self._nonce = 0
+        self._random_keys = seed is None
+        if nonce_start is None:
+            nonce_start = _urandom64() >> 1 if seed is None else 0
+        self._nonce = int(nonce_start)
 
     # -- plumbing ---------------------------------------------------------------------------
     def _check(self, rc):
@@ -303,7 +326,11 @@ class Engine:
         k.engine = self
         return k
 
-    def create_secret_key(self, seed: int = 0) -> SecretKey:
+    def create_secret_key(self, seed: int | None = None) -> SecretKey:
+        """Ternary secret key.  seed None: 0 for a seeded engine (reproducible), else a fresh
+        os.urandom value -- engine_context.py:62 calls this without arguments."""
+        if seed is None:
+            seed = _urandom64() if self._random_keys else 0
         out = C.c_void_p()
         self._check(self._lib.key_secret(self._h, seed, C.byref(out)))
         return self._key(SecretKey, out.value)
@@ -351,8 +378,10 @@ class Engine:
         self._check(self._lib.rotate_hoisted(self._h, ct._h, arr, n, outs))
         return [self._ct(h) for h in outs]
 
-    def create_sparse_secret_key(self, hw: int, seed: int = 0) -> SecretKey:
+    def create_sparse_secret_key(self, hw: int, seed: int | None = None) -> SecretKey:
         """Ternary secret with exactly hw nonzeros (aesfhe_key_secret_sparse)."""
+        if seed is None:
+            seed = _urandom64() if self._random_keys else 0
         out = C.c_void_p()
         self._check(self._lib.key_secret_sparse(self._h, seed, int(hw), C.byref(out)))
         return self._key(SecretKey, out.value)
@@ -642,6 +671,81 @@ class Engine:
         a = np.ascontiguousarray(arr, dtype=np.uint64)
         b, p, l1, _ = a.shape
         return self._call_ct(self._lib.ct_import, _as_ptr(a, C.c_uint64), b, p, l1 - 1)
+
+    # -- device-resident transfer (parallel.py: RCCL scatter / gather) ------------------------
+    @property
+    def on_device(self) -> bool:
+        """True for the HIP engine (buffers handed to export_into / import_from live in device
+        memory); False for the CPU oracle (host memory)."""
+        return self._lib.backend.startswith("hip")
+
+    def export_into(self, ct: Ciphertext, ptr: int, start: int = 0, count: int | None = None):
+        """Residues of batch elements [start, start + count) into the buffer at address `ptr`
+        (device memory of this engine's GPU; aesfhe_ct_export_device)."""
+        count = ct.batch - start if count is None else count
+        self._check(self._lib.ct_export_device(self._h, ct._h, int(start), int(count), C.c_void_p(ptr)))
+
+    def import_from(self, ptr: int, batch: int, npoly: int, level: int) -> Ciphertext:
+        """A ciphertext copied from residues at address `ptr` (aesfhe_ct_import_device)."""
+        return self._call_ct(self._lib.ct_import_device, C.c_void_p(ptr), int(batch), int(npoly), int(level))
+
+    # -- serialisation (SURVEY.md 8f item 4) --------------------------------------------------
+    def _fingerprint(self) -> dict:
+        return {"log_n": self.log_coeff_count, "max_level": self.max_level,
+                "special_primes": self.special_prime_count, "primes": self.primes}
+
+    def save(self, obj, path) -> None:
+        """Write a Ciphertext or key (SecretKey, PublicKey, RelinearizationKey, GaloisKey and
+        subclasses) to `path`: magic, a JSON header (kind, shape, the engine's prime chain) and
+        the NTT-domain residues as little-endian u64.  A RotationKey is not saved: it is derived
+        on use from its secret key."""
+        import json
+        hdr = {"fp": self._fingerprint()}
+        if isinstance(obj, Ciphertext):
+            data = self.export_residues(obj)
+            hdr.update(type="ciphertext", batch=obj.batch, npoly=obj.npoly, level=obj.level)
+        elif isinstance(obj, _Key):
+            kind, g, seed, words = C.c_int32(), C.c_uint64(), C.c_uint64(), C.c_int64()
+            self._check(self._lib.key_export(self._h, obj._h, C.byref(kind), C.byref(g), C.byref(seed),
+                                             C.byref(words), None))
+            data = np.empty(words.value, dtype=np.uint64)
+            self._check(self._lib.key_export(self._h, obj._h, C.byref(kind), C.byref(g), C.byref(seed),
+                                             C.byref(words), _as_ptr(data, C.c_uint64)))
+            hdr.update(type="key", cls=type(obj).__name__, kind=kind.value, galois=g.value,
+                       keyseed=seed.value, delta=getattr(obj, "delta", None))
+        else:
+            raise TypeError(f"cannot save {type(obj).__name__}")
+        head = json.dumps(hdr).encode()
+        with open(path, "wb") as f:
+            f.write(_MAGIC + len(head).to_bytes(8, "little") + head)
+            f.write(np.ascontiguousarray(data).astype("<u8", copy=False).tobytes())
+
+    def load(self, path):
+        """Read an object written by save(); raises RuntimeError if it was made by an engine with
+        other parameters (prime chain)."""
+        import json
+        with open(path, "rb") as f:
+            if f.read(len(_MAGIC)) != _MAGIC:
+                raise RuntimeError(f"{path}: not an aes-fhe object file")
+            hdr = json.loads(f.read(int.from_bytes(f.read(8), "little")))
+            data = np.frombuffer(f.read(), dtype="<u8")
+        if hdr["fp"] != self._fingerprint():
+            raise RuntimeError(f"{path}: written by an engine with different parameters")
+        if hdr["type"] == "ciphertext":
+            n = 1 << self.log_coeff_count
+            return self.import_residues(data.reshape(hdr["batch"], hdr["npoly"], hdr["level"] + 1, n))
+        cls = {c.__name__: c for c in (SecretKey, PublicKey, RelinearizationKey, GaloisKey,
+                                       ConjugationKey, FixedRotationKey)}[hdr["cls"]]
+        arr = np.ascontiguousarray(data, dtype=np.uint64)
+        out = C.c_void_p()
+        self._check(self._lib.key_import(self._h, hdr["kind"], hdr["galois"], hdr["keyseed"],
+                                         _as_ptr(arr, C.c_uint64), arr.size, C.byref(out)))
+        k = self._key(cls, out.value)
+        if isinstance(k, GaloisKey):
+            k.galois_elt = hdr["galois"]
+        if isinstance(k, FixedRotationKey):
+            k.delta = hdr["delta"]
+        return k
 
     def pool_stats(self) -> dict:
         """Device pool counters (aesfhe_engine_pool_stats): bytes held / live, hipMalloc calls,

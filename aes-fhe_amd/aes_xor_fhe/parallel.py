@@ -1,67 +1,116 @@
 """Ciphertext-batch sharding across GPUs of one node.
 
 The homomorphic AES path partitions perfectly: ciphertexts (each carrying n_blk AES blocks)
-are independent, so a batch of B ciphertext pairs is split contiguously over the ranks and
-every rank runs whole rounds locally -- no per-round collective.  The only data movement is
-the scatter of input ciphertexts from the client rank and the gather of the results, done
-with torch.distributed (RCCL over xGMI on GPUs, gloo on CPU) on the NTT-domain residues.
-Keys are never moved: every rank derives the same keys from the shared engine seed.
+are independent, so a batch is split contiguously over the ranks (`shard_range`) and every
+rank runs whole rounds locally -- no per-round collective.  The only data movement is the
+scatter of input ciphertexts from the client rank and the gather of the results.
+
+Transfers are device-resident: residues go from the engine's device buffers into torch tensors
+on the same GPU (aesfhe_ct_export_device, a device-to-device copy) and torch.distributed moves
+those tensors -- with the "nccl" backend that is RCCL over xGMI, GPU to GPU, never through host
+memory.  With the CPU oracle engine (tests, "gloo") the same code runs on host tensors.
+
+Keys are never moved: every rank derives the same keys from the shared engine seed; each rank
+encrypts with its own nonce range (`rank_nonce_start`) so no two ranks reuse randomness.
 """
 from __future__ import annotations
-
-from typing import Optional
 
 import numpy as np
 
 
 def shard_range(total: int, world: int, rank: int):
-    """Contiguous [start, stop) share of `total` items for `rank` (first ranks take +1)."""
+    """Contiguous [start, stop) share of `total` items for `rank` (the first total % world ranks
+    take one more)."""
     base, extra = divmod(total, world)
     start = rank * base + min(rank, extra)
     return start, start + base + (1 if rank < extra else 0)
 
 
-def _meta(ct, world):
-    return np.array([ct.batch, ct.npoly, ct.level], dtype=np.int64)
+def rank_nonce_start(rank: int) -> int:
+    """First encryption nonce of `rank` for engines sharing one seed: disjoint 2^48 ranges."""
+    return (int(rank) + 1) << 48
 
 
-def scatter_ciphertext(engine, ct, src: int = 0, group=None, device=None):
-    """Split a batched ciphertext held by rank `src` across all ranks (batch dimension).
-    Non-source ranks pass ct=None.  Returns this rank's share as a Ciphertext."""
+def _torch_device(engine):
+    import torch
+    if engine.on_device:
+        return torch.device("cuda", engine.device_id)
+    return torch.device("cpu")
+
+
+def _sync(dev):
+    """Finish torch's pending work on `dev` before the engine's own stream touches (or after RCCL
+    has written) a torch-allocated buffer: the two are different HIP streams."""
+    if dev.type == "cuda":
+        import torch
+        torch.cuda.current_stream(dev).synchronize()
+
+
+def _words(engine, npoly, level):
+    return npoly * (level + 1) * (1 << engine.log_coeff_count)
+
+
+def scatter_ciphertext(engine, ct, src: int = 0, group=None):
+    """Split a batched ciphertext held by rank `src` across all ranks along the batch dimension
+    (shard_range: uneven batches allowed).  Non-source ranks pass ct=None.  Returns this rank's
+    share (None for a rank whose share is empty)."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    meta = torch.zeros(3, dtype=torch.int64)
+    dev = _torch_device(engine)
+    meta = torch.zeros(3, dtype=torch.int64, device=dev)
     if rank == src:
-        meta = torch.from_numpy(_meta(ct, world))
+        meta = torch.tensor([ct.batch, ct.npoly, ct.level], dtype=torch.int64, device=dev)
     dist.broadcast(meta, src, group=group)
-    batch, npoly, level = (int(x) for x in meta)
-    if batch % world:
-        raise ValueError(f"batch {batch} not divisible by world size {world}")
-    share = batch // world
-    n = 1 << engine.log_coeff_count
-    shape = (share, npoly, level + 1, n)
-    dev = device if device is not None else torch.device("cpu")
-    out = torch.empty(shape, dtype=torch.int64, device=dev)
+    batch, npoly, level = (int(x) for x in meta.cpu())
+    per = _words(engine, npoly, level)
+    smax = -(-batch // world)  # padded share: scatter needs equal sizes
+    out = torch.empty((smax, per), dtype=torch.int64, device=dev)
     parts = None
     if rank == src:
-        res = engine.export_residues(ct).view(np.int64)
-        parts = [torch.from_numpy(np.ascontiguousarray(res[i * share:(i + 1) * share])).to(dev)
-                 for i in range(world)]
+        parts = []
+        for r in range(world):
+            a, b = shard_range(batch, world, r)
+            t = torch.empty((smax, per), dtype=torch.int64, device=dev)
+            _sync(dev)
+            if b > a:
+                engine.export_into(ct, t.data_ptr(), a, b - a)
+            parts.append(t)
     dist.scatter(out, parts, src=src, group=group)
-    return engine.import_residues(out.cpu().numpy().view(np.uint64))
+    a, b = shard_range(batch, world, rank)
+    if b == a:
+        return None
+    _sync(dev)  # RCCL wrote `out` on torch's stream
+    return engine.import_from(out.data_ptr(), b - a, npoly, level)
 
 
-def gather_ciphertext(engine, ct, dst: int = 0, group=None, device=None):
-    """Concatenate every rank's batched ciphertext (same shape on all ranks) on rank `dst`."""
+def gather_ciphertext(engine, ct, dst: int = 0, group=None):
+    """Concatenate every rank's batched ciphertext (same npoly / level on all ranks, batch may
+    differ; a rank may pass None for an empty share) on rank `dst`, in rank order."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    dev = device if device is not None else torch.device("cpu")
-    res = torch.from_numpy(engine.export_residues(ct).view(np.int64)).to(dev)
-    bufs = [torch.empty_like(res) for _ in range(world)] if rank == dst else None
-    dist.gather(res, bufs, dst=dst, group=group)
+    dev = _torch_device(engine)
+    mine = torch.tensor([ct.batch if ct is not None else 0,
+                         ct.npoly if ct is not None else -1,
+                         ct.level if ct is not None else -1], dtype=torch.int64, device=dev)
+    metas = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(metas, mine, group=group)
+    metas = [m.cpu().tolist() for m in metas]
+    shapes = {(p, l) for b, p, l in metas if b > 0}
+    if len(shapes) != 1:
+        raise ValueError(f"gather_ciphertext: ranks disagree on (npoly, level): {sorted(shapes)}")
+    npoly, level = shapes.pop()
+    per = _words(engine, npoly, level)
+    smax = max(b for b, _, _ in metas)
+    buf = torch.zeros((smax, per), dtype=torch.int64, device=dev)
+    _sync(dev)
+    if ct is not None:
+        engine.export_into(ct, buf.data_ptr())
+    bufs = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+    dist.gather(buf, bufs, dst=dst, group=group)
     if rank != dst:
         return None
-    full = torch.cat(bufs, 0).cpu().numpy().view(np.uint64)
-    return engine.import_residues(full)
+    full = torch.cat([bufs[r][:metas[r][0]] for r in range(world)], 0).contiguous()
+    _sync(dev)
+    return engine.import_from(full.data_ptr(), full.shape[0], npoly, level)

@@ -22,7 +22,6 @@
 
 #include "../../include/aesfhe.h"
 #include "kernels_ops.h"
-#include "ntt256.h"
 #include "ntt256f.h"
 #include "ks_fused.h"
 
@@ -201,10 +200,6 @@ struct aesfhe_engine {
     u64 seed;
     Chain chain;
     hipStream_t stream;
-    // key-switch ModUp pipelining (AESFHE_KS_STREAMS): the ext column passes run on stream2 while
-    // the next digit's base conversion runs on stream (kKsEv fork / join events, no timing)
-    hipStream_t stream2 = nullptr;
-    hipEvent_t kev[16] = {};
     Pool pool;
     // device tables
     u64 *q, *psi, *ipsi, *ninv;
@@ -285,14 +280,6 @@ struct aesfhe_pt {
 static const int FAM_NTT = 0, FAM_KS = 1, FAM_EW = 2;
 static const int kMdrMaxR = 2, kMdrMaxE = 16;  // combined ModDown + rescale: r <= 2, K + r <= 16
 
-static bool ks_streams_on() {
-    static const bool on = [] {
-        const char* s = getenv("AESFHE_KS_STREAMS");
-        return s && atoi(s) > 0;
-    }();
-    return on;
-}
-
 struct ProfScope {
     aesfhe_engine* e;
     int fam;
@@ -327,11 +314,6 @@ struct ProfScope {
 static void prof_flush(aesfhe_engine* e) {
     if (e->recs.empty()) return;
     hipStreamSynchronize(e->stream);
-    if (e->stream2) {
-        hipStreamSynchronize(e->stream2);
-        for (auto ev : e->kev) hipEventDestroy(ev);
-        hipStreamDestroy(e->stream2);
-    }
     for (auto& r : e->recs) {
         float ms = 0;
         hipEventElapsedTime(&ms, r.a, r.b);
@@ -464,61 +446,28 @@ static void ntt_inv_t(aesfhe_engine* e, Span src, Span dst, int total) {
     }
 }
 
-// N = 2^16: register-resident radix-16x16 passes (ntt256.h)
-static bool g_ntt_int = getenv("AESFHE_NTT_INT") != nullptr;  // integer-arithmetic passes (A/B)
-
+// N = 2^16: register-resident radix-16x16 fp64-arithmetic passes (ntt256f.h)
 static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
     Tabs T = e->tabs();
     // algorithmic bytes per pass: 8 B * N * limbs = half of the transform's read-once +
     // write-once 16 B per coefficient (the two-pass split itself is charged as overhead)
     const double by = 8.0 * e->N * (double)total;
-    if (!g_ntt_int) {  // fp64-arithmetic passes (ntt256f.h)
-        {
-            ProfScope ps(e, FAM_NTT, by);
-            if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
-            else hipLaunchKernelGGL(k_nttf_inv_rows, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
-        }
+    {
         ProfScope ps(e, FAM_NTT, by);
-        if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_rows_t<false>, dim3(16, total), dim3(256), 0, e->stream, dst, T, RowFin{});
-        else hipLaunchKernelGGL(k_nttf_inv_cols, dim3(16, total), dim3(256), 0, e->stream, dst, T);
-        return;
+        if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
+        else hipLaunchKernelGGL(k_nttf_inv_rows, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
     }
-    if (!inverse) {
-        {
-            ProfScope ps(e, FAM_NTT, by);
-            hipLaunchKernelGGL(k_ntt256_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
-        }
-        ProfScope ps(e, FAM_NTT, by);
-        hipLaunchKernelGGL(k_ntt256_fwd_rows, dim3(16, total), dim3(256), 0, e->stream, dst, T);
-    } else {
-        {
-            ProfScope ps(e, FAM_NTT, by);
-            hipLaunchKernelGGL(k_ntt256_inv_rows, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
-        }
-        ProfScope ps(e, FAM_NTT, by);
-        hipLaunchKernelGGL(k_ntt256_inv_cols, dim3(16, total), dim3(256), 0, e->stream, dst, T);
-    }
+    ProfScope ps(e, FAM_NTT, by);
+    if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_rows_t<false>, dim3(16, total), dim3(256), 0, e->stream, dst, T, RowFin{});
+    else hipLaunchKernelGGL(k_nttf_inv_cols, dim3(16, total), dim3(256), 0, e->stream, dst, T);
 }
 
-static bool g_ntt_generic = getenv("AESFHE_NTT_GENERIC") != nullptr;
-static bool g_no_fuse = getenv("AESFHE_NO_FUSE") != nullptr;  // unfused key-switch epilogues (A/B)
-// base conversions: output-limb groups per coefficient (inputs are re-read once per group)
-static int g_bconv_groups = getenv("AESFHE_BCONV_GROUPS") ? atoi(getenv("AESFHE_BCONV_GROUPS")) : 1;
-// target-limb groups of a base-conversion launch (grid y).  AESFHE_BCONV_GROUPS=0 selects an
-// automatic count for small batches (groups added until ~4096 workgroups are in flight, each
-// re-converting the source limbs): measured neutral on both workloads, so the default is 1.
-static int bconv_groups(long xz_blocks, int targets) {
-    if (g_bconv_groups > 0) return g_bconv_groups;
-    int g = 1;
-    while (g < 8 && xz_blocks * g < 4096 && targets / (2 * g) >= 4) g *= 2;
-    return g;
-}
-// the N = 2^16 fp64 passes with fused epilogues are available
-static bool fused_ntt(const aesfhe_engine* e) { return e->logN == 16 && !g_ntt_generic && !g_ntt_int && !g_no_fuse; }
+// the N = 2^16 fp64 passes with fused epilogues (ModDown finish, key-switch inner product)
+static bool fused_ntt(const aesfhe_engine* e) { return e->logN == 16; }
 
 static void ntt(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
     if (total <= 0) return;
-    if (e->logN == 16 && !g_ntt_generic) {
+    if (e->logN == 16) {
         ntt256(e, src, dst, total, inverse);
         HIPC(hipGetLastError());
         return;
@@ -783,10 +732,6 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
         if (x >> 50) throw_err(AESFHE_EARG, "prime %llu exceeds 2^50", (unsigned long long)x);
     HIPC(hipSetDevice(e->device));
     HIPC(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-    if (ks_streams_on()) {
-        HIPC(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
-        for (auto& ev : e->kev) HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    }
     build_tables(e.get());
     {
         size_t fr = 0, tot = 0;
@@ -818,11 +763,6 @@ extern "C" void aesfhe_engine_destroy(aesfhe_engine* e) {
 static void engine_teardown(aesfhe_engine* e) {
     hipSetDevice(e->device);
     hipStreamSynchronize(e->stream);
-    if (e->stream2) {
-        hipStreamSynchronize(e->stream2);
-        for (auto ev : e->kev) hipEventDestroy(ev);
-        hipStreamDestroy(e->stream2);
-    }
     for (auto& r : e->recs) {
         hipEventDestroy(r.a);
         hipEventDestroy(r.b);
@@ -1155,6 +1095,67 @@ extern "C" int aesfhe_ct_import(aesfhe_engine* e, const uint64_t* in, int32_t B,
     HIPC(hipMemcpyAsync(c->d, in, c->bytes, hipMemcpyHostToDevice, e->stream));
     HIPC(hipStreamSynchronize(e->stream));
     *out = c;
+    API_END
+}
+// Device-resident transfer (the multi-GPU scatter/gather, parallel.py): residues of batch
+// elements [start, start + count) to / from a caller-owned device buffer of this engine's device
+// (a torch tensor that torch.distributed hands to RCCL), no host staging.  Both synchronise the
+// engine stream, so the buffer is complete (export) / reusable (import) on return.
+extern "C" int aesfhe_ct_export_device(aesfhe_engine* e, const aesfhe_ct* c, int32_t start, int32_t count, void* dst) {
+    API_BEGIN
+    if (!c || !dst || start < 0 || count < 1 || start + count > c->B) throw_err(AESFHE_EARG, "bad export range");
+    const size_t per = c->bytes / c->B;
+    HIPC(hipMemcpyAsync(dst, (const char*)c->d + per * start, per * count, hipMemcpyDeviceToDevice, e->stream));
+    HIPC(hipStreamSynchronize(e->stream));
+    API_END
+}
+extern "C" int aesfhe_ct_import_device(aesfhe_engine* e, const void* src, int32_t B, int32_t np, int32_t level,
+                                       aesfhe_ct** out) {
+    API_BEGIN
+    if (!src || B < 1 || np < 1 || np > 3 || level < 0 || level > e->L) throw_err(AESFHE_EARG, "bad shape");
+    aesfhe_ct* c = ct_new(e, B, np, level);
+    HIPC(hipMemcpyAsync(c->d, src, c->bytes, hipMemcpyDeviceToDevice, e->stream));
+    HIPC(hipStreamSynchronize(e->stream));
+    *out = c;
+    API_END
+}
+
+// Key serialisation (keyio.py): words of each kind -- 0 secret np*N, 1 public 2(L+1)N,
+// 2/3/5 switching keys dnum*2*np*N.
+static size_t key_words(const aesfhe_engine* e, int kind) {
+    switch (kind) {
+        case 0: return (size_t)e->np * e->N;
+        case 1: return (size_t)2 * e->Lp1 * e->N;
+        case 2: case 3: case 5: return (size_t)e->dnum * 2 * e->np * e->N;
+        default: return 0;
+    }
+}
+extern "C" int aesfhe_key_export(aesfhe_engine* e, const aesfhe_key* k, int32_t* kind, uint64_t* galois,
+                                 uint64_t* keyseed, int64_t* words, uint64_t* out) {
+    API_BEGIN
+    if (!k) throw_err(AESFHE_EARG, "null key");
+    *kind = k->kind;
+    *galois = k->galois;
+    *keyseed = k->keyseed;
+    *words = (int64_t)(k->bytes / 8);
+    if (out) {
+        HIPC(hipMemcpyAsync(out, k->d, k->bytes, hipMemcpyDeviceToHost, e->stream));
+        HIPC(hipStreamSynchronize(e->stream));
+    }
+    API_END
+}
+extern "C" int aesfhe_key_import(aesfhe_engine* e, int32_t kind, uint64_t galois, uint64_t keyseed,
+                                 const uint64_t* in, int64_t words, aesfhe_key** out) {
+    API_BEGIN
+    const size_t want = key_words(e, kind);
+    if (!in || !want) throw_err(AESFHE_EARG, "unknown key kind %d", kind);
+    if ((size_t)words != want) throw_err(AESFHE_EARG, "key of kind %d needs %zu words, got %lld", kind, want, (long long)words);
+    aesfhe_key* k = key_new(e, kind, want);
+    k->galois = galois;
+    k->keyseed = keyseed;
+    HIPC(hipMemcpyAsync(k->d, in, want * 8, hipMemcpyHostToDevice, e->stream));
+    HIPC(hipStreamSynchronize(e->stream));
+    *out = k;
     API_END
 }
 extern "C" int aesfhe_ct_copy(aesfhe_engine* e, const aesfhe_ct* c, aesfhe_ct** out) {
@@ -1643,16 +1644,10 @@ extern "C" int aesfhe_dot_pt(aesfhe_engine* e, const aesfhe_ct* const* cts, cons
 // accumulators in the inner product and one base conversion from E = {q_{l-r+1}..q_l, P} divides
 // by D = P q_l ... q_{l-r+1} (oracle/ckks_oracle.c moddown_r states the same procedure).
 // template launchers (a template argument list inside hipLaunchKernelGGL would split its macro args)
-static int g_modup_c = getenv("AESFHE_MODUP_C") ? atoi(getenv("AESFHE_MODUP_C")) : 2;  // A/B knob
 template <int A, typename... Args>
-static void launch_modup(dim3 g, hipStream_t s, Args... args) {
-    if (g_modup_c == 4 && g.x % 4 == 0) {
-        g.x /= 4;
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_modup<A, 4>), g, dim3(256), 0, s, args...);
-    } else {
-        g.x /= 2;
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_modup<A, 2>), g, dim3(256), 0, s, args...);
-    }
+static void launch_modup(dim3 g, hipStream_t s, Args... args) {  // two coefficients per thread
+    g.x /= 2;
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_modup<A, 2>), g, dim3(256), 0, s, args...);
 }
 template <int NE, typename... Args>
 static void launch_moddown(dim3 g, hipStream_t s, Args... args) {
@@ -1678,10 +1673,6 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
     // 1. INTT copy of the input
     Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1), sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
     ntt(e, sd, sdc, B * (l + 1), true);
-    // pipelined (stream2): the column passes of digit j overlap digit j + 1's base conversion
-    // (HBM-bound next to VALU-bound); joined back into e->stream before dc is released
-    const bool two = cols_only && e->stream2 && beta + 1 <= (int)(sizeof(e->kev) / sizeof(e->kev[0]));
-    hipStream_t cs = two ? e->stream2 : e->stream;
     for (int j = 0; j < beta; j++) {
         const int lo = j * K, hi = std::min(lo + K, l + 1), alpha = hi - lo;
         const size_t set = (size_t)j * K + (alpha - 1);
@@ -1690,29 +1681,21 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
             if (alpha < 1 || alpha > 16) throw_err(AESFHE_EUNSUPPORTED, "ModUp digit width outside 1..16");
-            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, bconv_groups((long)N / 512 * B, ne - alpha), B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
+            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, 1, B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
                               (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
                               e->np, e->q, e->qinv, e->Lp1, e->logN);
         }
         HIPC(hipGetLastError());
-        if (two) {
-            HIPC(hipEventRecord(e->kev[j], e->stream));
-            HIPC(hipStreamWaitEvent(e->stream2, e->kev[j], 0));
-        }
         auto fwd = [&](Span sp, int total) {
             if (!cols_only) return ntt(e, sp, sp, total, false);
-            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, cs);
-            hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, cs, sp, sp, e->tabs());
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+            hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, sp, sp, e->tabs());
         };
         if (lo > 0) fwd(span_s(exj, neN, lo, lo, 0, e->Lp1), B * lo);
         {
             int nrest = ne - hi, nq_rest = (l + 1) - hi;
             fwd(span_s(exj + (long)hi * N, neN, nrest, nq_rest, hi, e->Lp1), B * nrest);
         }
-    }
-    if (two) {
-        HIPC(hipEventRecord(e->kev[beta], e->stream2));
-        HIPC(hipStreamWaitEvent(e->stream, e->kev[beta], 0));
     }
 }
 
@@ -1735,10 +1718,8 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
         // (key read once per call, accumulators written; ext never leaves the chip)
         const int nown = std::min(l + 1, beta * K);
         ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))));
-        static const int G = getenv("AESFHE_KS_G") && atoi(getenv("AESFHE_KS_G")) == 2 ? 2 : 1;  // A/B knob
-        const int blocks = 8 * ((B + G - 1) / G) * (ne * 32 / 8);
-        auto kern = G == 2 ? k_nttf_rows_ks<2> : k_nttf_rows_ks<1>;
-        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum);
+        const int blocks = 8 * B * (ne * 32 / 8);
+        hipLaunchKernelGGL(k_nttf_rows_ks<1>, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum);
     } else {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B * (accum ? 2 : 1)));
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
@@ -1770,7 +1751,7 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1));
         if (K + r < 1 || K + r > 16) throw_err(AESFHE_EUNSUPPORTED, "ModDown source width outside 1..16");
-        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, bconv_groups((long)N / 512 * B * 2, lk + 1), B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN,
+        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, 1, B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN,
                            invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv,
                            r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN);
     }
@@ -1810,12 +1791,11 @@ static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, i
     moddown_acc(e, acc.p, B, l, r, fin_add, o);
 }
 
-static bool g_no_ks_fuse = getenv("AESFHE_NO_KS_FUSE") != nullptr;  // A/B: unfused inner product
 static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, const aesfhe_key* k,
                       Opnd addend, aesfhe_ct* o, int r = 0) {
     const long neN = (long)(l + 1 + e->K) * e->N;
     Tmp ext(e, (size_t)ks_beta(e, l) * B * neN);
-    const bool fuse = fused_ntt(e) && !g_no_ks_fuse;
+    const bool fuse = fused_ntt(e);
     ks_modup(e, d, dbs, B, l, ext.p, fuse);
     ks_apply(e, d, dbs, ext.p, B, l, k, addend, o, r, fuse);
 }
@@ -2142,7 +2122,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
         const int l2 = l - 1, ne2 = l2 + 1 + K;
         const long ne2N = (long)ne2 * N, l2N = (long)(l2 + 1) * N;
         std::unique_ptr<Tmp> accg;
-        const bool fuse = fused_ntt(e) && !g_no_ks_fuse;
+        const bool fuse = fused_ntt(e);
         for (int j = 0; j < ng; j++) {
             if (!gkeys[j]) {
                 if (!sumq) {
@@ -2683,16 +2663,14 @@ extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, in
         aesfhe_ct* d3 = ct_new(e, ml * B, 3, l);
         {
             ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml));
-            static const int mo = getenv("AESFHE_POLY2_OUT") && atoi(getenv("AESFHE_POLY2_OUT")) == 8 ? 8 : 4;  // A/B knob
+            constexpr int mo = 4;  // outputs per launch (8: 219 VGPRs, 2 waves, measured slower)
             for (int t0 = 0; t0 < ml; t0 += mo)
                 for (int la = 0; la < nl;) {  // runs of limbs of one prime-size class
                     const bool big = e->chain.q[la] >= (1ULL << 42);
                     int lb = la + 1;
                     while (lb < nl && (e->chain.q[lb] >= (1ULL << 42)) == big) lb++;
-                    auto kern = mo == 8 ? (big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max, 8> : k_poly2_int<true, 0, 8>)
-                                               : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max, 8> : k_poly2_int<false, 0, 8>))
-                                        : (big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max, 4> : k_poly2_int<true, 0, 4>)
-                                               : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max, 4> : k_poly2_int<false, 0, 4>));
+                    auto kern = big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max, mo> : k_poly2_int<true, 0, mo>)
+                                    : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max, mo> : k_poly2_int<false, 0, mo>);
                     hipLaunchKernelGGL(kern, dim3(N / 256, lb - la, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny,
                                        (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, ml, t0, std::min(mo, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN);
                     la = lb;

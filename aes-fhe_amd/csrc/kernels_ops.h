@@ -3,7 +3,6 @@
 // oracle, oracle/ckks_oracle.c, which these kernels must match residue for residue).
 #pragma once
 #include "kernels.h"
-#include "ntt256.h"
 
 namespace aesfhe {
 
@@ -162,7 +161,7 @@ __global__ void k_lincomb(const u64* const* __restrict__ ptrs, const long* __res
             const int i = i0 + c;
             if (i < n) {
                 const int fi = (i * nl + l) * 2 + h;
-                acc += mulw(v[c], f[fi], ff[fi], q);
+                acc += mul_w(v[c], f[fi], ff[fi], q);
             }
         }
     }
@@ -194,7 +193,7 @@ __global__ void k_lincomb_many(const u64* const* __restrict__ ptrs, const long* 
         for (int j = 0; j < kManyMax; j++) {
             if (j < n) {
                 const int fi = ((i * n + j) * nl + l) * 2 + h;
-                acc += mulw(v[j], F[fi], FF[fi], q);
+                acc += mul_w(v[j], F[fi], FF[fi], q);
             }
         }
         o[(long)i * orow] = red_m(acc, q, qinv[l]);

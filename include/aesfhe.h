@@ -155,6 +155,13 @@ int aesfhe_key_switch(aesfhe_engine *eng, const aesfhe_key *sk_from, const aesfh
 /* kind: 0 secret 1 public 2 relin 3 galois; galois_elt for kind 3 */
 int aesfhe_key_info(const aesfhe_key *key, int32_t *kind, uint64_t *galois_elt);
 void aesfhe_key_free(aesfhe_key *key);
+/* Key serialisation (desilofhe keeps keys inside its Engine object,
+ * engine_context.py:62-73): kind, galois element, key seed (from which derived keys' randomness
+ * is drawn) and the residues.  out NULL: only the header fields and *words are returned. */
+int aesfhe_key_export(aesfhe_engine *eng, const aesfhe_key *key, int32_t *kind, uint64_t *galois_elt,
+                      uint64_t *keyseed, int64_t *words, uint64_t *out);
+int aesfhe_key_import(aesfhe_engine *eng, int32_t kind, uint64_t galois_elt, uint64_t keyseed,
+                      const uint64_t *in, int64_t words, aesfhe_key **out);
 
 /* ---- ciphertexts ------------------------------------------------------------------------ */
 /* coeffs: batch*N integer coefficients (encoded at the canonical scale of `level`);
@@ -170,6 +177,16 @@ int aesfhe_ct_info(const aesfhe_ct *ct, int32_t info[4]);
 int aesfhe_ct_export(aesfhe_engine *eng, const aesfhe_ct *ct, uint64_t *out);
 int aesfhe_ct_import(aesfhe_engine *eng, const uint64_t *in, int32_t batch, int32_t npoly,
                      int32_t level, aesfhe_ct **out);
+/* Device-resident transfer for the multi-GPU batch scatter / gather (the
+ * reference has no multi-GPU path -- it replaces the host round trip a desilofhe user would make
+ * through ciphertext serialisation, xor_service.py:166-182 being the reader side the survey pairs
+ * it with): residues of batch elements [start, start + count), layout as aesfhe_ct_export, to /
+ * from a caller-owned buffer on the engine's device (host memory for the CPU oracle).  Both
+ * synchronise the engine stream before returning. */
+int aesfhe_ct_export_device(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t start, int32_t count,
+                            void *dst);
+int aesfhe_ct_import_device(aesfhe_engine *eng, const void *src, int32_t batch, int32_t npoly,
+                            int32_t level, aesfhe_ct **out);
 int aesfhe_ct_copy(aesfhe_engine *eng, const aesfhe_ct *ct, aesfhe_ct **out);
 /* batch slicing / concatenation (all parts at one level and npoly) */
 int aesfhe_ct_slice(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t start, int32_t count,

@@ -989,6 +989,52 @@ int aesfhe_ct_import(aesfhe_engine *e, const uint64_t *in, int32_t B, int32_t np
     *out = c;
     return 0;
 }
+/* "Device" transfer: the oracle's memory is host memory, so these are the host copies the
+ * CPU (gloo) path of parallel.py hands to torch.distributed. */
+int aesfhe_ct_export_device(aesfhe_engine *e, const aesfhe_ct *c, int32_t start, int32_t count, void *dst) {
+    if (!c || !dst || start < 0 || count < 1 || start + count > c->B) return fail(AESFHE_EARG, "bad export range");
+    size_t per = (size_t)c->npoly * (c->level + 1) * e->N;
+    memcpy(dst, c->data + per * start, sizeof(u64) * per * count);
+    return 0;
+}
+int aesfhe_ct_import_device(aesfhe_engine *e, const void *src, int32_t B, int32_t np, int32_t level,
+                            aesfhe_ct **out) {
+    if (!src) return fail(AESFHE_EARG, "null source");
+    return aesfhe_ct_import(e, (const uint64_t *)src, B, np, level, out);
+}
+
+static size_t key_words(const aesfhe_engine *e, int kind) {
+    switch (kind) {
+        case 0: return (size_t)e->np * e->N;
+        case 1: return (size_t)2 * (e->L + 1) * e->N;
+        case 2: case 3: case 5: return (size_t)e->dnum * 2 * e->np * e->N;
+        default: return 0;
+    }
+}
+int aesfhe_key_export(aesfhe_engine *e, const aesfhe_key *k, int32_t *kind, uint64_t *galois,
+                      uint64_t *keyseed, int64_t *words, uint64_t *out) {
+    if (!k) return fail(AESFHE_EARG, "null key");
+    *kind = k->kind;
+    *galois = k->galois;
+    *keyseed = k->keyseed;
+    *words = (int64_t)key_words(e, k->kind);
+    if (out) memcpy(out, k->data, sizeof(u64) * (size_t)*words);
+    return 0;
+}
+int aesfhe_key_import(aesfhe_engine *e, int32_t kind, uint64_t galois, uint64_t keyseed,
+                      const uint64_t *in, int64_t words, aesfhe_key **out) {
+    size_t want = key_words(e, kind);
+    if (!in || !want) return fail(AESFHE_EARG, "unknown key kind %d", kind);
+    if ((size_t)words != want) return fail(AESFHE_EARG, "key of kind %d needs %zu words, got %lld", kind, want, (long long)words);
+    aesfhe_key *k = calloc(1, sizeof *k);
+    k->kind = kind;
+    k->galois = galois;
+    k->keyseed = keyseed;
+    k->data = malloc(sizeof(u64) * want);
+    memcpy(k->data, in, sizeof(u64) * want);
+    *out = k;
+    return 0;
+}
 int aesfhe_ct_copy(aesfhe_engine *e, const aesfhe_ct *c, aesfhe_ct **out) {
     aesfhe_ct *r = ct_new(e, c->B, c->npoly, c->level);
     memcpy(r->data, c->data, sizeof(u64) * (size_t)c->B * c->npoly * (c->level + 1) * e->N);

@@ -1,6 +1,11 @@
 """Multi-rank path on CPU (gloo, world_size 2): ciphertext-batch scatter from the client rank,
-one AES round per rank on its shard with identical seed-derived keys, gather, decrypt, check
-against FIPS-197.  Same code drives the GPUs under torchrun (backend RCCL or gloo)."""
+AES on each rank's shard with identical seed-derived keys (and disjoint nonce ranges), gather,
+decrypt, check against FIPS-197.  Same code (parallel.py) drives the GPUs under torchrun with
+the nccl backend (RCCL), where the buffers are device tensors.
+
+  * byte-major nibble round (aes_round.AESRoundEngine), even split;
+  * the bench's row-sliced layout (aes_round_bits.AESRowRound) running full 10-round AES-128
+    with bit-mode bootstrapping, uneven split (3 sets over 2 ranks), the C.1 vector in set 0."""
 import os
 import socket
 import sys
@@ -54,6 +59,60 @@ def _worker(rank, world, port, so, result_q):
         dist.destroy_process_group()
 
 
+def _worker_rows(rank, world, port, so, result_q):
+    sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from aes_xor_fhe._abi import Lib
+        from aes_xor_fhe.fhe import Engine
+        from aes_xor_fhe.aes_round_bits import AESRowRound
+        from aes_xor_fhe.bootstrap import Bootstrapper
+        from aes_xor_fhe.parallel import (gather_ciphertext, rank_nonce_start, scatter_ciphertext,
+                                          shard_range)
+        from aes_xor_fhe import aes_tables as T
+        e = Engine(_lib=Lib(so), log_n=10, max_level=30, special_primes=4, scale_bits=41, seed=3,
+                   nonce_start=rank_nonce_start(rank), thread_count=4)
+        sk = e.create_secret_key(1)
+        rlk = e.create_relinearization_key(sk)
+        R = AESRowRound(e, sk, e.create_public_key(sk), rlk)
+        bs = Bootstrapper(e, sk, rlk)
+        key = np.arange(16, dtype=np.uint8)
+        total = 3
+        blocks = np.random.default_rng(9).integers(0, 256, (total, R.n_blk, 16), dtype=np.uint8)
+        blocks[0, 0] = np.frombuffer(bytes.fromhex("00112233445566778899aabbccddeeff"), np.uint8)
+        st = R.encrypt_blocks(blocks) if rank == 0 else [[None] * 8 for _ in range(4)]
+        mine = [[scatter_ciphertext(e, c) for c in row] for row in st]
+        a, b = shard_range(total, world, rank)
+        assert all(c.batch == b - a for row in mine for c in row)
+        keys = [R.encrypt_round_key(rk) for rk in T.expand_key(key)]
+        out, nref = R.encrypt_aes128(mine, keys, bs)
+        full = [[gather_ciphertext(e, c) for c in row] for row in out]
+        if rank == 0:
+            got = R.decrypt_blocks(full)
+            want = np.stack([[T.encrypt_block(x, key) for x in blk] for blk in blocks])
+            ok = nref == 4 and bool(np.array_equal(got, want)) and \
+                bytes(got[0, 0]) == bytes.fromhex("69c4e0d86a7b0430d8cdb78070b4c55a")
+            result_q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, so, world=2, timeout=900):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, so, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=timeout)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return q.get(timeout=5)
+
+
 def test_shard_range():
     from aes_xor_fhe.parallel import shard_range
     parts = [shard_range(10, 4, r) for r in range(4)]
@@ -61,15 +120,10 @@ def test_shard_range():
 
 
 def test_two_rank_scatter_round_gather(oracle_lib):
-    import torch.multiprocessing as mp
     from conftest import ORACLE_SO
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(ORACLE_SO), q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(timeout=600)
-    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    assert q.get(timeout=5) is True
+    assert _spawn(_worker, str(ORACLE_SO)) is True
+
+
+def test_two_rank_rows_aes128_with_bootstrap_uneven(oracle_lib):
+    from conftest import ORACLE_SO
+    assert _spawn(_worker_rows, str(ORACLE_SO)) is True
