@@ -8,7 +8,9 @@ scatter of input ciphertexts from the client rank and the gather of the results.
 Transfers are device-resident: residues go from the engine's device buffers into torch tensors
 on the same GPU (aesfhe_ct_export_device, a device-to-device copy) and torch.distributed moves
 those tensors -- with the "nccl" backend that is RCCL over xGMI, GPU to GPU, never through host
-memory.  With the CPU oracle engine (tests, "gloo") the same code runs on host tensors.
+memory.  With the CPU oracle engine (tests, "gloo") the same code runs on host tensors; with the
+HIP engine under gloo (several ranks rehearsing on one GPU, which RCCL refuses) the residues
+are staged through host tensors.
 
 Keys are never moved: every rank derives the same keys from the shared engine seed; each rank
 encrypts with its own nonce range (`rank_nonce_start`) so no two ranks reuse randomness.
@@ -31,11 +33,32 @@ def rank_nonce_start(rank: int) -> int:
     return (int(rank) + 1) << 48
 
 
-def _torch_device(engine):
+def _torch_device(engine, group=None):
+    """Where the transfer buffers live: the engine's GPU under the nccl backend (RCCL moves
+    device memory), host memory otherwise (the CPU oracle; gloo, e.g. a multi-rank rehearsal
+    sharing one GPU, where RCCL cannot run two ranks on one device)."""
     import torch
-    if engine.on_device:
+    import torch.distributed as dist
+    if engine.on_device and dist.get_backend(group) == "nccl":
         return torch.device("cuda", engine.device_id)
     return torch.device("cpu")
+
+
+def _export(engine, ct, buf, start=0, count=None):
+    if buf.device.type == "cpu" and engine.on_device:  # gloo with the HIP engine: host staging
+        import torch
+        count = ct.batch - start if count is None else count
+        res = engine.export_residues(ct)[start:start + count]
+        buf[:count].copy_(torch.from_numpy(res.reshape(count, -1).view(np.int64)))
+    else:
+        engine.export_into(ct, buf.data_ptr(), start, count)
+
+
+def _import(engine, buf, batch, npoly, level):
+    if buf.device.type == "cpu" and engine.on_device:
+        arr = buf[:batch].numpy().view(np.uint64)
+        return engine.import_residues(arr.reshape(batch, npoly, level + 1, -1))
+    return engine.import_from(buf.data_ptr(), batch, npoly, level)
 
 
 def _sync(dev):
@@ -57,7 +80,7 @@ def scatter_ciphertext(engine, ct, src: int = 0, group=None):
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    dev = _torch_device(engine)
+    dev = _torch_device(engine, group)
     meta = torch.zeros(3, dtype=torch.int64, device=dev)
     if rank == src:
         meta = torch.tensor([ct.batch, ct.npoly, ct.level], dtype=torch.int64, device=dev)
@@ -74,14 +97,14 @@ def scatter_ciphertext(engine, ct, src: int = 0, group=None):
             t = torch.empty((smax, per), dtype=torch.int64, device=dev)
             _sync(dev)
             if b > a:
-                engine.export_into(ct, t.data_ptr(), a, b - a)
+                _export(engine, ct, t, a, b - a)
             parts.append(t)
     dist.scatter(out, parts, src=src, group=group)
     a, b = shard_range(batch, world, rank)
     if b == a:
         return None
     _sync(dev)  # RCCL wrote `out` on torch's stream
-    return engine.import_from(out.data_ptr(), b - a, npoly, level)
+    return _import(engine, out, b - a, npoly, level)
 
 
 def gather_ciphertext(engine, ct, dst: int = 0, group=None):
@@ -90,7 +113,7 @@ def gather_ciphertext(engine, ct, dst: int = 0, group=None):
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    dev = _torch_device(engine)
+    dev = _torch_device(engine, group)
     mine = torch.tensor([ct.batch if ct is not None else 0,
                          ct.npoly if ct is not None else -1,
                          ct.level if ct is not None else -1], dtype=torch.int64, device=dev)
@@ -106,11 +129,11 @@ def gather_ciphertext(engine, ct, dst: int = 0, group=None):
     buf = torch.zeros((smax, per), dtype=torch.int64, device=dev)
     _sync(dev)
     if ct is not None:
-        engine.export_into(ct, buf.data_ptr())
+        _export(engine, ct, buf)
     bufs = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
     dist.gather(buf, bufs, dst=dst, group=group)
     if rank != dst:
         return None
     full = torch.cat([bufs[r][:metas[r][0]] for r in range(world)], 0).contiguous()
     _sync(dev)
-    return engine.import_from(full.data_ptr(), full.shape[0], npoly, level)
+    return _import(engine, full, full.shape[0], npoly, level)

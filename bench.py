@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark: homomorphic AES-128 rounds on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-check]
+                    [--no-cpu-baseline] [--cpu-extended] [--no-configs] [--aes10-batch S]
 
 One *step* = one full middle AES-128 round (ShiftRows -> SubBytes -> MixColumns ->
 AddRoundKey) at N = 2^16, L = 30 over a batch of B ciphertext sets per GPU.  Default layout
@@ -9,17 +10,30 @@ AddRoundKey) at N = 2^16, L = 30 over a batch of B ciphertext sets per GPU.  Def
 carrying 8192 AES blocks; layout "bytes" (aes_xor_fhe.aes_round.AESRoundEngine): a set is one
 byte-major (hi, lo) Zeta-16 nibble pair carrying 2048 blocks.  Inputs (encrypted synthetic
 random AES states) and the encrypted round key are resident in HBM before the timed region.
+The timed steps run with kernel profiling OFF; a separate profiled pass afterwards gives the
+roofline figures.  Every output is decrypted and checked against FIPS-197 (outside the timed
+region) unless --no-check.
+
+Also reported (rank 0, one JSON line):
+  aes128_10_rounds -- full AES-128 (ARK0 + 10 rounds, bit-mode bootstrapping) of --aes10-batch
+                      sets per GPU (16 x 8192 = 131 072 blocks = BASELINE config 4's 64 x 2048);
+  configs          -- BASELINE configs 2 (SubBytes via the reference-order
+                      sbox_service.sub_bytes_array, 1 ct) and 3 (nibble-domain ShiftRows +
+                      MixColumns, 2048 blocks/ct), FIPS-verified (N = 1 only);
+  scatter_gather   -- N > 1: one set per rank encrypted on rank 0, scattered GPU-to-GPU with
+                      RCCL (parallel.scatter_ciphertext, device tensors), one round per rank,
+                      gathered back and verified on rank 0; times reported separately;
+  roofline         -- the NTT kernels (dominant family): algorithmic bytes per launch / average
+                      launch duration from HIP events on the engine stream (profiled pass);
+                      peak 8 TB/s HBM3E (MI355X_MICROARCH.md);
+  cpu_baseline     -- the CPU oracle (oracle/, a C restatement of the same engine) running one
+                      full round of one set (8192 blocks) at N = 2^16, L = 30, measured (not
+                      extrapolated), all of this process's OMP threads; rank 0 at N = 1 only.
 
 Multi-GPU (torchrun, one process per GPU): every rank runs its own shard of ciphertexts --
-the path is embarrassingly parallel (no data-path collective), so the scaling is weak.  The
-barrier and the max-over-ranks reduction of the step time use torch.distributed (gloo).
-
-Printed on rank 0: ONE JSON line with metric/value/... plus
-  roofline     -- the NTT kernels (dominant family): algorithmic bytes per launch / average
-                  launch duration, from HIP events recorded on the engine stream over the
-                  timed region; peak 8 TB/s HBM3E (MI355X_MICROARCH.md);
-  cpu_baseline -- the CPU oracle (oracle/, a C restatement of the same engine) running the
-                  same round on a bounded sample, rank 0 only.
+the path is embarrassingly parallel (no data-path collective), so the scaling is weak.
+Barriers, the max-over-ranks reduction and the scatter/gather use torch.distributed with the
+nccl backend (RCCL) on GPUs (gloo without one).
 """
 from __future__ import annotations
 
@@ -37,7 +51,7 @@ sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
 
 PEAK_HBM_GBS = 8000.0
 METRIC = "AES-128 blocks/sec (homomorphic full round) at N=2^16, L=30; 1/2/4/8 MI355X"
-
+SEED = 0x5EED5EED  # shared by every rank: identical keys without key traffic
 
 PMC_FILE = ROOT / "profiles" / "r01" / "pmc" / "ntt_traffic.json"
 PMC_NOTE = ("HBM bytes per NTT launch = algorithmic bytes x the HBM/algorithmic ratio measured by "
@@ -66,10 +80,18 @@ def parse():
     ap.add_argument("--special-primes", type=int, default=10,
                     help="K special primes = key-switch digit size alpha (dnum = ceil((L+1)/K))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--check", action="store_true", help="decrypt and verify against FIPS-197")
+    ap.add_argument("--cpu-extended", action="store_true",
+                    help="also time the CPU oracle at 8 threads and on configs 2 and 3 (minutes)")
+    ap.add_argument("--no-check", dest="check", action="store_false",
+                    help="skip decrypting and verifying against FIPS-197")
+    ap.add_argument("--check", dest="check", action="store_true")
+    ap.set_defaults(check=True)
+    ap.add_argument("--no-configs", action="store_true", help="skip the config 2 / 3 legs")
+    ap.add_argument("--profile-steps", type=int, default=2,
+                    help="profiled (HIP-event) round steps after the timed region, for the roofline")
     ap.add_argument("--aes10-ppc", type=int, default=0,
                     help="bit-ciphertext pairs per bootstrap call (0: 32 / aes10-batch)")
-    ap.add_argument("--aes10-batch", type=int, default=8,
+    ap.add_argument("--aes10-batch", type=int, default=16,
                     help="ciphertext sets for the full 10-round AES-128 measurement (0: skip)")
     return ap.parse_args()
 
@@ -97,38 +119,39 @@ class RoundDriver:
     def round(self, st, key):
         return self.R.round(st, key) if self.layout == "rows" else self.R.round(st[0], st[1], key)
 
-    def sub_bytes(self, st):
-        """Bounded CPU sample: SubBytes of the first state row (rows) / the nibble pair (bytes)."""
-        if self.layout == "rows":
-            return self.R.sub_bytes(st[:1])
-        return self.R.sub_bytes(st[0], st[1])
-
     def decrypt(self, st):
         return self.R.decrypt_blocks(st) if self.layout == "rows" else self.R.decrypt_blocks(*st)
 
+    def cts(self, st):
+        """The state's ciphertexts, flat (for scatter / gather)."""
+        return [c for row in st for c in row] if self.layout == "rows" else list(st)
 
-def setup_engine(args, device):
+    def from_cts(self, cts):
+        return [cts[8 * r:8 * r + 8] for r in range(4)] if self.layout == "rows" else tuple(cts)
+
+
+def setup_engine(args, device, rank):
     from aes_xor_fhe.fhe import Engine
-    eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes, device_id=device)
+    from aes_xor_fhe.parallel import rank_nonce_start
+    eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes,
+                 device_id=device, seed=SEED, nonce_start=rank_nonce_start(rank))
     sk = eng.create_secret_key(1)
     pk = eng.create_public_key(sk)
     rlk = eng.create_relinearization_key(sk)
     cjk = eng.create_conjugation_key(sk)
     drv = RoundDriver(args.layout, eng, sk, pk, rlk, cjk)
-    drv.keys = (sk, rlk, cjk)
+    drv.keys = (sk, pk, rlk, cjk)
     return eng, drv
 
 
-def aes128_full(args, eng, drv, rank, barrier, dist):
+def aes128_full(args, eng, drv, rank, barrier, allmax):
     """Full AES-128 (ARK0 + 10 rounds, FIPS-197 5.1) with bit-mode bootstrapping on the rows
     layout: a warm-up encryption of the same shape (bootstrap plaintexts, device pool), then one
     timed encryption of args.aes10_batch ciphertext sets (x 8192 blocks at N = 2^16)."""
-    import torch
-
     from aes_xor_fhe import aes_tables as T
     from aes_xor_fhe.bootstrap import Bootstrapper
     R = drv.R
-    sk, rlk, cjk = drv.keys
+    sk, _, rlk, cjk = drv.keys
     t0 = time.perf_counter()
     bs = Bootstrapper(eng, sk, rlk, cjk)
     eng.synchronize()
@@ -151,17 +174,13 @@ def aes128_full(args, eng, drv, rank, barrier, dist):
     t0 = time.perf_counter()
     out, nref = R.encrypt_aes128(st, keys, bs, timings=tm, pairs_per_call=ppc)
     barrier()
-    el = time.perf_counter() - t0
+    el = allmax(time.perf_counter() - t0)
     timed_mallocs = eng.pool_stats()["mallocs"] - m0
-    if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
     ok = None
     if args.check:
         got = R.decrypt_blocks(out)
-        ok = bool(all((got[i] == np.stack([T.encrypt_block(b, key) for b in blocks[i]])).all()
-                      for i in range(nb)))
+        want = np.stack([[T.encrypt_block(b, key) for b in blk] for blk in blocks])
+        ok = bool(np.array_equal(got, want))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     return {"metric": "AES-128 blocks/sec (10 rounds incl. bootstrapping)",
             "value": round(nb * R.n_blk * world / el, 2), "unit": "blocks/s",
@@ -175,50 +194,146 @@ def aes128_full(args, eng, drv, rank, barrier, dist):
             "timed_mallocs": timed_mallocs}
 
 
-def cpu_baseline(args):
-    """Oracle (CPU restatement) on a bounded sample of the same workload, scaled to blocks/s.
+def _timed(eng, fn, reps=1):
+    eng.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = fn()
+    eng.synchronize()
+    return out, (time.perf_counter() - t0) / reps
 
-    The full round at N=2^16 takes minutes on the oracle, so the sample is: SubBytes of one
-    state row (rows layout) / nibble pair (bytes layout) at N=2^16, L=30 (timed), scaled by the oracle's own full-round/SubBytes
-    time ratio measured at N=2^12, L=30 on the same op sequence (same layout as the GPU run)."""
-    sys.path.insert(0, str(ROOT / "tests"))
+
+def config_legs(args, eng, drv):
+    """BASELINE configs 2 and 3 on this engine (N = 2^16, L = 30), each timed after a warm-up
+    call of the same shape and verified against FIPS-197."""
+    from types import SimpleNamespace
+
+    from aes_xor_fhe import aes_tables as T
+    from aes_xor_fhe.aes_round import AESRoundEngine
+    from aes_xor_fhe.sbox.sbox_service import SBoxService
+    from aes_xor_fhe.utils import zeta_decode, zeta_encode
+    sk, pk, rlk, cjk = drv.keys
+    out = {}
+    # config 2: SubBytes of one ciphertext (32768 bytes = 2048 blocks), reference op order
+    ctx = SimpleNamespace(engine=eng, relinearization_key=rlk)
+    sb = SBoxService(ctx)
+    x = np.random.default_rng(1).integers(0, 256, eng.slot_count)
+    ct = eng.encrypt(zeta_encode(x, modulus=256), pk)
+    c2 = {"workload": "SubBytes, 1 ciphertext (32768 bytes = 2048 blocks), zeta-256 byte, "
+                      "degree-255 hi/lo LUT polynomials (sbox_service.sub_bytes_array)"}
+    for name, fn in (("reference_order", sb.sub_bytes_array), ("fused", sb.sub_bytes_fused)):
+        fn(ct)  # warm-up
+        res, t = _timed(eng, lambda: fn(ct))
+        ok = None
+        if args.check:
+            ok = bool(np.array_equal(zeta_decode(eng.decrypt(res, sk), modulus=256), T.SBOX[x]))
+        c2[name] = {"value": round(2048 / t, 1), "unit": "blocks/s", "ms": round(t * 1e3, 2),
+                    "verified": ok, "level_drop": ct.level - res.level}
+    out["config2_subbytes"] = c2
+    # config 3: ShiftRows + MixColumns, byte-major Zeta-16 nibble pair (2048 blocks per ct)
+    R = AESRoundEngine(eng, sk, pk, rlk, cjk)
+    c3 = {"workload": "ShiftRows+MixColumns, byte-major zeta-16 (hi, lo) nibble pair, 2048 "
+                      "blocks/ct (aes_round.AESRoundEngine: rotate-mask terms + nibble XOR LUTs)"}
+    for nb in (1, 8):
+        blocks = np.random.default_rng(2025 + nb).integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
+        h, l = R.encrypt_blocks(blocks)
+
+        def sm():
+            return R.mix_columns(R.shift_mix_terms(h), R.shift_mix_terms(l))
+        sm()
+        res, t = _timed(eng, sm)
+        ok = None
+        if args.check:
+            ok = bool(np.array_equal(R.decrypt_blocks(*res), T.mix_columns(T.shift_rows(blocks))))
+        c3[f"batch_{nb}"] = {"value": round(nb * R.n_blk / t, 1), "unit": "blocks/s",
+                             "ms": round(t * 1e3, 2), "verified": ok}
+    out["config3_shiftrows_mixcolumns"] = c3
+    return out
+
+
+def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
+    """One set per rank encrypted on rank 0, scattered to the ranks (device tensors, RCCL),
+    one round per rank, gathered and verified on rank 0.  Times: scatter and gather of the
+    whole state (32 bit ciphertexts per set at the round's input/output levels)."""
+    from aes_xor_fhe import aes_tables as T
+    from aes_xor_fhe.parallel import gather_ciphertext, scatter_ciphertext
+    rk = np.random.default_rng(31).integers(0, 256, 16, dtype=np.uint8)
+    blocks = np.random.default_rng(77).integers(0, 256, (world, drv.n_blk, 16), dtype=np.uint8)
+    cts = drv.cts(drv.encrypt(blocks)) if rank == 0 else [None] * (32 if drv.layout == "rows" else 2)
+    key = drv.key(rk)
+    barrier()
+    t0 = time.perf_counter()
+    mine = [scatter_ciphertext(eng, c) for c in cts]
+    barrier()
+    t_sc = allmax(time.perf_counter() - t0)
+    bytes_in = sum(c.batch * c.npoly * (c.level + 1) for c in mine) * 8 * (1 << eng.log_coeff_count)
+    res = drv.cts(drv.round(drv.from_cts(mine), key))
+    barrier()
+    t0 = time.perf_counter()
+    full = [gather_ciphertext(eng, c) for c in res]
+    barrier()
+    t_ga = allmax(time.perf_counter() - t0)
+    ok = None
+    if rank == 0 and args.check:
+        ok = bool((drv.decrypt(drv.from_cts(full)) == T.aes_round(blocks, rk)).all())
+    return {"sets": world, "bytes_per_rank_in": bytes_in, "scatter_ms": round(t_sc * 1e3, 2),
+            "gather_ms": round(t_ga * 1e3, 2),
+            "scatter_gbs_per_rank": round(bytes_in / t_sc / 1e9, 2) if t_sc else None,
+            "verified": ok, "path": "aesfhe_ct_export_device -> torch.distributed scatter/gather "
+                                    "(nccl backend = RCCL over xGMI) -> aesfhe_ct_import_device"}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(args):
+    """The oracle (CPU restatement of the same engine) timing one full middle round of one set
+    at the GPU workload's parameters -- measured, not extrapolated; OMP over limbs with this
+    process's OMP_NUM_THREADS (16 on the GPU box)."""
     import subprocess
     so = ROOT / "oracle" / "_build" / "liboracle_ckks.so"
     if not so.exists():
         subprocess.run(["make", "-C", str(ROOT / "oracle")], check=True, stdout=subprocess.DEVNULL)
+    from aes_xor_fhe import aes_tables as T
     from aes_xor_fhe._abi import Lib
     from aes_xor_fhe.fhe import Engine
     lib = Lib(so)
     threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
-    times = {}
-    for log_n in (12, args.log_n):
-        eng = Engine(log_n=log_n, max_level=args.max_level, special_primes=args.special_primes, thread_count=threads, _lib=lib)
+
+    def round_time(nthr):
+        eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes,
+                     thread_count=nthr, seed=SEED, _lib=lib)
         sk = eng.create_secret_key(1)
-        pk = eng.create_public_key(sk)
-        R = RoundDriver(args.layout, eng, sk, pk, eng.create_relinearization_key(sk),
-                        eng.create_conjugation_key(sk),
-                        rotation_keys={} if log_n != 12 else None)
-        rng = np.random.default_rng(log_n)
+        R = RoundDriver(args.layout, eng, sk, eng.create_public_key(sk), eng.create_relinearization_key(sk),
+                        eng.create_conjugation_key(sk))
+        rng = np.random.default_rng(5)
         blocks = rng.integers(0, 256, (1, R.n_blk, 16), dtype=np.uint8)
-        st = R.encrypt(blocks)
+        rk = rng.integers(0, 256, 16, dtype=np.uint8)
+        st, key = R.encrypt(blocks), R.key(rk)
         t0 = time.perf_counter()
-        R.sub_bytes(st)
-        times[(log_n, "sb")] = time.perf_counter() - t0
-        if log_n == 12:
-            key = R.key(rng.integers(0, 256, 16, dtype=np.uint8))
-            t0 = time.perf_counter()
-            R.round(st, key)
-            times[(log_n, "round")] = time.perf_counter() - t0
-    ratio = times[(12, "round")] / times[(12, "sb")]
-    est_round = times[(args.log_n, "sb")] * ratio
-    n_blk = (1 << (args.log_n - 1)) // (4 if args.layout == "rows" else 16)
-    return {
-        "value": n_blk / est_round, "unit": "blocks/s", "cores": threads, "kind": "port",
-        "sample": (f"oracle SubBytes of 1 row/pair ({args.layout} layout, {n_blk} blocks/set) at N=2^{args.log_n} "
-                   f"L={args.max_level}: {times[(args.log_n, 'sb')]:.2f} s, scaled by the oracle's "
-                   f"round/SubBytes ratio {ratio:.2f} measured at N=2^12 -> est. {est_round:.1f} s "
-                   f"per round"),
-    }
+        out = R.round(st, key)
+        t = time.perf_counter() - t0
+        ok = bool((R.decrypt(out) == T.aes_round(blocks, rk)).all())
+        return R.n_blk, t, ok
+
+    n_blk, t, ok = round_time(threads)
+    rec = {"value": round(n_blk / t, 2), "unit": "blocks/s", "cores": threads, "kind": "port",
+           "measured": True, "verified": ok, "os_cpu_count": os.cpu_count(), "cpu_model": _cpu_model(),
+           "sample": (f"oracle (oracle/ckks_oracle.c, gcc -O2, OpenMP over limbs, {threads} threads) "
+                      f"timing one full middle AES-128 round ({args.layout} layout) of one set = "
+                      f"{n_blk} blocks at N=2^{args.log_n}, L={args.max_level}, K={args.special_primes}: "
+                      f"{t:.1f} s, FIPS-verified")}
+    if args.cpu_extended:
+        _, t8, ok8 = round_time(8)
+        rec["threads_8"] = {"value": round(n_blk / t8, 2), "s": round(t8, 1), "verified": ok8}
+    return rec
 
 
 def main():
@@ -226,21 +341,39 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
     import torch
-
-    from aes_xor_fhe import aes_tables as T
-
+    dist = None
     # one rank per GPU; more ranks than GPUs (a multi-rank rehearsal on a 1-GPU box) share them
     ndev = torch.cuda.device_count() or 1
     device = local % ndev
-    eng, R = setup_engine(args, device)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() and ndev >= world else "gloo"
+        if torch.cuda.is_available():
+            torch.cuda.set_device(device)
+        dist.init_process_group(backend, rank=rank, world_size=world)
+    from aes_xor_fhe import aes_tables as T
+
+    eng, R = setup_engine(args, device, rank)
     if torch.cuda.is_available():
         torch.cuda.set_device(device)
+    red_dev = torch.device("cuda", device) if dist is not None and dist.get_backend() == "nccl" else torch.device("cpu")
+
+    def barrier():
+        eng.synchronize()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    def allmax(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     rng = np.random.default_rng(1000 + rank)
     blocks = rng.integers(0, 256, (args.batch, R.n_blk, 16), dtype=np.uint8)
     rk = np.random.default_rng(25073102).integers(0, 256, 16, dtype=np.uint8)
@@ -255,51 +388,61 @@ def main():
         out = step()
     eng.synchronize()
 
-    def barrier():
-        eng.synchronize()
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-
     import ctypes as C
-    eng._check(eng._lib.engine_profile(eng._h, 1 | 2))  # ntt + keyswitch families only
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = step()
     barrier()
-    elapsed = time.perf_counter() - t0
-    n_ntt, ms_ntt, by_ntt = C.c_int64(), C.c_double(), C.c_double()
-    eng._check(eng._lib.engine_profile_read(eng._h, b"ntt", C.byref(n_ntt), C.byref(ms_ntt), C.byref(by_ntt)))
-    n_ks, ms_ks, by_ks = C.c_int64(), C.c_double(), C.c_double()
-    eng._check(eng._lib.engine_profile_read(eng._h, b"keyswitch", C.byref(n_ks), C.byref(ms_ks), C.byref(by_ks)))
-    eng._check(eng._lib.engine_profile(eng._h, 0))
-
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    elapsed = allmax(time.perf_counter() - t0)
     round_pool = eng.pool_stats()
     ok = None
     if args.check:
-        got = R.decrypt(out)
-        ok = bool((got == T.aes_round(blocks, rk)).all())
+        ok = bool((R.decrypt(out) == T.aes_round(blocks, rk)).all())
+        if dist is not None:
+            ok = allmax(0.0 if ok else 1.0) == 0.0
 
-    aes10 = None
-    if args.aes10_batch > 0 and args.layout == "rows":
-        # the round's buffers and cached blocks (other sizes) would otherwise crowd the device
-        # inside the timed 10-round run; release them between the two workloads
-        del st, out
-        import gc
+    # profiled pass (not timed): per-launch HIP events of the ntt and keyswitch families
+    n_ntt, ms_ntt, by_ntt = C.c_int64(), C.c_double(), C.c_double()
+    n_ks, ms_ks, by_ks = C.c_int64(), C.c_double(), C.c_double()
+    prof_ms = 0.0
+    if args.profile_steps > 0:
+        eng._check(eng._lib.engine_profile(eng._h, 1 | 2))
+        eng.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.profile_steps):
+            out = step()
+        eng.synchronize()
+        prof_ms = (time.perf_counter() - t0) * 1e3 / args.profile_steps
+        eng._check(eng._lib.engine_profile_read(eng._h, b"ntt", C.byref(n_ntt), C.byref(ms_ntt), C.byref(by_ntt)))
+        eng._check(eng._lib.engine_profile_read(eng._h, b"keyswitch", C.byref(n_ks), C.byref(ms_ks), C.byref(by_ks)))
+        eng._check(eng._lib.engine_profile(eng._h, 0))
+
+    # the round's buffers and cached blocks (other sizes) would otherwise crowd the device in
+    # the following legs; release them between workloads
+    del st, out
+    import gc
+    gc.collect()
+    eng.pool_trim()
+
+    sg = None
+    if dist is not None:
+        sg = scatter_gather_leg(args, eng, R, rank, world, barrier, allmax)
         gc.collect()
         eng.pool_trim()
-        aes10 = aes128_full(args, eng, R, rank, barrier, dist)
+    configs = None
+    if world == 1 and not args.no_configs and args.log_n == 16:
+        configs = config_legs(args, eng, R)
+        gc.collect()
+        eng.pool_trim()
+    aes10 = None
+    if args.aes10_batch > 0 and args.layout == "rows":
+        aes10 = aes128_full(args, eng, R, rank, barrier, allmax)
 
     blocks_per_step = args.batch * R.n_blk * world
     value = blocks_per_step * args.steps / elapsed
     if rank == 0:
+        steps_prof = max(args.profile_steps, 1)
         avg_launch_ms = ms_ntt.value / max(n_ntt.value, 1)
         achieved = by_ntt.value / (ms_ntt.value * 1e-3) / 1e9 if ms_ntt.value else 0.0
         rec = {
@@ -333,14 +476,18 @@ def main():
                 "frac_per_pass_rw": round(2 * achieved / PEAK_HBM_GBS, 4),  # each pass's own read+write
                 "traffic": traffic_per_launch(by_ntt.value / max(n_ntt.value, 1)),
                 "traffic_source": PMC_NOTE,
+                "measured_over": f"{args.profile_steps} profiled round steps after the timed region",
                 "launches": n_ntt.value, "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "alg_bytes_per_launch": round(by_ntt.value / max(n_ntt.value, 1)),
-                "ntt_share_of_step": round(ms_ntt.value / (elapsed * 1e3), 3),
+                "ntt_share_of_step": round(ms_ntt.value / steps_prof / max(prof_ms, 1e-9), 3),
                 "keyswitch_kernels_gbs": round(by_ks.value / (ms_ks.value * 1e-3) / 1e9, 1) if ms_ks.value else None,
-                "keyswitch_share_of_step": round(ms_ks.value / (elapsed * 1e3), 3),
+                "keyswitch_share_of_step": round(ms_ks.value / steps_prof / max(prof_ms, 1e-9), 3),
+                "profiled_ms_per_step": round(prof_ms, 1),
             },
             "cpu_baseline": None,
             "aes128_10_rounds": aes10,
+            "configs": configs,
+            "scatter_gather": sg,
         }
         if not args.no_cpu_baseline and world == 1:
             try:

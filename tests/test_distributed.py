@@ -127,3 +127,28 @@ def test_two_rank_scatter_round_gather(oracle_lib):
 def test_two_rank_rows_aes128_with_bootstrap_uneven(oracle_lib):
     from conftest import ORACLE_SO
     assert _spawn(_worker_rows, str(ORACLE_SO)) is True
+
+
+@pytest.mark.gpu
+def test_rccl_device_scatter_gather_single_rank(product_lib, gpu_available):
+    """The device-tensor path of parallel.py under the nccl backend (RCCL): scatter and gather
+    through torch CUDA tensors filled / read by aesfhe_ct_export_device / import_device, uneven
+    shares included (world 1 on the 1-GPU test box; the driver's 8-GPU bench runs world 8)."""
+    import torch
+    import torch.distributed as dist
+    from aes_xor_fhe.fhe import Engine
+    from aes_xor_fhe.parallel import gather_ciphertext, scatter_ciphertext
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        torch.cuda.set_device(0)
+        e = Engine(_lib=product_lib, log_n=12, max_level=6, special_primes=2, seed=3)
+        sk = e.create_secret_key()
+        ct = e.encrypt(np.random.default_rng(0).standard_normal((3, 64)), sk)
+        mine = scatter_ciphertext(e, ct)
+        assert mine.batch == 3
+        assert np.array_equal(e.export_residues(mine), e.export_residues(ct))
+        back = gather_ciphertext(e, e.multiply(mine, 2.0))
+        want = e.export_residues(e.multiply(ct, 2.0))
+        assert np.array_equal(e.export_residues(back), want)
+    finally:
+        dist.destroy_process_group()
