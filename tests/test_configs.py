@@ -1,0 +1,101 @@
+"""BASELINE.json configs 1 and 5 at their own parameters.
+
+Config 1 -- "Single AES round, 1 ciphertext, N=2^14, L=8, CPU engine_context (test_total.py
+plumbing)": the reference's AddRoundKey driver (test_all_process.py:12-48: EngineContext ->
+EngineWrapper -> XORService -> AESFHERound.full_round, seeds 25073101 / 25073102) at N = 2^14,
+L = 8 (the 128-bit budget of N = 2^14 leaves K = 1 special prime), checked against the reference's
+own decoded output for those seeds (tests/golden/golden.npz "ark16_*", made by
+tests/golden/make_golden.py) and against state ^ key on a full 8192-byte ciphertext; on the CPU
+oracle and on the HIP engine (residue-identical to each other).
+
+Config 5 -- "Full AES-128 10 rounds, N=2^17, L=35, batch=512 ciphertexts over 8 GPUs": one
+rank's shard runs on one GPU.  Bit-exact ct x ct multiply + rotation against the oracle at
+N = 2^17, L = 35, and full AES-128 (ARK0 + 10 rounds with bit-mode bootstrapping) at those
+parameters, FIPS-197 verified (C.1 vector in block 0).
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from aes_xor_fhe import aes_tables as T
+from aes_xor_fhe.engine_context import EngineContext
+from aes_xor_fhe.new import AESFHERound
+from aes_xor_fhe.xor_service import EngineWrapper, XORConfig, XORService
+
+GOLD = np.load(Path(__file__).resolve().parent / "golden" / "golden.npz")
+CONFIG1 = dict(log_n=14, special_primes=1)
+
+
+def _config1(lib, seed=25073101):
+    ctx = EngineContext(signature=2, max_level=8, seed=seed, _lib=lib, **CONFIG1)
+    e = ctx.engine
+    assert (e.log_coeff_count, e.max_level, e.slot_count) == (14, 8, 8192)
+    wrap = EngineWrapper(XORConfig(max_level=8), ctx=ctx)
+    ark = AESFHERound(wrap, XORService(wrap))
+    out16 = ark.full_round(GOLD["ark16_state"], GOLD["ark16_key"], recombine=True)
+    assert np.array_equal(out16, GOLD["ark16_out"])
+    assert np.array_equal(out16, GOLD["ark16_state"] ^ GOLD["ark16_key"])
+    rng = np.random.default_rng(25073102)
+    st, ky = (rng.integers(0, 256, 8192, dtype=np.uint8) for _ in range(2))
+    hi, lo = ark.full_round(st, ky, recombine=False)
+    assert min(hi.level, lo.level) >= 0
+    from aes_xor_fhe.new import decrypt_and_recombine
+    assert np.array_equal(decrypt_and_recombine(hi, lo, wrap, length=8192), st ^ ky)
+    return e.export_residues(hi)
+
+
+def test_config1_ark_oracle(oracle_lib):
+    _config1(oracle_lib)
+
+
+@pytest.mark.gpu
+def test_config1_ark_gpu_matches_oracle(product_lib, oracle_lib, gpu_available):
+    assert np.array_equal(_config1(product_lib), _config1(oracle_lib))
+
+
+CONFIG5 = dict(log_n=17, max_level=35, special_primes=12)
+
+
+@pytest.mark.gpu
+def test_config5_mul_rotate_bit_exact(product_lib, oracle_lib, gpu_available):
+    from aes_xor_fhe.fhe import Engine
+    g = Engine(_lib=product_lib, seed=5, **CONFIG5)
+    o = Engine(_lib=oracle_lib, seed=5, thread_count=8, **CONFIG5)
+    assert g.primes == o.primes and g.slot_count == 65536
+    res = []
+    z = np.exp(-2j * np.pi * np.random.default_rng(3).integers(0, 256, g.slot_count) / 256)
+    for e in (g, o):
+        sk = e.create_secret_key(7)
+        ct = e.encrypt(z, e.create_public_key(sk))
+        m = e.multiply(ct, ct, e.create_relinearization_key(sk))
+        r = e.rotate(m, e.create_fixed_rotation_key(sk, -4096), -4096)
+        res.append((e.export_residues(m), e.export_residues(r)))
+        if e is g:
+            np.testing.assert_allclose(e.decrypt(r, sk), np.roll(z * z, -4096), atol=1e-5)
+    assert np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1])
+
+
+@pytest.mark.gpu
+def test_config5_aes128_ten_rounds(product_lib, gpu_available):
+    from aes_xor_fhe.aes_round_bits import AESRowRound
+    from aes_xor_fhe.bootstrap import Bootstrapper
+    from aes_xor_fhe.fhe import Engine
+    e = Engine(_lib=product_lib, seed=17, **CONFIG5)
+    sk = e.create_secret_key()
+    rlk = e.create_relinearization_key(sk)
+    R = AESRowRound(e, sk, e.create_public_key(sk), rlk)
+    assert R.n_blk == 16384
+    bs = Bootstrapper(e, sk, rlk)
+    key = np.arange(16, dtype=np.uint8)
+    blocks = np.random.default_rng(5).integers(0, 256, (1, R.n_blk, 16), dtype=np.uint8)
+    blocks[0, 0] = np.frombuffer(bytes.fromhex("00112233445566778899aabbccddeeff"), np.uint8)
+    st = R.encrypt_blocks(blocks)
+    one = R.round(st, R.encrypt_round_key(T.expand_key(key)[1]))       # one middle round
+    assert np.array_equal(R.decrypt_blocks(one), T.aes_round(blocks, T.expand_key(key)[1]))
+    out, nref = R.encrypt_aes128(st, [R.encrypt_round_key(k) for k in T.expand_key(key)], bs)
+    got = R.decrypt_blocks(out)
+    want = np.stack([[T.encrypt_block(b, key) for b in blk] for blk in blocks])
+    assert np.array_equal(got, want)
+    assert bytes(got[0, 0]) == bytes.fromhex("69c4e0d86a7b0430d8cdb78070b4c55a")
