@@ -187,19 +187,29 @@ class AESRowRound:
                 out[r][j + 4] = e.slice(yb, k * nb, nb)
         return out
 
+    # A round multiplies the slot error of its input by ~10-15 (the S-box's Walsh polynomial sums
+    # ~10 products, MixColumns chains three), and bit-mode bootstrapping returns its input error
+    # squared: so the error at a refresh must stay ~1e-2.  Three rounds from a fresh encryption
+    # or refresh reach ~5e-3 at N = 2^16 / 2^17 (measured, tools/aes10_diag.py); a fourth (L = 35
+    # allows it by levels) reached 0.12 at N = 2^17 and the run diverged.
+    MAX_ROUNDS_PER_REFRESH = 3
+
     def encrypt_aes128(self, bits, keys, bs, timings: dict | None = None, pairs_per_call: int = 8):
         """AES-128 encryption of the bit state under the 11 encrypted round keys `keys`
         (FIPS-197 section 5.1), bootstrapping with `bs` (a bootstrap.Bootstrapper) as the level
-        budget requires.  Returns the state and the number of refreshes."""
+        budget requires, and at least every MAX_ROUNDS_PER_REFRESH rounds.  Returns the state
+        and the number of refreshes."""
         import time
         stc = len(bs.stc_bits)
         S = self.add_round_key(bits, keys[0])
         refreshes = 0
+        since = 0
         for rnd in range(1, 11):
             final = rnd == 10
             need = self.FINAL_DEPTH if final else self.ROUND_DEPTH
             lvl = min(c.level for row in S for c in row)
-            if lvl < need or (not final and lvl - need < stc):
+            if lvl < need or (not final and lvl - need < stc) or since >= self.MAX_ROUNDS_PER_REFRESH:
+                since = 0
                 t0 = time.perf_counter()
                 S = self.refresh(S, bs, pairs_per_call)
                 refreshes += 1
@@ -209,6 +219,7 @@ class AESRowRound:
             t0 = time.perf_counter()
             lvl = min(c.level for row in S for c in row)
             S = self.final_round(S, keys[rnd]) if final else self.round(S, keys[rnd])
+            since += 1
             if timings is not None:
                 self.e.synchronize()
                 dt = time.perf_counter() - t0

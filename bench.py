@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--max-level", type=int, default=30)
     ap.add_argument("--special-primes", type=int, default=10,
                     help="K special primes = key-switch digit size alpha (dnum = ceil((L+1)/K))")
+    ap.add_argument("--scale-bits", type=int, default=40,
+                    help="log2 of the top-level scale (config 5, N=2^17 L=35: 44)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-extended", action="store_true",
                     help="also time the CPU oracle at 8 threads and on configs 2 and 3 (minutes)")
@@ -134,7 +136,8 @@ def setup_engine(args, device, rank):
     from aes_xor_fhe.fhe import Engine
     from aes_xor_fhe.parallel import rank_nonce_start
     eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes,
-                 device_id=device, seed=SEED, nonce_start=rank_nonce_start(rank))
+                 scale_bits=args.scale_bits, device_id=device, seed=SEED,
+                 nonce_start=rank_nonce_start(rank))
     sk = eng.create_secret_key(1)
     pk = eng.create_public_key(sk)
     rlk = eng.create_relinearization_key(sk)
@@ -309,7 +312,7 @@ def cpu_baseline(args):
 
     def round_time(nthr):
         eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes,
-                     thread_count=nthr, seed=SEED, _lib=lib)
+                     scale_bits=args.scale_bits, thread_count=nthr, seed=SEED, _lib=lib)
         sk = eng.create_secret_key(1)
         R = RoundDriver(args.layout, eng, sk, eng.create_public_key(sk), eng.create_relinearization_key(sk),
                         eng.create_conjugation_key(sk))
@@ -465,6 +468,7 @@ def main():
                              else "nibble-domain Zeta-16 LUTs, byte-major SIMD packing")),
                 "layout": args.layout,
                 "log_n": args.log_n, "max_level": args.max_level, "special_primes": args.special_primes,
+                "scale_bits": args.scale_bits,
                 "ciphertext_sets_per_gpu": args.batch, "blocks_per_gpu_per_step": args.batch * R.n_blk,
                 "parallelism": f"ciphertext-batch sharding x{world} (no data-path collective)",
                 "verified": ok, "pool_after_round": round_pool,

@@ -12,8 +12,9 @@ identity that restores the top level.  Every engine call is appended to a trace.
 
 The reference sources are read in place from /root/reference and never copied; this script
 only runs in the build container.  Output (committed):
-  golden.npz   decoded outputs + their inputs
-  traces.json  op-count traces of each service call
+  golden.npz   decoded outputs + their inputs (XOR, ARK, SubBytes, ShiftRows, MixRow, GF x2/x3
+               and the GF coefficient vectors the reference's generator makes)
+  traces.json  op-count traces of each service call (incl. GF mul2/mul3, AESFHETransformer)
 Run: python tests/golden/make_golden.py
 """
 from __future__ import annotations
@@ -214,6 +215,38 @@ def main():
     st4 = np.arange(16).reshape(4, 4) % 16
     out, traces["mixrow_merged_shift_mix"] = counts(lambda: mr.merged_shift_mix_fhe(st4))
     g["mixrow_abs_max"] = np.array([np.abs(ew.decrypt(out)).max()])
+
+    # GF(2^8) x2 / x3 (gf_service.py:55-78).  The coefficient files it loads are absent from the
+    # reference tree; they are produced by the reference's own generator
+    # (generator/generate_gf2_gf3_coeffs.py:47-70, main()) redirected into a temp dir, never
+    # into /root/reference.
+    import importlib
+    import tempfile
+    tmp = Path(tempfile.mkdtemp(prefix="aesfhe_gf_"))
+    gen = importlib.import_module("aes_xor_fhe.generator.generate_gf2_gf3_coeffs")
+    gen.__file__ = str(tmp / "generator" / "generate_gf2_gf3_coeffs.py")
+    gen.main()
+    import aes_xor_fhe.gf_service as gfs
+    gfs.__file__ = str(tmp / "gf_service.py")      # base = tmp / "generator/coeffs"
+    for k in ("gf2_hi", "gf2_lo", "gf3_hi", "gf3_lo"):
+        g[f"{k}_coeffs"] = gfs._load_coeffs(tmp / "generator" / "coeffs" / f"{k}_coeffs.json")
+    gf = gfs.GFService(ew, svc)
+    gplain = np.tile(np.arange(256, dtype=np.uint8), SLOTS // 256)
+    gct = ew.encrypt(zeta_encode(gplain, modulus=256))
+    g["gf_in"] = gplain
+    for name, fn in (("gf2", gf.mul2), ("gf3", gf.mul3)):
+        (hi, lo), traces[f"gf_{name[2]}_mul"] = counts(lambda: fn(gct))
+        g[f"{name}_hi_out"] = zeta_decode(ew.decrypt(hi), modulus=256)
+        g[f"{name}_lo_out"] = zeta_decode(ew.decrypt(lo), modulus=256)
+        g[f"{name}_level_drop"] = np.array([MAX_LEVEL - hi.level])
+
+    # AESFHETransformer.merged_shift_mix (mixcolumns_service.py:21-83): op trace; its decoded
+    # output diverges (8-bit zeta values through the 4-bit XOR LUT), so only finiteness is kept
+    import aes_xor_fhe.mixcolumns_service as mcs
+    tr = mcs.AESFHETransformer(ew, svc, gf)
+    out, traces["transformer_merged_shift_mix"] = counts(
+        lambda: tr.merged_shift_mix(np.arange(16, dtype=np.uint8)))
+    g["transformer_out_finite"] = np.array([bool(np.all(np.isfinite(ew.decrypt(out))))])
 
     np.savez_compressed(OUT / "golden.npz", **g)
     (OUT / "traces.json").write_text(json.dumps(traces, indent=1, sort_keys=True))

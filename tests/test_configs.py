@@ -54,7 +54,9 @@ def test_config1_ark_gpu_matches_oracle(product_lib, oracle_lib, gpu_available):
     assert np.array_equal(_config1(product_lib), _config1(oracle_lib))
 
 
-CONFIG5 = dict(log_n=17, max_level=35, special_primes=12)
+# 44-bit scale: the 128-bit budget of N = 2^17 (log QP <= 3544) leaves room (50 + 35 * 44 + 12 * 50 =
+# 2190), and at a 40-bit scale the slot error after a round was ~2x N = 2^16's (aes10_diag.py)
+CONFIG5 = dict(log_n=17, max_level=35, special_primes=12, scale_bits=44)
 
 
 @pytest.mark.gpu
