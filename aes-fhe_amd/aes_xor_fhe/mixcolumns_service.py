@@ -3,7 +3,8 @@ contiguous 16-slot blocks (reference: mixcolumns_service.py:11-88), same operati
 rotations -1/-6/-11, per output block GF x2/x3 (hi, lo) -> recombine -> xor_cipher chain,
 four bootstraps, final rotate-XOR.  As written in the reference it feeds 8-bit Zeta-256
 values to the 4-bit XOR LUT and diverges; it needs bootstrapping.  Kept for
-call-surface / op-trace parity; the correct round is aes_round.AESRoundEngine.
+call-surface / op-trace parity (recombination included: XORService.recombine_nibbles_ref); the
+correct round is aes_round.AESRoundEngine.
 """
 from __future__ import annotations
 
@@ -40,7 +41,7 @@ class AESFHETransformer:
                     terms.append(c)
                 else:
                     hi, lo = getattr(self.gf_svc, fn)(c)
-                    terms.append(self.xor_svc.recombine_nibbles(hi, lo))
+                    terms.append(self.xor_svc.recombine_nibbles_ref(hi, lo))
             acc = terms[0]
             for t in terms[1:]:
                 acc = self.xor_svc.xor_cipher(acc, t)

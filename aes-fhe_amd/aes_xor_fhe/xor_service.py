@@ -248,6 +248,13 @@ class XORService:
             lo_ct = self._lut_16_to_256(lo_ct)
         return eng.multiply(hi_ct, lo_ct, eng.relin_key)
 
+    def recombine_nibbles_ref(self, hi_ct, lo_ct):
+        """The reference's recombine_nibbles op for op (xor_service.py:256-269): hi^16 from a
+        degree-16 power basis, times lo.  hi = zeta_16^h makes hi^16 = 1, so the result is just
+        lo; kept only where the reference's op trace is the contract (AESFHETransformer)."""
+        eng = self.eng_wrap
+        return eng.multiply(eng.make_power_basis(hi_ct, 16)[15], lo_ct)
+
     def _lut_16_to_256(self, ct):
         if self._lut16_to_256 is None:
             self._lut16_to_256 = coeffs_gen.lut_1d(lambda x: x, 16, out_mod=256)

@@ -224,6 +224,7 @@ def main():
     import tempfile
     tmp = Path(tempfile.mkdtemp(prefix="aesfhe_gf_"))
     gen = importlib.import_module("aes_xor_fhe.generator.generate_gf2_gf3_coeffs")
+    (tmp / "generator").mkdir()
     gen.__file__ = str(tmp / "generator" / "generate_gf2_gf3_coeffs.py")
     gen.main()
     import aes_xor_fhe.gf_service as gfs

@@ -81,3 +81,64 @@ def test_aes_round_engine_batched(wrap):
     h, l = R.encrypt_blocks(blocks)
     oh, ol = R.round(h, l, R.encrypt_round_key(rk))
     assert np.array_equal(R.decrypt_blocks(oh, ol), T.aes_round(blocks, rk))
+
+
+# ---- GF x2 / x3, MixRow and AESFHETransformer on the HIP engine with the real Engine.bootstrap
+import json  # noqa: E402
+
+TRACES = json.loads((Path(__file__).resolve().parent / "golden" / "traces.json").read_text())
+
+
+@pytest.fixture(scope="module")
+def twrap(product_lib, gpu_available):
+    """BASELINE parameters (N = 2^16, L = 30) with the tracing engine: engine calls are counted
+    in the golden trace's categories, Engine.bootstrap as one entry (tests/_tracing.py)."""
+    from _tracing import make_wrap
+    return make_wrap(product_lib, log_n=16, L=30, K=8, tracing=True)
+
+
+def test_gf_mul2_mul3_match_reference_32768(twrap):   # gf_service.py:55-78
+    from aes_xor_fhe.gf_service import GFService
+    from aes_xor_fhe.utils import zeta_decode, zeta_encode
+    w = twrap
+    gf = GFService(w, XORService(w))
+    ct = w.engine.encrypt(zeta_encode(GOLD["gf_in"], modulus=256), w.public_key)
+    for t, fn in ((2, gf.mul2), (3, gf.mul3)):
+        w.engine.trace.clear()
+        hi, lo = fn(ct)
+        assert dict(w.engine.trace) == TRACES[f"gf_{t}_mul"]
+        assert np.array_equal(zeta_decode(w.decrypt(hi), modulus=256), GOLD[f"gf{t}_hi_out"])
+        assert np.array_equal(zeta_decode(w.decrypt(lo), modulus=256), GOLD[f"gf{t}_lo_out"])
+        assert 30 - hi.level == int(GOLD[f"gf{t}_level_drop"][0])
+
+
+def test_mixrow_with_bootstrap(twrap):                 # shift_mix_zeta.py:14-69
+    """23 xor_cipher calls; operands below level 8 are refreshed by the real Engine.bootstrap
+    (general mode) exactly where the reference's xor_cipher calls it (xor_service.py:274-277).
+    In exact arithmetic every output slot is 0 (golden mixrow_abs_max); here the slots stay
+    within the general-mode bootstrap's error of it."""
+    from aes_xor_fhe.shift_mix_zeta import MixRow
+    w = twrap
+    svc = XORService(w)
+    svc.coeff_cache.get_plaintext_coeffs(w)
+    w.engine.trace.clear()
+    out = MixRow(svc, w).merged_shift_mix_fhe(np.arange(16).reshape(4, 4) % 16)
+    assert {k: v for k, v in w.engine.trace.items() if v} == TRACES["mixrow_merged_shift_mix"]
+    err = np.abs(w.decrypt(out)).max()
+    print("MixRow max |slot| (exact: 0):", err)
+    assert err < 0.05 and float(GOLD["mixrow_abs_max"][0]) == 0.0
+
+
+def test_transformer_with_bootstrap(twrap):           # mixcolumns_service.py:21-83
+    """Runs end to end on the GPU with the real Engine.bootstrap and the reference's op trace
+    (its values diverge in exact arithmetic: 8-bit zeta values through the 4-bit XOR LUT)."""
+    from aes_xor_fhe.gf_service import GFService
+    from aes_xor_fhe.mixcolumns_service import AESFHETransformer
+    w = twrap
+    svc = XORService(w)
+    svc.coeff_cache.get_plaintext_coeffs(w)
+    gf = GFService(w, svc)
+    w.engine.trace.clear()
+    out = AESFHETransformer(w, svc, gf).merged_shift_mix(np.arange(16, dtype=np.uint8))
+    assert {k: v for k, v in w.engine.trace.items() if v} == TRACES["transformer_merged_shift_mix"]
+    assert out.npoly == 2 and 0 <= out.level <= 30

@@ -20,67 +20,7 @@ GOLD = np.load(Path(__file__).resolve().parent / "golden" / "golden.npz")
 TRACES = json.loads((Path(__file__).resolve().parent / "golden" / "traces.json").read_text())
 
 
-class Tracing(Engine):
-    """Counts engine calls with the categories of the golden stand-in trace."""
-
-    def __init__(self, *a, **kw):
-        super().__init__(*a, **kw)
-        self.trace = Counter()
-
-    def encode(self, vec, *a, **k):
-        self.trace["encode"] += 1
-        return super().encode(vec, *a, **k)
-
-    def encrypt(self, data, key, level=None):
-        self.trace["encrypt"] += 1
-        return super().encrypt(data, key, level)
-
-    def decrypt(self, ct, sk):
-        self.trace["decrypt"] += 1
-        return super().decrypt(ct, sk)
-
-    def add(self, a, b):
-        both = isinstance(a, Ciphertext) and isinstance(b, Ciphertext)
-        self.trace["add_ct_ct" if both else "add_ct_pt"] += 1
-        return super().add(a, b)
-
-    def multiply(self, a, b, relinearization_key=None):
-        if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
-            self.trace["mul_ct_ct"] += 1
-        elif isinstance(a, Plaintext) or isinstance(b, Plaintext):
-            self.trace["mul_ct_pt"] += 1
-        else:
-            self.trace["mul_ct_scalar"] += 1
-        return super().multiply(a, b, relinearization_key)
-
-    def make_power_basis(self, ct, degree, rlk):
-        self.trace[f"power_basis_{degree}"] += 1
-        return super().make_power_basis(ct, degree, rlk)
-
-    def conjugate(self, ct, key):
-        self.trace["conjugate"] += 1
-        return super().conjugate(ct, key)
-
-    def rotate(self, ct, key, delta=None):
-        self.trace["rotate"] += 1
-        return super().rotate(ct, key, delta)
-
-    def relinearize(self, ct, rlk):
-        self.trace["relinearize"] += 1
-        return super().relinearize(ct, rlk)
-
-
-def make_wrap(lib, log_n=10, L=12, K=4, tracing=False):
-    cls = Tracing if tracing else Engine
-    # EngineContext builds the engine itself; inject the class through a tiny subclass
-    import aes_xor_fhe.engine_context as ec
-    orig = ec.Engine
-    ec.Engine = cls
-    try:
-        ctx = EngineContext(signature=1, log_n=log_n, max_level=L, special_primes=K, seed=9, _lib=lib)
-    finally:
-        ec.Engine = orig
-    return EngineWrapper(XORConfig(), ctx=ctx)
+from _tracing import Tracing, make_wrap  # noqa: E402  (shared with test_gpu_services.py)
 
 
 @pytest.fixture(scope="module")
@@ -259,3 +199,61 @@ def test_mixrow_trace_matches_reference(oracle_lib):
     mr.merged_shift_mix_fhe(np.arange(16).reshape(4, 4) % 16)
     got = {k: v for k, v in e.trace.items() if v}
     assert got == TRACES["mixrow_merged_shift_mix"]
+
+
+def test_gf_coefficients_match_reference_generator():
+    """coeffs_gen's GF x2 / x3 LUT coefficients against the vectors the reference's own
+    generator writes (generator/generate_gf2_gf3_coeffs.py:47-70, run by make_golden.py)."""
+    from aes_xor_fhe.coeffs_gen import load_1d
+    from aes_xor_fhe.gf_service import COEFF_DIR
+    for k in ("gf2_hi", "gf2_lo", "gf3_hi", "gf3_lo"):
+        np.testing.assert_allclose(load_1d(COEFF_DIR / f"{k}_coeffs.json"), GOLD[f"{k}_coeffs"],
+                                   rtol=0, atol=1e-13)
+
+
+def test_gf_mul2_mul3_match_reference(oracle_lib):
+    """GFService.mul2 / mul3 (gf_service.py:55-78): decoded (hi, lo) outputs, level drop and op
+    trace equal the reference's (golden run over the stand-in engine)."""
+    from aes_xor_fhe.gf_service import GFService
+    from aes_xor_fhe.utils import zeta_decode, zeta_encode
+    w = make_wrap(oracle_lib, L=12, tracing=True)
+    gf = GFService(w, XORService(w))
+    n = w.engine.slot_count
+    x = GOLD["gf_in"][:n]
+    ct = w.engine.encrypt(zeta_encode(x, modulus=256), w.public_key)
+    for t, fn in ((2, gf.mul2), (3, gf.mul3)):
+        w.engine.trace.clear()
+        hi, lo = fn(ct)
+        assert dict(w.engine.trace) == TRACES[f"gf_{t}_mul"]
+        assert np.array_equal(zeta_decode(w.decrypt(hi), modulus=256), GOLD[f"gf{t}_hi_out"][:n])
+        assert np.array_equal(zeta_decode(w.decrypt(lo), modulus=256), GOLD[f"gf{t}_lo_out"][:n])
+        assert ct.level - hi.level == int(GOLD[f"gf{t}_level_drop"][0])
+
+
+@pytest.mark.slow
+def test_transformer_trace_matches_reference(oracle_lib):
+    """AESFHETransformer.merged_shift_mix (mixcolumns_service.py:21-83): the same op sequence as
+    the reference (its values diverge in exact arithmetic -- 8-bit zeta values through the 4-bit
+    XOR LUT -- so only the trace is comparable); a client-aided refresh stands in for the four
+    bootstraps here, tests/test_gpu_services.py runs it with the real Engine.bootstrap."""
+    from aes_xor_fhe.gf_service import GFService
+    from aes_xor_fhe.mixcolumns_service import AESFHETransformer
+    w = make_wrap(oracle_lib, L=30, K=8, tracing=True)
+    e = w.engine
+
+    def refresh(ct):
+        e.trace["bootstrap"] += 1
+        v = np.nan_to_num(e.decrypt(ct, w.secret_key))
+        v = np.clip(v.real, -4, 4) + 1j * np.clip(v.imag, -4, 4)
+        e.trace["decrypt"] -= 1
+        e.trace["encrypt"] -= 1
+        return e.encrypt(v, w.public_key)
+    w.bootstrap = refresh
+    svc = XORService(w)
+    svc.coeff_cache.get_plaintext_coeffs(w)   # warm, as in the golden run
+    gf = GFService(w, svc)
+    tr = AESFHETransformer(w, svc, gf)
+    e.trace.clear()
+    tr.merged_shift_mix(np.arange(16, dtype=np.uint8))
+    got = {k: v for k, v in e.trace.items() if v}
+    assert got == TRACES["transformer_merged_shift_mix"]

@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python tools/aes10_diag.py 17 35 12 44 > gpurun_out/aes10diag17.log 2>&1; rc=$?
-timeout -k 10 400 python tools/aes10_diag.py 17 35 12 40 > gpurun_out/aes10diag17s40.log 2>&1
-cat gpurun_out/aes10diag17.log gpurun_out/aes10diag17s40.log | tail -40
-exit $rc
+for a in "16 30 8 40 50" "16 30 8 44 50" "16 30 8 40 45" "16 30 8 40 47"; do
+  timeout -k 10 300 python tools/boot_general_diag.py $a >> gpurun_out/bootgen.log 2>&1 || exit 1
+done
+grep -v amdgpu gpurun_out/bootgen.log
