@@ -59,6 +59,14 @@ PMC_NOTE = ("HBM bytes per NTT launch = algorithmic bytes x the HBM/algorithmic 
             "at the same parameters (profiles/r01/pmc/ntt_traffic.json)")
 
 
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    """Progress on stderr (the JSON result is the only stdout line)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def traffic_per_launch(alg_bytes):
     """HBM bytes per NTT launch from the committed PMC measurement (None if absent)."""
     try:
@@ -166,11 +174,13 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     ppc = args.aes10_ppc or max(1, 32 // nb)  # ~32 ciphertexts per Bootstrapper call
     # warm-up of the same shape: materialises the bootstrap plaintexts and fills the device pool
     # with every buffer size of the run, so the timed run makes no hipMalloc
+    log("aes10: bootstrapper ready; warm-up run")
     warm = R.encrypt_aes128(R.encrypt_blocks(rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)),
                             keys, bs, pairs_per_call=ppc)
     del warm
     blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
     st = R.encrypt_blocks(blocks)
+    log("aes10: timed run")
     tm = {}
     barrier()
     m0 = eng.pool_stats()["mallocs"]
@@ -326,6 +336,7 @@ def cpu_baseline(args):
         ok = bool((R.decrypt(out) == T.aes_round(blocks, rk)).all())
         return R.n_blk, t, ok
 
+    log(f"cpu baseline: oracle round at {threads} threads")
     n_blk, t, ok = round_time(threads)
     rec = {"value": round(n_blk / t, 2), "unit": "blocks/s", "cores": threads, "kind": "port",
            "measured": True, "verified": ok, "os_cpu_count": os.cpu_count(), "cpu_model": _cpu_model(),
@@ -358,7 +369,9 @@ def main():
         dist.init_process_group(backend, rank=rank, world_size=world)
     from aes_xor_fhe import aes_tables as T
 
+    log(f"rank {rank}/{world}: engine N=2^{args.log_n} L={args.max_level} K={args.special_primes}")
     eng, R = setup_engine(args, device, rank)
+    log("keys ready")
     if torch.cuda.is_available():
         torch.cuda.set_device(device)
     red_dev = torch.device("cuda", device) if dist is not None and dist.get_backend() == "nccl" else torch.device("cpu")
@@ -383,13 +396,15 @@ def main():
     st = R.encrypt(blocks)
     key = R.key(rk)
     eng.synchronize()
+    log(f"{args.batch} sets encrypted")
 
     def step():
         return R.round(st, key)
 
     for _ in range(args.warmup):
         out = step()
-    eng.synchronize()
+        eng.synchronize()
+        log("warm-up step")
 
     import ctypes as C
     barrier()
@@ -398,6 +413,7 @@ def main():
         out = step()
     barrier()
     elapsed = allmax(time.perf_counter() - t0)
+    log(f"timed: {args.steps} steps, {elapsed / args.steps * 1e3:.1f} ms/step")
     round_pool = eng.pool_stats()
     ok = None
     if args.check:
@@ -428,17 +444,20 @@ def main():
     gc.collect()
     eng.pool_trim()
 
+    log(f"checked ({ok}), profiled")
     sg = None
     if dist is not None:
         sg = scatter_gather_leg(args, eng, R, rank, world, barrier, allmax)
         gc.collect()
         eng.pool_trim()
     configs = None
+    log("scatter/gather done" if sg else "no scatter/gather leg")
     if world == 1 and not args.no_configs and args.log_n == 16:
         configs = config_legs(args, eng, R)
         gc.collect()
         eng.pool_trim()
     aes10 = None
+    log("config legs done" if configs else "no config legs")
     if args.aes10_batch > 0 and args.layout == "rows":
         aes10 = aes128_full(args, eng, R, rank, barrier, allmax)
 
