@@ -1,0 +1,30 @@
+"""AddressSanitizer + UBSan runs of the host-side C/C++ (GPU sanitizers are not available on
+this pool; host code only):
+  * the CPU oracle (oracle/ckks_oracle.c) driven over the whole ABI by oracle/asan_check.c,
+    engine destroyed before its objects (make -C oracle asan);
+  * the HIP engine's host pieces (aes-fhe_amd/csrc/ckks_host.h: prime chain, roots, PRNG, codec)
+    at every ring size, tests/native/host_asan.cpp.
+A sanitizer report makes the program exit non-zero."""
+import os
+import subprocess
+
+from conftest import ROOT
+
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", OMP_NUM_THREADS="2",
+           UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+
+
+def test_oracle_asan():
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "asan"], check=True)
+    r = subprocess.run([str(ROOT / "oracle" / "_build" / "asan_check")], env=ENV,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "asan_check ok" in r.stdout, r.stderr[-4000:]
+
+
+def test_host_codec_asan(tmp_path):
+    exe = tmp_path / "host_asan"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-ffp-contract=off",
+                    "-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-o", str(exe),
+                    str(ROOT / "tests" / "native" / "host_asan.cpp")], check=True)
+    r = subprocess.run([str(exe)], env=ENV, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "host_asan ok" in r.stdout, r.stderr[-4000:]

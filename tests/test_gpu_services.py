@@ -97,6 +97,15 @@ def twrap(product_lib, gpu_available):
     return make_wrap(product_lib, log_n=16, L=30, K=8, tracing=True)
 
 
+def _same_trace(got, ref):
+    """The reference's op trace, except the number of bootstraps: the golden stand-in's
+    bootstrap returns the top level, the real one (bootstrap.py, general mode) level L - 16, so
+    the reference's `level < 8` checks (xor_service.py:274-277) refresh at least as often."""
+    got = {k: v for k, v in got.items() if v}
+    assert got.pop("bootstrap", 0) >= ref.get("bootstrap", 0)
+    assert got == {k: v for k, v in ref.items() if k != "bootstrap"}
+
+
 def test_gf_mul2_mul3_match_reference_32768(twrap):   # gf_service.py:55-78
     from aes_xor_fhe.gf_service import GFService
     from aes_xor_fhe.utils import zeta_decode, zeta_encode
@@ -123,7 +132,7 @@ def test_mixrow_with_bootstrap(twrap):                 # shift_mix_zeta.py:14-69
     svc.coeff_cache.get_plaintext_coeffs(w)
     w.engine.trace.clear()
     out = MixRow(svc, w).merged_shift_mix_fhe(np.arange(16).reshape(4, 4) % 16)
-    assert {k: v for k, v in w.engine.trace.items() if v} == TRACES["mixrow_merged_shift_mix"]
+    _same_trace(w.engine.trace, TRACES["mixrow_merged_shift_mix"])
     err = np.abs(w.decrypt(out)).max()
     print("MixRow max |slot| (exact: 0):", err)
     assert err < 0.05 and float(GOLD["mixrow_abs_max"][0]) == 0.0
@@ -140,5 +149,5 @@ def test_transformer_with_bootstrap(twrap):           # mixcolumns_service.py:21
     gf = GFService(w, svc)
     w.engine.trace.clear()
     out = AESFHETransformer(w, svc, gf).merged_shift_mix(np.arange(16, dtype=np.uint8))
-    assert {k: v for k, v in w.engine.trace.items() if v} == TRACES["transformer_merged_shift_mix"]
+    _same_trace(w.engine.trace, TRACES["transformer_merged_shift_mix"])
     assert out.npoly == 2 and 0 <= out.level <= 30
