@@ -194,11 +194,12 @@ class AESRowRound:
     # allows it by levels) reached 0.12 at N = 2^17 and the run diverged.
     MAX_ROUNDS_PER_REFRESH = 3
 
-    def encrypt_aes128(self, bits, keys, bs, timings: dict | None = None, pairs_per_call: int = 8):
+    def encrypt_aes128(self, bits, keys, bs, timings: dict | None = None, pairs_per_call: int = 8,
+                       progress=None):
         """AES-128 encryption of the bit state under the 11 encrypted round keys `keys`
         (FIPS-197 section 5.1), bootstrapping with `bs` (a bootstrap.Bootstrapper) as the level
         budget requires, and at least every MAX_ROUNDS_PER_REFRESH rounds.  Returns the state
-        and the number of refreshes."""
+        and the number of refreshes.  progress: optional callable(str) told after each step."""
         import time
         stc = len(bs.stc_bits)
         S = self.add_round_key(bits, keys[0])
@@ -213,6 +214,8 @@ class AESRowRound:
                 t0 = time.perf_counter()
                 S = self.refresh(S, bs, pairs_per_call)
                 refreshes += 1
+                if progress:
+                    progress(f"refresh {refreshes} before round {rnd}")
                 if timings is not None:
                     self.e.synchronize()
                     timings["bootstrap"] = timings.get("bootstrap", 0.0) + time.perf_counter() - t0
@@ -220,6 +223,8 @@ class AESRowRound:
             lvl = min(c.level for row in S for c in row)
             S = self.final_round(S, keys[rnd]) if final else self.round(S, keys[rnd])
             since += 1
+            if progress:
+                progress(f"round {rnd} from level {lvl}")
             if timings is not None:
                 self.e.synchronize()
                 dt = time.perf_counter() - t0

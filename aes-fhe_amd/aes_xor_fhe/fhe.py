@@ -31,7 +31,12 @@ SECURITY_BUDGET = {11: 54, 12: 109, 13: 218, 14: 438, 15: 881, 16: 1772, 17: 354
 # seed None: a fresh 64-bit engine seed from the OS entropy pool (os.urandom) per engine, so
 # that no two default engines derive the same keys; an explicit seed reproduces every key and
 # encryption (tests, and multi-rank key sharing -- see `nonce_start`).
-DEFAULT_PARAMS = dict(log_n=16, max_level=30, special_primes=8, scale_bits=40, base_bits=50,
+# scale 44 with K = 8: log QP = 50 + 30 * 44 + 8 * 50 = 1770 <= 1772 (128-bit at N = 2^16).  The
+# general-mode Engine.bootstrap the reference's services call (xor_service.py:120-129) needs it:
+# measured at N = 2^16, L = 30 (tools/boot_general_diag.py): max slot error 4.7e-3 at scale 44,
+# 1.16 (unusable) at scale 40, below the zeta-256 decision margin sin(pi/256) = 0.012 only at 44.
+# The bench's bit-mode path keeps its own explicit 40-bit scale and K = 10.
+DEFAULT_PARAMS = dict(log_n=16, max_level=30, special_primes=8, scale_bits=44, base_bits=50,
                       special_bits=50, seed=None)
 
 

@@ -1296,20 +1296,46 @@ extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int
     API_END
 }
 
+// Decrypt: m = c0 + c1 s (+ c2 s^2) on limb 0, and on limb 1 too when the
+// ciphertext has it; the two residues are CRT-combined and centred mod q0 q1 (a level-0
+// ciphertext: mod q0), so the plaintext capacity is q0 q1 / (2 Delta) instead of q0 / (2 Delta)
+// (= 32 at a 44-bit scale).  Coefficients beyond +-(2^63 - 1) saturate.
 extern "C" int aesfhe_decrypt(aesfhe_engine* e, const aesfhe_key* sk, const aesfhe_ct* c, int64_t* out) {
     API_BEGIN
     if (!sk || sk->kind != 0) throw_err(AESFHE_EARG, "decryption needs the secret key");
     const int N = e->N;
-    Tmp t(e, (size_t)c->B * N);
+    const int nl = c->level >= 1 ? 2 : 1;
+    Tmp t(e, (size_t)nl * c->B * N);
     View v = view_of(c);
-    hipLaunchKernelGGL(k_dec_limb0, dim3(N / 256, 1, c->B), dim3(256), 0, e->stream, v.d, v.bs, v.ps, c->np, (const u64*)sk->d, t.p, e->chain.q[0], 1.0 / (double)e->chain.q[0], e->logN);
-    Span s = span_s(t.p, N, 1, 1, 0, e->Lp1);
-    ntt(e, s, s, c->B, true);
-    std::vector<u64> h((size_t)c->B * N);
+    for (int i = 0; i < nl; i++) {
+        u64* ti = t.p + (size_t)i * c->B * N;
+        hipLaunchKernelGGL(k_dec_limb0, dim3(N / 256, 1, c->B), dim3(256), 0, e->stream, v.d + (size_t)i * N, v.bs, v.ps, c->np,
+                           (const u64*)sk->d + (size_t)i * N, ti, e->chain.q[i], 1.0 / (double)e->chain.q[i], e->logN);
+        Span s = span_s(ti, N, 1, 1, i, e->Lp1);
+        ntt(e, s, s, c->B, true);
+    }
+    std::vector<u64> h((size_t)nl * c->B * N);
     HIPC(hipMemcpyAsync(h.data(), t.p, h.size() * 8, hipMemcpyDeviceToHost, e->stream));
     HIPC(hipStreamSynchronize(e->stream));
-    const u64 q = e->chain.q[0];
-    for (size_t i = 0; i < h.size(); i++) out[i] = h[i] > q / 2 ? (int64_t)h[i] - (int64_t)q : (int64_t)h[i];
+    const u64 q0 = e->chain.q[0];
+    const size_t cnt = (size_t)c->B * N;
+    if (nl == 1) {
+        for (size_t i = 0; i < cnt; i++) out[i] = h[i] > q0 / 2 ? (int64_t)h[i] - (int64_t)q0 : (int64_t)h[i];
+    } else {
+        const u64 q1 = e->chain.q[1], q0inv = h_invmod(q0 % q1, q1);
+        const u128 Q = (u128)q0 * q1;
+        for (size_t i = 0; i < cnt; i++) {
+            const u64 r0 = h[i], r1 = h[cnt + i];
+            const u64 d = h_mulmod(h_submod(r1, r0 % q1, q1), q0inv, q1);
+            const u128 x = (u128)r0 + (u128)q0 * d;  // in [0, q0 q1)
+            if (x > Q / 2) {
+                const u128 m = Q - x;
+                out[i] = m > (u128)INT64_MAX ? -INT64_MAX : -(int64_t)m;
+            } else {
+                out[i] = x > (u128)INT64_MAX ? INT64_MAX : (int64_t)x;
+            }
+        }
+    }
     API_END
 }
 

@@ -175,8 +175,12 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     # warm-up of the same shape: materialises the bootstrap plaintexts and fills the device pool
     # with every buffer size of the run, so the timed run makes no hipMalloc
     log("aes10: bootstrapper ready; warm-up run")
+    def prog(msg):
+        ps = eng.pool_stats()
+        log(f"aes10: {msg} (pool held {ps['held'] / 1e9:.1f} GB live {ps['live'] / 1e9:.1f} GB "
+            f"mallocs {ps['mallocs']} trims {ps['trims']})")
     warm = R.encrypt_aes128(R.encrypt_blocks(rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)),
-                            keys, bs, pairs_per_call=ppc)
+                            keys, bs, pairs_per_call=ppc, progress=prog)
     del warm
     blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
     st = R.encrypt_blocks(blocks)
@@ -185,7 +189,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     barrier()
     m0 = eng.pool_stats()["mallocs"]
     t0 = time.perf_counter()
-    out, nref = R.encrypt_aes128(st, keys, bs, timings=tm, pairs_per_call=ppc)
+    out, nref = R.encrypt_aes128(st, keys, bs, timings=tm, pairs_per_call=ppc, progress=log)
     barrier()
     el = allmax(time.perf_counter() - t0)
     timed_mallocs = eng.pool_stats()["mallocs"] - m0

@@ -168,7 +168,8 @@ int aesfhe_key_import(aesfhe_engine *eng, int32_t kind, uint64_t galois_elt, uin
  * key: public key (or secret key: symmetric encryption).  nonce selects the randomness. */
 int aesfhe_encrypt(aesfhe_engine *eng, const aesfhe_key *key, const int64_t *coeffs,
                    int32_t batch, int32_t level, uint64_t nonce, aesfhe_ct **out);
-/* Decrypt to batch*N centered coefficients modulo q_0. */
+/* Decrypt to batch*N centred coefficients: limbs 0 and 1 CRT-combined modulo q_0 q_1 (a level-0
+ * ciphertext: modulo q_0), saturated to +-(2^63 - 1). */
 int aesfhe_decrypt(aesfhe_engine *eng, const aesfhe_key *sk, const aesfhe_ct *ct,
                    int64_t *coeffs_out);
 /* info[0]=batch info[1]=npoly info[2]=level info[3]=is_zero */

@@ -410,7 +410,9 @@ int aesfhe_engine_create(const aesfhe_params *pp, aesfhe_engine **out) {
     e->seed = pp->seed;
     e->threads = pp->threads;
 #ifdef _OPENMP
-    if (e->threads > 0) omp_set_num_threads(e->threads);
+    /* per-engine thread count (num_threads on every parallel loop): never the process-wide
+     * omp_set_num_threads, which would leak one engine's setting into every other engine */
+    if (e->threads <= 0) e->threads = omp_get_max_threads();
 #endif
     if (pp->primes) {
         for (int i = 0; i < e->np; i++) e->q[i] = pp->primes[i];
@@ -723,7 +725,7 @@ int aesfhe_key_secret(aesfhe_engine *e, uint64_t seed, aesfhe_key **out) {
     i64 *s = malloc(sizeof(i64) * e->N);
     u64 key = derive(k->keyseed, 1);
     for (int i = 0; i < e->N; i++) s[i] = ternary(rnd(key, (u64)i));
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int p = 0; p < e->np; p++) coeffs_to_ntt(e, s, k->data + (size_t)p * e->N, p);
     free(s);
     *out = k;
@@ -740,7 +742,7 @@ int aesfhe_key_public(aesfhe_engine *e, const aesfhe_key *sk, aesfhe_key **out) 
     u64 ka = derive(sk->keyseed, 2), ke = derive(sk->keyseed, 3);
     i64 *ee = malloc(sizeof(i64) * N);
     for (int i = 0; i < N; i++) ee[i] = cbd21(rnd(ke, (u64)i));
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int p = 0; p < nq; p++) {
         u64 *b = k->data + (size_t)p * N, *a = k->data + ((size_t)nq + p) * N;
         const u64 *s = sk->data + (size_t)p * N;
@@ -794,7 +796,7 @@ static aesfhe_key *make_ksk_t(aesfhe_engine *e, const u64 *starget, u64 keyseed,
         i64 *ee = malloc(sizeof(i64) * N);
         for (int i = 0; i < N; i++) ee[i] = cbd21(rnd(ke, (u64)i));
         int lo = d * e->K, hi = lo + e->K; /* digit primes [lo, hi) intersect [0, nq) */
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
         for (int p = 0; p < np; p++) {
             u64 *b = k->data + (((size_t)d * 2 + 0) * np + p) * N;
             u64 *a = k->data + (((size_t)d * 2 + 1) * np + p) * N;
@@ -850,7 +852,7 @@ int aesfhe_key_secret_sparse(aesfhe_engine *e, uint64_t seed, int32_t hw, aesfhe
         idx[j] = t;
         s[idx[i]] = (rnd(key, (u64)N + i) & 1) ? -1 : 1;
     }
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int p = 0; p < e->np; p++) coeffs_to_ntt(e, s, k->data + (size_t)p * N, p);
     free(s);
     free(idx);
@@ -913,7 +915,7 @@ int aesfhe_encrypt(aesfhe_engine *e, const aesfhe_key *key, const int64_t *co, i
             e1[i] = cbd21(rnd(k2, (u64)i));
         }
         const i64 *m = co + (size_t)b * N;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
         for (int p = 0; p <= level; p++) {
             const u64 q = e->q[p];
             u64 *c0 = limb(e, c, b, 0, p), *c1 = limb(e, c, b, 1, p);
@@ -950,30 +952,57 @@ int aesfhe_encrypt(aesfhe_engine *e, const aesfhe_key *key, const int64_t *co, i
     return 0;
 }
 
+/* limb 0, and limb 1 when present, CRT-combined and centred mod q0 q1 (level 0:
+ * mod q0); coefficients beyond +-(2^63 - 1) saturate. */
+static void dec_limb(aesfhe_engine *e, const aesfhe_key *sk, const aesfhe_ct *c, int b, int p, u64 *t) {
+    const int N = e->N;
+    const u64 q = e->q[p];
+    const u64 *s = sk->data + (size_t)p * N;
+    const u64 *c0 = limb(e, c, b, 0, p);
+    for (int j = 0; j < N; j++) t[j] = c0[j];
+    if (c->npoly >= 2) {
+        const u64 *c1 = limb(e, c, b, 1, p);
+        for (int j = 0; j < N; j++) t[j] = add_mod(t[j], mul_mod(c1[j], s[j], &e->mont[p]), q);
+    }
+    if (c->npoly == 3) {
+        const u64 *c2 = limb(e, c, b, 2, p);
+        for (int j = 0; j < N; j++) {
+            u64 s2 = mul_mod(s[j], s[j], &e->mont[p]);
+            t[j] = add_mod(t[j], mul_mod(c2[j], s2, &e->mont[p]), q);
+        }
+    }
+    ntt_inv(e, t, p);
+}
+
 int aesfhe_decrypt(aesfhe_engine *e, const aesfhe_key *sk, const aesfhe_ct *c, int64_t *out) {
     if (!sk || sk->kind != 0) return fail(AESFHE_EARG, "decryption needs the secret key");
     const int N = e->N;
-    const u64 q = e->q[0];
-    u64 *t = malloc(sizeof(u64) * N);
-    const u64 *s = sk->data;
+    const u64 q0 = e->q[0];
+    u64 *t0 = malloc(sizeof(u64) * N), *t1 = malloc(sizeof(u64) * N);
     for (int b = 0; b < c->B; b++) {
-        const u64 *c0 = limb(e, c, b, 0, 0);
-        for (int j = 0; j < N; j++) t[j] = c0[j];
-        if (c->npoly >= 2) {
-            const u64 *c1 = limb(e, c, b, 1, 0);
-            for (int j = 0; j < N; j++) t[j] = add_mod(t[j], mul_mod(c1[j], s[j], &e->mont[0]), q);
+        dec_limb(e, sk, c, b, 0, t0);
+        int64_t *o = out + (size_t)b * N;
+        if (c->level < 1) {
+            for (int j = 0; j < N; j++) o[j] = t0[j] > q0 / 2 ? (i64)t0[j] - (i64)q0 : (i64)t0[j];
+            continue;
         }
-        if (c->npoly == 3) {
-            const u64 *c2 = limb(e, c, b, 2, 0);
-            for (int j = 0; j < N; j++) {
-                u64 s2 = mul_mod(s[j], s[j], &e->mont[0]);
-                t[j] = add_mod(t[j], mul_mod(c2[j], s2, &e->mont[0]), q);
+        dec_limb(e, sk, c, b, 1, t1);
+        const u64 q1 = e->q[1], q0inv = pow_mod(q0 % q1, q1 - 2, q1);
+        const u128 Q = (u128)q0 * q1;
+        for (int j = 0; j < N; j++) {
+            u64 r1 = t1[j], r0m = t0[j] % q1;
+            u64 d = (u64)((u128)(r1 >= r0m ? r1 - r0m : r1 + q1 - r0m) * q0inv % q1);
+            u128 x = (u128)t0[j] + (u128)q0 * d;
+            if (x > Q / 2) {
+                u128 m = Q - x;
+                o[j] = m > (u128)INT64_MAX ? -INT64_MAX : -(i64)m;
+            } else {
+                o[j] = x > (u128)INT64_MAX ? INT64_MAX : (i64)x;
             }
         }
-        ntt_inv(e, t, 0);
-        for (int j = 0; j < N; j++) out[(size_t)b * N + j] = t[j] > q / 2 ? (i64)t[j] - (i64)q : (i64)t[j];
     }
-    free(t);
+    free(t0);
+    free(t1);
     return 0;
 }
 
@@ -1084,7 +1113,7 @@ int aesfhe_pt_create(aesfhe_engine *e, const int64_t *co, int32_t level, aesfhe_
     aesfhe_pt *p = calloc(1, sizeof *p);
     p->level = level;
     p->data = malloc(sizeof(u64) * (size_t)(level + 1) * e->N);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int i = 0; i <= level; i++) coeffs_to_ntt(e, co, p->data + (size_t)i * e->N, i);
     *out = p;
     return 0;
@@ -1097,7 +1126,7 @@ int aesfhe_pt_create_ext(aesfhe_engine *e, const int64_t *co, int32_t level, aes
     p->level = level;
     p->ext = 1;
     p->data = malloc(sizeof(u64) * (size_t)ne * e->N);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int t = 0; t < ne; t++) coeffs_to_ntt(e, co, p->data + (size_t)t * e->N, t < nl ? t : e->L + 1 + (t - nl));
     *out = p;
     return 0;
@@ -1120,7 +1149,7 @@ static aesfhe_ct *rescale_raw(aesfhe_engine *e, const aesfhe_ct *c) {
             u64 *x = malloc(sizeof(u64) * N);
             memcpy(x, limb(e, c, b, pp, l), sizeof(u64) * N);
             ntt_inv(e, x, l);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
             for (int i = 0; i < l; i++) {
                 const u64 q = e->q[i];
                 u64 *t = malloc(sizeof(u64) * N);
@@ -1374,7 +1403,7 @@ static u64 *ks_acc(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k) {
     for (int t = 0; t < ne; t++) pid[t] = t <= l ? t : nq + (t - l - 1);
     u64 *dc = malloc(sizeof(u64) * (size_t)(l + 1) * N);
     memcpy(dc, d, sizeof(u64) * (size_t)(l + 1) * N);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int i = 0; i <= l; i++) ntt_inv(e, dc + (size_t)i * N, i);
     u64 *acc = calloc((size_t)2 * ne * N, sizeof(u64));
     int beta = (l + 1 + K - 1) / K;
@@ -1395,7 +1424,7 @@ static u64 *ks_acc(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k) {
         }
         const u64 *kb = k->data + ((size_t)j * 2 + 0) * e->np * N;
         const u64 *ka = k->data + ((size_t)j * 2 + 1) * e->np * N;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
         for (int t = 0; t < ne; t++) {
             const u64 qt = e->q[pid[t]];
             u64 *ext = malloc(sizeof(u64) * N);
@@ -1464,7 +1493,7 @@ static void moddown_r(aesfhe_engine *e, const u64 *acc, int l, int r, u64 *out0,
         const u64 *a = acc + (size_t)c * ne * N;
         u64 *outc = c == 0 ? out0 : out1;
         u64 *y = malloc(sizeof(u64) * (size_t)nE * N);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
         for (int j = 0; j < nE; j++) {
             const int p = Ep[j];
             u64 *z = y + (size_t)j * N;
@@ -1472,7 +1501,7 @@ static void moddown_r(aesfhe_engine *e, const u64 *acc, int l, int r, u64 *out0,
             ntt_inv(e, z, p);
             for (int x = 0; x < N; x++) z[x] = mul_mod_slow(z[x], inv[j], e->q[p]);
         }
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
         for (int i = 0; i <= lk; i++) {
             const u64 qi = e->q[i];
             u64 *conv = malloc(sizeof(u64) * N);
@@ -1528,7 +1557,7 @@ static aesfhe_ct *relin_rescale_raw(aesfhe_engine *e, const aesfhe_ct *c, const 
     for (int b = 0; b < c->B; b++) {
         u64 *acc = ks_acc(e, limb(e, c, b, 2, 0), l, rlk);
         for (int cc = 0; cc < 2; cc++)
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
             for (int i = 0; i <= l; i++) {
                 const u64 qi = e->q[i];
                 u64 P = 1;
@@ -1750,7 +1779,7 @@ int aesfhe_linear_bsgs(aesfhe_engine *e, const aesfhe_ct *c, int32_t nb, const a
             memset(S, 0, sizeof(u64) * eN);
             for (int t = t0; t < t0 + nterm[j]; t++) {
                 const u64 *Ei = E + eN * tbaby[t];
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
                 for (int y = 0; y < 2 * ne; y++) {
                     const int lt = y % ne, p = pid[lt];
                     const u64 *pv = pts[t]->data + (size_t)lt * N;
@@ -2025,7 +2054,7 @@ int aesfhe_poly2(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, const
             continue;
         }
         aesfhe_ct *acc = ct_new(e, B, 3, l);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
         for (int li = 0; li <= l; li++) {
             const u64 q = e->q[li];
             const mont_t *mt = &e->mont[li];
@@ -2158,7 +2187,7 @@ int aesfhe_poly2_int(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, c
             continue;
         }
         aesfhe_ct *acc = ct_new(e, B, 3, l);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
         for (int li = 0; li <= l; li++) {
             const u64 q = e->q[li];
             const mont_t *mt = &e->mont[li];
@@ -2227,7 +2256,7 @@ int aesfhe_mod_raise(aesfhe_engine *e, const aesfhe_ct *c, int32_t level, aesfhe
             memcpy(t, limb(e, c, b, pp, 0), sizeof(u64) * N);
             ntt_inv(e, t, 0);
             for (int k = 0; k < N; k++) x[k] = t[k] > (q0 >> 1) ? (i64)t[k] - (i64)q0 : (i64)t[k];
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
             for (int i = 0; i <= level; i++) coeffs_to_ntt(e, x, limb(e, r, b, pp, i), i);
             free(x);
             free(t);
@@ -2268,7 +2297,7 @@ int aesfhe_dot_pt(aesfhe_engine *e, const aesfhe_ct *const *cts, const aesfhe_pt
         aesfhe_ct *t = level_down_raw(e, cts[i], l);
         for (int b = 0; b < B; b++)
             for (int pp = 0; pp < np; pp++)
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
                 for (int x = 0; x <= l; x++) {
                     const u64 q = e->q[x];
                     const u64 *src = limb(e, t, t->B == 1 ? 0 : b, pp, x);
@@ -2293,7 +2322,7 @@ int aesfhe_dot_pt(aesfhe_engine *e, const aesfhe_ct *const *cts, const aesfhe_pt
 int aesfhe_ntt_host(aesfhe_engine *e, uint64_t *limbs, int32_t nlimb, const int32_t *pids, int32_t inv) {
     for (int i = 0; i < nlimb; i++)
         if (pids[i] < 0 || pids[i] >= e->np) return fail(AESFHE_EARG, "bad prime index");
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int i = 0; i < nlimb; i++) {
         if (inv) ntt_inv(e, limbs + (size_t)i * e->N, pids[i]);
         else ntt_fwd(e, limbs + (size_t)i * e->N, pids[i]);

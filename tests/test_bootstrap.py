@@ -133,3 +133,25 @@ def test_bootstrap_bits_full_params(product_lib, gpu_available):
     assert ya.level == 17
     assert np.abs(e.decrypt(ya, sk) - a).max() < 1e-3
     assert np.abs(e.decrypt(yb, sk) - b).max() < 1e-3
+
+
+@pytest.mark.gpu
+def test_bootstrap_general_default_params_decodes_zeta256(product_lib, gpu_available):
+    """The reference's Engine.bootstrap (xor_service.py:120-129) at the default engine
+    parameters (N = 2^16, L = 30, K = 8, 44-bit scale -- fhe.DEFAULT_PARAMS): zeta-256 bytes come
+    back within their decision margin sin(pi / 256) = 0.0123 (measured max error ~4.7e-3; at a
+    40-bit scale it was 1.16, which is why the default is 44)."""
+    from aes_xor_fhe.utils import zeta_decode
+    e = Engine(seed=3, _lib=product_lib)
+    assert (e.log_coeff_count, e.max_level, e.special_prime_count) == (16, 30, 8)
+    sk = e.create_secret_key()
+    pk, rlk, cjk = e.create_public_key(sk), e.create_relinearization_key(sk), e.create_conjugation_key(sk)
+    bk = e.create_bootstrap_key(sk)
+    x = np.random.default_rng(8).integers(0, 256, e.slot_count)
+    z = np.exp(-2j * np.pi * x / 256)
+    out = e.bootstrap(e.encrypt(z, pk, level=0), rlk, cjk, bk)
+    got = e.decrypt(out, sk)
+    err = np.abs(got - z).max()
+    assert err < np.sin(np.pi / 256), err
+    assert np.array_equal(zeta_decode(got, modulus=256), x.astype(np.uint8))
+    assert out.level == e.max_level - bk.bootstrapper(rlk, cjk).depth
