@@ -35,6 +35,7 @@ class Params(C.Structure):
         ("threads", C.c_int32),
         ("seed", C.c_uint64),
         ("primes", C.POINTER(C.c_uint64)),
+        ("seed_ext", C.c_uint64 * 3),
     ]
 
 

@@ -28,9 +28,9 @@ from ._abi import Lib, Params, c_ct_p, c_key_p, c_pt_p, load_product
 # HomomorphicEncryption.org 128-bit bound on log2(QP) for ternary secrets
 SECURITY_BUDGET = {11: 54, 12: 109, 13: 218, 14: 438, 15: 881, 16: 1772, 17: 3544}
 
-# seed None: a fresh 64-bit engine seed from the OS entropy pool (os.urandom) per engine, so
-# that no two default engines derive the same keys; an explicit seed reproduces every key and
-# encryption (tests, and multi-rank key sharing -- see `nonce_start`).
+# seed None: a fresh 256-bit ChaCha20 engine key from the OS entropy pool (os.urandom) per
+# engine, so that no two default engines derive the same keys; an explicit 64-bit seed reproduces
+# every key and encryption (tests, and multi-rank key sharing -- see `nonce_start`).
 # scale 44 with K = 8: log QP = 50 + 30 * 44 + 8 * 50 = 1770 <= 1772 (128-bit at N = 2^16).  The
 # general-mode Engine.bootstrap the reference's services call (xor_service.py:120-129) needs it:
 # measured at N = 2^16, L = 30 (tools/boot_general_diag.py): max slot error 4.7e-3 at scale 44,
@@ -57,8 +57,10 @@ def _params_for(log_n=None, max_level=None, special_primes=None, scale_bits=None
             p[k] = v
     p["threads"] = threads
     p["device"] = device
+    p["seed_ext"] = (0, 0, 0)
     if p["seed"] is None:
         p["seed"] = _urandom64()
+        p["seed_ext"] = (_urandom64(), _urandom64(), _urandom64())
     return p
 
 
@@ -258,7 +260,8 @@ class Engine:
         self._lib = _lib if _lib is not None else load_product()
         self._params = p
         cp = Params(p["log_n"], p["max_level"], p["special_primes"], p["scale_bits"],
-                    p["base_bits"], p["special_bits"], p["device"], p["threads"], p["seed"], None)
+                    p["base_bits"], p["special_bits"], p["device"], p["threads"], p["seed"], None,
+                    (C.c_uint64 * 3)(*p["seed_ext"]))
         h = C.c_void_p()
         self._check(self._lib.engine_create(C.byref(cp), C.byref(h)))
         self._h = h.value

@@ -74,8 +74,56 @@ inline unsigned bit_reverse(unsigned x, int bits) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// counter-based PRNG.  NOT a cryptographic generator: a production deployment
-// swaps mix64 for ChaCha20 behind the same (key, index) interface.
+// counter-based PRNG.  rnd(K, label, idx) = 64-bit word idx mod 8 of the
+// ChaCha20 block (RFC 7539 rounds; the original 64-bit counter / 64-bit nonce layout) keyed by the
+// engine's 256-bit key K, nonce = the stream label, block counter = idx / 8.  Labels are public
+// domain separators (derive: SplitMix64 mixing of key seeds, purposes and nonces); every secret and
+// every error / mask sample comes from ChaCha20 under K, so its strength rests on K's entropy
+// (256 bits from the OS for an unseeded engine; an explicit 64-bit seed is for reproducible tests).
+struct ChaKey {
+    uint32_t k[8];
+};
+AESFHE_HD inline uint32_t cc_rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+#define AESFHE_QR(a, b, c, d)                 \
+    a += b, d ^= a, d = cc_rotl(d, 16);       \
+    c += d, b ^= c, b = cc_rotl(b, 12);       \
+    a += b, d ^= a, d = cc_rotl(d, 8);        \
+    c += d, b ^= c, b = cc_rotl(b, 7)
+AESFHE_HD inline void chacha20_block(const ChaKey& K, u64 label, u64 ctr, uint32_t out[16]) {
+    uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                      K.k[0], K.k[1], K.k[2], K.k[3], K.k[4], K.k[5], K.k[6], K.k[7],
+                      (uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)label, (uint32_t)(label >> 32)};
+    uint32_t w[16];
+    for (int i = 0; i < 16; i++) w[i] = x[i];
+    for (int r = 0; r < 10; r++) {
+        AESFHE_QR(w[0], w[4], w[8], w[12]);
+        AESFHE_QR(w[1], w[5], w[9], w[13]);
+        AESFHE_QR(w[2], w[6], w[10], w[14]);
+        AESFHE_QR(w[3], w[7], w[11], w[15]);
+        AESFHE_QR(w[0], w[5], w[10], w[15]);
+        AESFHE_QR(w[1], w[6], w[11], w[12]);
+        AESFHE_QR(w[2], w[7], w[8], w[13]);
+        AESFHE_QR(w[3], w[4], w[9], w[14]);
+    }
+    for (int i = 0; i < 16; i++) out[i] = w[i] + x[i];
+}
+#undef AESFHE_QR
+AESFHE_HD inline u64 rnd(const ChaKey& K, u64 label, u64 idx) {
+    uint32_t o[16];
+    chacha20_block(K, label, idx >> 3, o);
+    const int w = (int)(idx & 7);
+    return (u64)o[2 * w] | ((u64)o[2 * w + 1] << 32);
+}
+// engine key from the engine seed words (seed, ext[0..2]) as little-endian 32-bit halves
+inline ChaKey chacha_key(u64 seed, const u64* ext) {
+    ChaKey K;
+    const u64 w[4] = {seed, ext ? ext[0] : 0, ext ? ext[1] : 0, ext ? ext[2] : 0};
+    for (int i = 0; i < 4; i++) {
+        K.k[2 * i] = (uint32_t)w[i];
+        K.k[2 * i + 1] = (uint32_t)(w[i] >> 32);
+    }
+    return K;
+}
 AESFHE_HD inline u64 mix64(u64 z) {
     z += 0x9E3779B97F4A7C15ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -83,7 +131,6 @@ AESFHE_HD inline u64 mix64(u64 z) {
     return z ^ (z >> 31);
 }
 AESFHE_HD inline u64 derive(u64 a, u64 b) { return mix64(a ^ mix64(b)); }
-AESFHE_HD inline u64 rnd(u64 key, u64 idx) { return mix64(key ^ (idx * 0xD1B54A32D192ED03ULL)); }
 AESFHE_HD inline i64 ternary(u64 r) {
     u64 t = r % 3;
     return t == 0 ? 0 : (t == 1 ? 1 : -1);

@@ -198,6 +198,7 @@ struct aesfhe_engine {
     int logN, N, L, K, dnum, np, Lp1;
     int device;
     u64 seed;
+    ChaKey ck;  // ChaCha20 key of every random stream
     Chain chain;
     hipStream_t stream;
     Pool pool;
@@ -446,7 +447,9 @@ static void ntt_inv_t(aesfhe_engine* e, Span src, Span dst, int total) {
     }
 }
 
-// N = 2^16: register-resident radix-16x16 fp64-arithmetic passes (ntt256f.h)
+// N = 2^16 / 2^17: register-resident fp64-arithmetic passes over R = N / 256 rows of 256
+// (ntt256f.h): a column pass (the first log2 R stages) and a row pass (the last 8)
+template <int R>
 static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
     Tabs T = e->tabs();
     // algorithmic bytes per pass: 8 B * N * limbs = half of the transform's read-once +
@@ -454,21 +457,29 @@ static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse
     const double by = 8.0 * e->N * (double)total;
     {
         ProfScope ps(e, FAM_NTT, by);
-        if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
-        else hipLaunchKernelGGL(k_nttf_inv_rows, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
+        if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_cols<R>, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
+        else hipLaunchKernelGGL(k_nttf_inv_rows<R>, dim3(R / 16, total), dim3(256), 0, e->stream, src, dst, T);
     }
     ProfScope ps(e, FAM_NTT, by);
-    if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_rows_t<false>, dim3(16, total), dim3(256), 0, e->stream, dst, T, RowFin{});
-    else hipLaunchKernelGGL(k_nttf_inv_cols, dim3(16, total), dim3(256), 0, e->stream, dst, T);
+    if (!inverse) hipLaunchKernelGGL((k_nttf_fwd_rows_t<false, R>), dim3(R / 16, total), dim3(256), 0, e->stream, dst, T, RowFin{});
+    else hipLaunchKernelGGL(k_nttf_inv_cols<R>, dim3(16, total), dim3(256), 0, e->stream, dst, T);
 }
 
-// the N = 2^16 fp64 passes with fused epilogues (ModDown finish, key-switch inner product)
-static bool fused_ntt(const aesfhe_engine* e) { return e->logN == 16; }
+// the N = 2^16 / 2^17 fp64 passes with fused epilogues (ModDown finish, key-switch inner product)
+static bool fused_ntt(const aesfhe_engine* e) { return e->logN == 16 || e->logN == 17; }
+
+// the fp64 column pass alone (the extension limbs and the conv of a ModDown, whose row passes run
+// fused with their consumers)
+static void ntt_fwd_cols(aesfhe_engine* e, Span sp, int total) {
+    if (e->logN == 16) hipLaunchKernelGGL(k_nttf_fwd_cols<256>, dim3(16, total), dim3(256), 0, e->stream, sp, sp, e->tabs());
+    else hipLaunchKernelGGL(k_nttf_fwd_cols<512>, dim3(16, total), dim3(256), 0, e->stream, sp, sp, e->tabs());
+}
 
 static void ntt(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
     if (total <= 0) return;
-    if (e->logN == 16) {
-        ntt256(e, src, dst, total, inverse);
+    if (e->logN == 16 || e->logN == 17) {
+        if (e->logN == 16) ntt256<256>(e, src, dst, total, inverse);
+        else ntt256<512>(e, src, dst, total, inverse);
         HIPC(hipGetLastError());
         return;
     }
@@ -547,13 +558,14 @@ static void build_tables(aesfhe_engine* e) {
     up(hipsif, &e->ipsif);
     up(hninv, &e->ninv);
     up(hninvf, &e->ninvf);
-    if (e->logN == 16) {  // row factors psi^{+-brv(row << s)} / q, s = 0..7 (ntt256f.h tw_row)
-        std::vector<double> hr((size_t)np * 2048), hir((size_t)np * 2048);
+    if (fused_ntt(e)) {  // row factors psi^{+-brv(row << s)} / q, s = 0..7, [np][R][8] (ntt256f.h tw_row)
+        const int R = N / 256;
+        std::vector<double> hr((size_t)np * R * 8), hir((size_t)np * R * 8);
         for (int p = 0; p < np; p++)
-            for (int row = 0; row < 256; row++)
+            for (int row = 0; row < R; row++)
                 for (int sh = 0; sh < 8; sh++) {
-                    hr[(size_t)p * 2048 + row * 8 + sh] = hpsif[(size_t)p * N + (row << sh)];
-                    hir[(size_t)p * 2048 + row * 8 + sh] = hipsif[(size_t)p * N + (row << sh)];
+                    hr[((size_t)p * R + row) * 8 + sh] = hpsif[(size_t)p * N + (row << sh)];
+                    hir[((size_t)p * R + row) * 8 + sh] = hipsif[(size_t)p * N + (row << sh)];
                 }
         up(hr, &e->rtwf);
         up(hir, &e->irtwf);
@@ -722,6 +734,7 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
     e->dnum = (e->L + 1 + e->K - 1) / e->K;
     e->device = pp->device;
     e->seed = pp->seed;
+    e->ck = chacha_key(pp->seed, pp->seed_ext);
     if (pp->primes) {
         e->chain.q.assign(pp->primes, pp->primes + e->np);
         e->chain.scale = scales_from_primes(e->chain.q, e->L, pp->scale_bits);
@@ -930,7 +943,7 @@ static aesfhe_key* key_new(aesfhe_engine* e, int kind, size_t words) {
 static void sample_small_ntt(aesfhe_engine* e, u64* dst, int nprimes, u64 key, int kind) {
     Span s = span_s(dst, 0, nprimes, std::min(nprimes, e->Lp1), 0, e->Lp1);
     s.pstride = (long)nprimes * e->N;
-    hipLaunchKernelGGL(k_sample_small, dim3(e->N / 256, nprimes), dim3(256), 0, e->stream, s, key, kind, e->q, e->logN, e->Lp1);
+    hipLaunchKernelGGL(k_sample_small, dim3(e->N / 256, nprimes), dim3(256), 0, e->stream, s, e->ck, key, kind, e->q, e->logN, e->Lp1);
     ntt(e, s, s, nprimes, false);
 }
 
@@ -952,7 +965,7 @@ extern "C" int aesfhe_key_public(aesfhe_engine* e, const aesfhe_key* sk, aesfhe_
     u64* b = k->d;
     u64* a = k->d + (size_t)nq * N;
     Span sa = span_s(a, 0, nq, nq, 0, e->Lp1);
-    hipLaunchKernelGGL(k_sample_uniform, dim3(N / 256, nq), dim3(256), 0, e->stream, sa, derive(sk->keyseed, 2), e->q, e->logN, e->Lp1);
+    hipLaunchKernelGGL(k_sample_uniform, dim3(N / 256, nq), dim3(256), 0, e->stream, sa, e->ck, derive(sk->keyseed, 2), e->q, e->logN, e->Lp1);
     Tmp et(e, (size_t)nq * N);
     sample_small_ntt(e, et.p, nq, derive(sk->keyseed, 3), 1);
     hipLaunchKernelGGL(k_key_combine, dim3(N / 256, nq), dim3(256), 0, e->stream, a, sk->d, et.p, (const u64*)nullptr, (const u64*)nullptr, 0, 0, b, e->q, e->qinv, e->logN);
@@ -976,7 +989,7 @@ static aesfhe_key* make_ksk_t(aesfhe_engine* e, const u64* starget, u64 keyseed,
         u64* kb = k->d + ((size_t)d * 2 + 0) * np * N;
         u64* ka = k->d + ((size_t)d * 2 + 1) * np * N;
         Span sa = span_s(ka, 0, np, e->Lp1, 0, e->Lp1);
-        hipLaunchKernelGGL(k_sample_uniform, dim3(N / 256, np), dim3(256), 0, e->stream, sa, derive(base, 2 * (u64)d), e->q, e->logN, e->Lp1);
+        hipLaunchKernelGGL(k_sample_uniform, dim3(N / 256, np), dim3(256), 0, e->stream, sa, e->ck, derive(base, 2 * (u64)d), e->q, e->logN, e->Lp1);
         sample_small_ntt(e, et.p, np, derive(base, 2 * (u64)d + 1), 1);
         int lo = d * e->K, hi = std::min(lo + e->K, e->Lp1);
         hipLaunchKernelGGL(k_key_combine, dim3(N / 256, np), dim3(256), 0, e->stream, (const u64*)ka, starget, et.p, sprime, e->pmod, lo, hi, kb, e->q, e->qinv, e->logN);
@@ -1029,7 +1042,7 @@ extern "C" int aesfhe_key_galois_hoisted(aesfhe_engine* e, const aesfhe_key* sk,
 
 // Sparse ternary secret with exactly hw nonzero coefficients (bootstrapping's ephemeral secret):
 // key = derive(derive(seed_e, seed), 9); partial Fisher-Yates over 0..N-1: position i swaps with
-// i + rnd(key, i) mod (N - i), the coefficient there is -1 if rnd(key, N + i) is odd else +1.
+// i + rnd(K, key, i) mod (N - i), the coefficient there is -1 if rnd(K, key, N + i) is odd else +1.
 extern "C" int aesfhe_key_secret_sparse(aesfhe_engine* e, uint64_t seed, int32_t hw, aesfhe_key** out) {
     API_BEGIN
     const int N = e->N;
@@ -1041,9 +1054,9 @@ extern "C" int aesfhe_key_secret_sparse(aesfhe_engine* e, uint64_t seed, int32_t
     for (int i = 0; i < N; i++) idx[i] = i;
     std::vector<int64_t> co(N, 0);
     for (int i = 0; i < hw; i++) {
-        const int j = i + (int)(rnd(key, (u64)i) % (u64)(N - i));
+        const int j = i + (int)(rnd(e->ck, key, (u64)i) % (u64)(N - i));
         std::swap(idx[i], idx[j]);
-        co[idx[i]] = (rnd(key, (u64)N + i) & 1) ? -1 : 1;
+        co[idx[i]] = (rnd(e->ck, key, (u64)N + i) & 1) ? -1 : 1;
     }
     Tmp dco(e, N);
     HIPC(hipMemcpyAsync(dco.p, co.data(), (size_t)N * 8, hipMemcpyHostToDevice, e->stream));
@@ -1273,10 +1286,10 @@ extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int
         u64* vb = vem.p + (size_t)b * 4 * step;
         Span sv = span_s(vb, 0, nl, nl, 0, e->Lp1), se0 = span_s(vb + step, 0, nl, nl, 0, e->Lp1), se1 = span_s(vb + 2 * step, 0, nl, nl, 0, e->Lp1);
         if (key->kind == 1)
-            hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, sv, k0, 0, e->q, e->logN, e->Lp1);
-        hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, se0, k1, 1, e->q, e->logN, e->Lp1);
+            hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, sv, e->ck, k0, 0, e->q, e->logN, e->Lp1);
+        hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, se0, e->ck, k1, 1, e->q, e->logN, e->Lp1);
         if (key->kind == 1)
-            hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, se1, k2, 1, e->q, e->logN, e->Lp1);
+            hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, se1, e->ck, k2, 1, e->q, e->logN, e->Lp1);
         hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, nl, 1), dim3(256), 0, e->stream, (const i64*)(dco.p + (size_t)b * N), vb + 3 * step, nl, e->q, e->logN);
     }
     // NTT everything: B * 4 groups of nl limbs (pid = limb index)
@@ -1288,7 +1301,7 @@ extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int
         hipLaunchKernelGGL(k_enc_pk, dim3(N / 256, nl, B), dim3(256), 0, e->stream, (const u64*)vem.p, pk0, pk1, c->d, nl, e->q, e->qinv, e->logN);
     } else {
         u64* dk = upload_small(e, k0s.data(), k0s.size());
-        hipLaunchKernelGGL(k_enc_sk, dim3(N / 256, nl, B), dim3(256), 0, e->stream, (const u64*)vem.p, (const u64*)key->d, c->d, nl, e->q, e->qinv, (const u64*)dk, e->logN);
+        hipLaunchKernelGGL(k_enc_sk, dim3(N / 256, nl, B), dim3(256), 0, e->stream, (const u64*)vem.p, (const u64*)key->d, c->d, nl, e->q, e->qinv, e->ck, (const u64*)dk, e->logN);
     }
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(e->stream));  // host coefficient buffer may be reused by caller
@@ -1715,7 +1728,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         auto fwd = [&](Span sp, int total) {
             if (!cols_only) return ntt(e, sp, sp, total, false);
             ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
-            hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, sp, sp, e->tabs());
+            ntt_fwd_cols(e, sp, total);
         };
         if (lo > 0) fwd(span_s(exj, neN, lo, lo, 0, e->Lp1), B * lo);
         {
@@ -1744,8 +1757,9 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
         // (key read once per call, accumulators written; ext never leaves the chip)
         const int nown = std::min(l + 1, beta * K);
         ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))));
-        const int blocks = 8 * B * (ne * 32 / 8);
-        hipLaunchKernelGGL(k_nttf_rows_ks<1>, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum);
+        const int R = N / 256, blocks = 8 * B * (ne * (R / 8) / 8);
+        auto kern = R == 256 ? k_nttf_rows_ks<1, 256> : k_nttf_rows_ks<1, 512>;
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum);
     } else {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B * (accum ? 2 : 1)));
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
@@ -1789,13 +1803,14 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
         const int total = B * 2 * (lk + 1);
         {
             ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
-            hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, total), dim3(256), 0, e->stream, sc, sc, T);
+            ntt_fwd_cols(e, sc, total);
         }
         RowFin f{(const u64*)acc, 2 * neN, neN, Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}, o->d,
                  2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf, lk + 1};
         // the row pass (credited half an NTT) plus the finish: acc read, output written (+ addend)
         ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total * (3.0 + (fin_add.ptr ? 1.0 : 0.0)));
-        hipLaunchKernelGGL(k_nttf_fwd_rows_t<true>, dim3(16, total), dim3(256), 0, e->stream, sc, T, f);
+        if (N == 65536) hipLaunchKernelGGL((k_nttf_fwd_rows_t<true, 256>), dim3(16, total), dim3(256), 0, e->stream, sc, T, f);
+        else hipLaunchKernelGGL((k_nttf_fwd_rows_t<true, 512>), dim3(32, total), dim3(256), 0, e->stream, sc, T, f);
         HIPC(hipGetLastError());
         return;
     }

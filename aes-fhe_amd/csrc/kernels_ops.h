@@ -582,21 +582,21 @@ __global__ void k_galois(Span src, Span dst, u64 g, int logN, int Lp1) {
 
 // ---------------------------------------------------------------------------------------------
 // sampling.  Uniform residues directly in the NTT domain, index pid*N + k.
-__global__ void k_sample_uniform(Span dst, u64 key, const u64* __restrict__ qall, int logN,
+__global__ void k_sample_uniform(Span dst, ChaKey K, u64 key, const u64* __restrict__ qall, int logN,
                                  int Lp1) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     int pid;
     u64* out = span_ptr(dst, blockIdx.y, logN, Lp1, pid);
-    out[k] = __umul64hi(rnd(key, ((u64)pid << logN) + k), qall[pid]);
+    out[k] = __umul64hi(rnd(K, key, ((u64)pid << logN) + k), qall[pid]);
 }
 
 // small coefficient polynomial (kind 0 ternary, 1 CBD-21) -> residues of every limb (coef form)
-__global__ void k_sample_small(Span dst, u64 key, int kind, const u64* __restrict__ qall,
+__global__ void k_sample_small(Span dst, ChaKey K, u64 key, int kind, const u64* __restrict__ qall,
                                int logN, int Lp1) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     int pid;
     u64* out = span_ptr(dst, blockIdx.y, logN, Lp1, pid);
-    const u64 r = rnd(key, (u64)k);
+    const u64 r = rnd(K, key, (u64)k);
     const i64 v = kind == 0 ? ternary(r) : cbd21(r);
     const u64 q = qall[pid];
     out[k] = v >= 0 ? (u64)v : q - (u64)(-v);
@@ -653,7 +653,7 @@ __global__ void k_enc_pk(const u64* __restrict__ vem, const u64* __restrict__ pk
 // secret-key encryption: c1 = a (uniform, NTT), c0 = -a s + e0 + m ; vem as above with v unused
 __global__ void k_enc_sk(const u64* __restrict__ vem, const u64* __restrict__ s,
                          u64* __restrict__ ct, int nl, const u64* __restrict__ qs,
-                         const double* __restrict__ qinv, const u64* __restrict__ keys, int logN) {
+                         const double* __restrict__ qinv, ChaKey K, const u64* __restrict__ keys, int logN) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int l = blockIdx.y, bb = blockIdx.z;
     const u64 q = qs[l];
@@ -662,7 +662,7 @@ __global__ void k_enc_sk(const u64* __restrict__ vem, const u64* __restrict__ s,
     const long step = (long)nl << logN;
     const u64* base = vem + (long)bb * 4 * step + lo;
     u64 e0 = base[step], m = base[3 * step];
-    u64 a = __umul64hi(rnd(keys[bb], ((u64)l << logN) + k), q);
+    u64 a = __umul64hi(rnd(K, keys[bb], ((u64)l << logN) + k), q);
     u64* c = ct + (long)bb * 2 * step + lo;
     c[step] = a;
     c[0] = add_m(add_m(sub_m(0, mul_m(a, s[lo], q, qi), q), e0, q), m, q);

@@ -1,4 +1,4 @@
-// ks_fused.h -- key-switch inner product fused into the row pass of the ext NTT (N = 2^16).
+// ks_fused.h -- key-switch inner product fused into the row pass of the ext NTT (N = 2^16, 2^17).
 //
 // The unfused key switch (engine.hip ks_modup / ks_apply) writes every extended limb ext[j][b][t]
 // in canonical NTT form (row pass) and reads it straight back in k_ks_inner_all:
@@ -106,12 +106,13 @@ __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, doub
     __syncthreads();  // the next digit rewrites sr
 }
 
-// grid: 8 * ceil(B / G) * (ne * 32 / 8) blocks of 256 (8 rows x 32 lanes); block id -> (xcd group
+// grid: 8 * ceil(B / G) * (ne * (R / 8) / 8) blocks of 256 (8 rows x 32 lanes; R = N / 256 rows:
+// 256 or 512); block id -> (xcd group
 // x = id & 7, batch group, pair), pair = (t, 8-row block): all batch groups of one (t, row block)
 // are dealt to one XCD (blocks x, x + 8, ...) so the key rows they share are L2 hits.  G batch
 // elements per workgroup share each key word loaded (G = 2 halves the key reads, the largest
 // load stream of the kernel, at the price of a second pair of accumulators).
-template <int G>
+template <int G, int R = 256>
 __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64* __restrict__ d, long dbs,
                                                       const u64* __restrict__ ext, long exs, long exj,
                                                       const u64* __restrict__ key, long kdig, long kcomp,
@@ -123,7 +124,9 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
     const int nbg = (B + G - 1) / G;
     const int id = blockIdx.x, x8 = id & 7, rest = id >> 3;
     const int b0 = (rest % nbg) * G, pair = (rest / nbg) * 8 + x8;
-    const int t = pair >> 5, rb = pair & 31;
+    constexpr int RB = R / 8;  // 8-row blocks per limb
+    constexpr int LOGN = R == 256 ? 16 : 17;
+    const int t = pair / RB, rb = pair - t * RB;
     if (t >= ne) return;
     const int pid = t <= l ? t : T.Lp1 + (t - l - 1);
     const int own = t <= l ? t / K : -1;  // the digit whose limbs include t (Q limbs only)
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
     const int row = rb * 8 + rl;
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
-    const double* W = T.psif + ((long)pid << 16);
+    const double* W = T.psif + ((long)pid << LOGN);
     double* sr = s + rl * 288;
     // the row's 255 twiddles are the same for every digit: staged in LDS once per workgroup
     double* tw = s + 8 * 288 + rl * 256;
@@ -140,11 +143,11 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
         const int e = L + 32 * m;
         if (e > 0) {
             const int ml = 1 << (31 - __clz(e));
-            tw[e] = W[(long)ml * (256 + row) + (e - ml)];
+            tw[e] = W[(long)ml * (R + row) + (e - ml)];
         }
     }
     __syncthreads();
-    const long roff = ((long)t << 16) + (long)row * 256 + L;  // element (row, L + 32 r) at roff + 32 r
+    const long roff = ((long)t << LOGN) + (long)row * 256 + L;  // element (row, L + 32 r) at roff + 32 r
     double a0[G][8], a1[G][8];
 #pragma unroll
     for (int g = 0; g < G; g++)
@@ -153,7 +156,7 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
 #pragma unroll 1
     for (int j = 0; j < beta; j++) {
         // the key digit's words are loaded first: they arrive while the row NTT computes
-        const u64* kp = key + (long)j * kdig + ((long)pid << 16) + (long)row * 256 + L;
+        const u64* kp = key + (long)j * kdig + ((long)pid << LOGN) + (long)row * 256 + L;
         u64 kbw[8], kaw[8];
 #pragma unroll
         for (int r = 0; r < 8; r++) {
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
 #pragma unroll
                 for (int r = 0; r < 8; r++) v[r] = u2d(dp[32 * r]);
             } else {
-                row_ntt8_fwd(v, ext + (long)j * exj + (long)bb * exs + ((long)t << 16) + (long)row * 256, sr, L, 1,
+                row_ntt8_fwd(v, ext + (long)j * exj + (long)bb * exs + ((long)t << LOGN) + (long)row * 256, sr, L, 1,
                              tw, q, qi, big);
             }
 #pragma unroll
@@ -200,8 +203,8 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
 #pragma unroll
             for (int r = 0; r < 8; r++) {
                 const int kk = row * 256 + L + 32 * r;
-                a0[g][r] = fred(a0[g][r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 0, t, kk, 16)), w, f, q);
-                a1[g][r] = fred(a1[g][r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, kk, 16)), w, f, q);
+                a0[g][r] = fred(a0[g][r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 0, t, kk, LOGN)), w, f, q);
+                a1[g][r] = fred(a1[g][r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, kk, LOGN)), w, f, q);
             }
         }
 #pragma unroll

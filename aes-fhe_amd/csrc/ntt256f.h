@@ -74,11 +74,18 @@ __device__ __forceinline__ void st_d(u64* p, double v) { __builtin_nontemporal_s
 
 constexpr int kPadF = 17;  // LDS row stride (8 B words) of the 16 x 16 transpose tiles
 
-// Forward, column pass: stages m = 1..128 on columns of stride 256; canonical u64 in, raw
-// doubles out.  Workgroup = 16 columns [c0, c0+16); lane (cl, b) = (tid & 15, tid >> 4).
+// Forward, column pass: the first log2(R) stages on columns of stride 256 (R = N / 256 rows:
+// 256 for N = 2^16, 512 for N = 2^17); canonical u64 in, raw doubles out.  Workgroup = 16
+// columns [c0, c0+16); lane (cl, b) = (tid & 15, tid >> 4).  R = 512: the first stage (distance
+// 256 rows) pairs the two 256-row halves in registers; each half is then an independent
+// 256-point column transform whose stage-m twiddles sit at m (2 + h) + group (half h, group
+// within the half), so the R = 256 code runs on each half with the index multiplier 2 + h.
+template <int R = 256>
 __global__ __launch_bounds__(256) void k_nttf_fwd_cols(Span src, Span dst, Tabs T) {
+    static_assert(R == 256 || R == 512, "rows of 256: N = 2^16 or 2^17");
+    constexpr int H = R / 256;
     __shared__ double s[256 * kPadF];
-    __shared__ double twq[256];
+    __shared__ double twq[R];
     int pid;
     const u64* in = span_ptr(src, blockIdx.y, T.logN, T.Lp1, pid);
     u64* out = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
@@ -87,45 +94,59 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_cols(Span src, Span dst, Tabs 
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* tg = T.psif + ((long)pid << T.logN);
-    twq[tid] = tg[tid];
-    double x[16];
 #pragma unroll
-    for (int a = 0; a < 16; a++) x[a] = u2d(in[(a * 16 + b) * 256 + c]);
+    for (int h = 0; h < H; h++) twq[tid + 256 * h] = tg[tid + 256 * h];
+    double x[16 * H];
+#pragma unroll
+    for (int h = 0; h < H; h++)
+#pragma unroll
+        for (int a = 0; a < 16; a++) x[16 * h + a] = u2d(in[(h * 256 + a * 16 + b) * 256 + c]);
     __syncthreads();
+    if (H == 2) {  // stage m = 1 across the halves: canonical in, (-q, 2q) out
+        const double w = tg[1];
 #pragma unroll
-    for (int st = 0; st < 4; st++) {
-        const int m = 1 << st, h = 8 >> st;
-        if (big && st == 2) {
-#pragma unroll
-            for (int a = 0; a < 16; a++) x[a] = fred(x[a], q, qi);
-        }
-#pragma unroll
-        for (int a = 0; a < 16; a++) {
-            if (a & h) continue;
-            ct_f(x[a], x[a + h], tg[m + (a >> (4 - st))], q);  // uniform: scalar load
-        }
+        for (int a = 0; a < 16; a++) ct_f(x[a], x[16 + a], w, q);
     }
 #pragma unroll
-    for (int a = 0; a < 16; a++) s[(a * 16 + b) * kPadF + cl] = x[a];
-    __syncthreads();
-    const int ap = b;
+    for (int h = 0; h < H; h++) {
+        double* xh = x + 16 * h;
+        const int mul = H == 1 ? 1 : 2 + h;
 #pragma unroll
-    for (int bb = 0; bb < 16; bb++) x[bb] = s[(ap * 16 + bb) * kPadF + cl];
+        for (int st = 0; st < 4; st++) {
+            const int m = 1 << st, hh = 8 >> st;
+            if (big && (H == 1 ? st == 2 : (st & 1) == 0)) {
 #pragma unroll
-    for (int st = 4; st < 8; st++) {
-        const int m = 1 << st, h = 128 >> st;
-        if (big && (st & 1) == 0) {
+                for (int a = 0; a < 16; a++) xh[a] = fred(xh[a], q, qi);
+            }
 #pragma unroll
-            for (int bb = 0; bb < 16; bb++) x[bb] = fred(x[bb], q, qi);
+            for (int a = 0; a < 16; a++) {
+                if (a & hh) continue;
+                ct_f(xh[a], xh[a + hh], tg[m * mul + (a >> (4 - st))], q);  // uniform: scalar load
+            }
+        }
+        if (h > 0) __syncthreads();  // the previous half's LDS reads are done
+#pragma unroll
+        for (int a = 0; a < 16; a++) s[(a * 16 + b) * kPadF + cl] = xh[a];
+        __syncthreads();
+        const int ap = b;
+#pragma unroll
+        for (int bb = 0; bb < 16; bb++) xh[bb] = s[(ap * 16 + bb) * kPadF + cl];
+#pragma unroll
+        for (int st = 4; st < 8; st++) {
+            const int m = 1 << st, hh = 128 >> st;
+            if (big && (st & 1) == 0) {
+#pragma unroll
+                for (int bb = 0; bb < 16; bb++) xh[bb] = fred(xh[bb], q, qi);
+            }
+#pragma unroll
+            for (int bb = 0; bb < 16; bb++) {
+                if (bb & hh) continue;
+                ct_f(xh[bb], xh[bb + hh], twq[m * mul + ap * (m >> 4) + (bb >> (8 - st))], q);
+            }
         }
 #pragma unroll
-        for (int bb = 0; bb < 16; bb++) {
-            if (bb & h) continue;
-            ct_f(x[bb], x[bb + h], twq[m + ap * (m >> 4) + (bb >> (8 - st))], q);
-        }
+        for (int bb = 0; bb < 16; bb++) st_d(&out[(h * 256 + ap * 16 + bb) * 256 + c], xh[bb]);
     }
-#pragma unroll
-    for (int bb = 0; bb < 16; bb++) st_d(&out[(ap * 16 + bb) * 256 + c], x[bb]);
 }
 
 // ModDown finish fused into the row pass of the conv NTT (key switch): limb y of
@@ -145,6 +166,7 @@ struct RowFin {
 // row = r0 + rl from rp (raw doubles, stride-16 gather), 4 stages in registers, LDS transpose
 // through sr = s + rl * 16 * kPadF, 4 stages.  On return lane ap = b holds elements
 // ap * 16 + bb (bb = 0..15) of its row, lazily reduced (ranges: file header).
+template <int RR>
 __device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, double* sr, int b, int row,
                                             const double* W, const double* R, double q, double qi,
                                             bool big) {
@@ -161,7 +183,7 @@ __device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, doub
 #pragma unroll
         for (int j = 0; j < ml; j++) {  // butterflies of twiddle j: a = j * 2h + k, k < h
             double w, wq;
-            tw_row(W, 256 * ml + j, rq, q, qi, w, wq);
+            tw_row(W, RR * ml + j, rq, q, qi, w, wq);
 #pragma unroll
             for (int k = 0; k < h; k++) ct_fw(x[j * 2 * h + k], x[j * 2 * h + k + h], w, wq, q);
         }
@@ -183,7 +205,7 @@ __device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, doub
 #pragma unroll
         for (int j = 0; j < nj; j++) {  // bb = j * 2h + k, k < h
             double w, wq;
-            tw_row(W, 256 * ml + ap * nj + j, rq, q, qi, w, wq);
+            tw_row(W, RR * ml + ap * nj + j, rq, q, qi, w, wq);
 #pragma unroll
             for (int k = 0; k < h; k++) ct_fw(x[j * 2 * h + k], x[j * 2 * h + k + h], w, wq, q);
         }
@@ -199,7 +221,7 @@ __device__ __forceinline__ int row_tile_idx(int e) {
 // Forward, row pass: stages m = 256..32768 within rows of 256 contiguous elements; raw doubles
 // in, canonical u64 out (FIN: the ModDown finish above).  Workgroup = 16 rows [r0, r0+16);
 // lane (b, rl) = (tid & 15, tid >> 4).
-template <bool FIN>
+template <bool FIN, int R = 256>
 __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFin fin) {
     __shared__ double s[16 * 16 * kPadF];
     int pid;
@@ -209,11 +231,11 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* W = T.psif + ((long)pid << T.logN);
-    const double* R = T.rtwf + ((long)pid << 11) + row * 8;
+    const double* Rf = T.rtwf + (long)pid * R * 8 + row * 8;
     double x[16];
     double* sr = s + rl * 16 * kPadF;
     const int ap = b;
-    row_ntt_fwd(x, io + (long)row * 256, sr, b, row, W, R, q, qi, big);
+    row_ntt_fwd<R>(x, io + (long)row * 256, sr, b, row, W, Rf, q, qi, big);
     // coalesced store through LDS: canonical residues, then row-major copy-out
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) sr[ap * kPadF + bb] = __longlong_as_double((long long)fcanon(x[bb], q, qi));
@@ -245,6 +267,7 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
 
 // Inverse, row pass (Gentleman-Sande, distances 1..128 within rows): canonical u64 in (src),
 // raw doubles out (dst).
+template <int RR = 256>
 __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Tabs T) {
     __shared__ double s[16 * 16 * kPadF];
     int pid;
@@ -267,7 +290,7 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
     double x[16];
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) x[bb] = sr[ap * kPadF + bb];
-    const double* R = T.irtwf + ((long)pid << 11) + row * 8;
+    const double* R = T.irtwf + (long)pid * RR * 8 + row * 8;
     auto stages_lo = [&](auto fold) {
 #pragma unroll
         for (int st = 0; st < 4; st++) {
@@ -276,7 +299,7 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
 #pragma unroll
             for (int j = 0; j < nj; j++) {  // butterflies of twiddle j: bb = j * 2t + k, k < t
                 double w, wq;
-                tw_row(W, 256 * ml + ap * nj + j, rq, q, qi, w, wq);
+                tw_row(W, RR * ml + ap * nj + j, rq, q, qi, w, wq);
 #pragma unroll
                 for (int k = 0; k < t; k++)
                     gs_fw<decltype(fold)::value>(x[j * 2 * t + k], x[j * 2 * t + k + t], w, wq, q, qi);
@@ -298,7 +321,7 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
 #pragma unroll
             for (int j = 0; j < ml; j++) {  // a = j * 2ta + k, k < ta
                 double w, wq;
-                tw_row(W, 256 * ml + j, rq, q, qi, w, wq);
+                tw_row(W, RR * ml + j, rq, q, qi, w, wq);
 #pragma unroll
                 for (int k = 0; k < ta; k++)
                     gs_fw<decltype(fold)::value>(x[j * 2 * ta + k], x[j * 2 * ta + k + ta], w, wq, q, qi);
@@ -312,11 +335,16 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
     for (int a = 0; a < 16; a++) st_d(&op[a * 16 + b], x[a]);
 }
 
-// Inverse, column pass (distances 256..32768 = rows 1..128) and the N^{-1} scaling: raw
-// doubles in, canonical u64 out.
+// Inverse, column pass (distances 256..32768 = rows 1..128 of each 256-row half) and the N^{-1}
+// scaling: raw doubles in, canonical u64 out.  R = 512 (N = 2^17): both halves run the R = 256
+// stages (twiddle index multiplier 2 + h, as in the forward pass), stay in registers, and the
+// last stage (distance 256 rows) pairs them before the scaling.
+template <int R = 256>
 __global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T) {
+    static_assert(R == 256 || R == 512, "rows of 256: N = 2^16 or 2^17");
+    constexpr int H = R / 256;
     __shared__ double s[256 * kPadF];
-    __shared__ double twq[256];
+    __shared__ double twq[R];
     int pid;
     u64* io = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
     const int tid = threadIdx.x, cl = tid & 15, b = tid >> 4;
@@ -324,51 +352,71 @@ __global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T) {
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* tg = T.ipsif + ((long)pid << T.logN);
-    twq[tid] = tg[tid];
+#pragma unroll
+    for (int h = 0; h < H; h++) twq[tid + 256 * h] = tg[tid + 256 * h];
     const int ap = b;
-    double x[16];
+    double x[16 * H];
 #pragma unroll
-    for (int bb = 0; bb < 16; bb++) x[bb] = fred(ld_d(&io[(ap * 16 + bb) * 256 + c]), q, qi);
-    __syncthreads();
-    auto stages_lo = [&](auto fold) {
+    for (int h = 0; h < H; h++)
 #pragma unroll
-        for (int st = 0; st < 4; st++) {
-            const int tr = 1 << st;
-            const int base = 128 / tr + ap * (8 / tr);
-#pragma unroll
-            for (int bb = 0; bb < 16; bb++) {
-                if (bb & tr) continue;
-                gs_f<decltype(fold)::value>(x[bb], x[bb + tr], twq[base + (bb >> (st + 1))], q, qi);
-            }
-        }
-    };
-    if (big) stages_lo(std::true_type{});
-    else stages_lo(std::false_type{});
-#pragma unroll
-    for (int bb = 0; bb < 16; bb++) s[(ap * 16 + bb) * kPadF + cl] = x[bb];
+        for (int bb = 0; bb < 16; bb++) x[16 * h + bb] = fred(ld_d(&io[(h * 256 + ap * 16 + bb) * 256 + c]), q, qi);
     __syncthreads();
 #pragma unroll
-    for (int a = 0; a < 16; a++) x[a] = s[(a * 16 + b) * kPadF + cl];
-    auto stages_hi = [&](auto fold) {
+    for (int h = 0; h < H; h++) {
+        double* xh = x + 16 * h;
+        const int mul = H == 1 ? 1 : 2 + h;
+        auto stages_lo = [&](auto fold) {
 #pragma unroll
-        for (int st = 4; st < 8; st++) {
-            const int tr = 1 << st, ta = tr >> 4;
-            const int base = 128 / tr;
+            for (int st = 0; st < 4; st++) {
+                const int tr = 1 << st;
+                const int base = (128 / tr) * mul + ap * (8 / tr);
 #pragma unroll
-            for (int a = 0; a < 16; a++) {
-                if (a & ta) continue;
-                gs_f<decltype(fold)::value>(x[a], x[a + ta], tg[base + (a >> (st - 3))], q, qi);  // uniform
+                for (int bb = 0; bb < 16; bb++) {
+                    if (bb & tr) continue;
+                    gs_f<decltype(fold)::value>(xh[bb], xh[bb + tr], twq[base + (bb >> (st + 1))], q, qi);
+                }
             }
+        };
+        if (big) stages_lo(std::true_type{});
+        else stages_lo(std::false_type{});
+        if (h > 0) __syncthreads();  // the previous half's LDS reads are done
+#pragma unroll
+        for (int bb = 0; bb < 16; bb++) s[(ap * 16 + bb) * kPadF + cl] = xh[bb];
+        __syncthreads();
+#pragma unroll
+        for (int a = 0; a < 16; a++) xh[a] = s[(a * 16 + b) * kPadF + cl];
+        auto stages_hi = [&](auto fold) {
+#pragma unroll
+            for (int st = 4; st < 8; st++) {
+                const int tr = 1 << st, ta = tr >> 4;
+                const int base = (128 / tr) * mul;
+#pragma unroll
+                for (int a = 0; a < 16; a++) {
+                    if (a & ta) continue;
+                    gs_f<decltype(fold)::value>(xh[a], xh[a + ta], tg[base + (a >> (st - 3))], q, qi);  // uniform
+                }
+            }
+        };
+        if (big) stages_hi(std::true_type{});
+        else stages_hi(std::false_type{});
+    }
+    if (H == 2) {  // stage m = 1 across the halves (inputs folded to |x| <= q/2 + 1)
+        const double w = tg[1];
+#pragma unroll
+        for (int a = 0; a < 16; a++) {
+            x[a] = fred(x[a], q, qi);
+            x[16 + a] = fred(x[16 + a], q, qi);
+            gs_f<false>(x[a], x[16 + a], w, q, qi);
         }
-    };
-    if (big) stages_hi(std::true_type{});
-    else stages_hi(std::false_type{});
+    }
     const double ni = (double)T.ninv[pid], nif = T.ninvf[pid];
 #pragma unroll
-    for (int a = 0; a < 16; a++) {
-        const double r = fred(x[a], q, qi);
-        __builtin_nontemporal_store(fcanon(fmul_rem(r, ni, nif, q), q, qi), &io[(a * 16 + b) * 256 + c]);
-    }
+    for (int h = 0; h < H; h++)
+#pragma unroll
+        for (int a = 0; a < 16; a++) {
+            const double r = fred(x[16 * h + a], q, qi);
+            __builtin_nontemporal_store(fcanon(fmul_rem(r, ni, nif, q), q, qi), &io[(h * 256 + a * 16 + b) * 256 + c]);
+        }
 }
 
 

@@ -171,7 +171,9 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     keys = [R.encrypt_round_key(rk) for rk in T.expand_key(key)]
     rng = np.random.default_rng(2000 + rank)
     nb = args.aes10_batch
-    ppc = args.aes10_ppc or max(1, 32 // nb)  # ~32 ciphertexts per Bootstrapper call
+    # ~32 ciphertexts per Bootstrapper call at N = 2^16; half that per doubling of N (a bit
+    # ciphertext at N = 2^17, L = 35 is 2.3x larger: 32 per call overflowed the pool, measured)
+    ppc = args.aes10_ppc or max(1, (32 >> max(0, args.log_n - 16)) // nb)
     # warm-up of the same shape: materialises the bootstrap plaintexts and fills the device pool
     # with every buffer size of the run, so the timed run makes no hipMalloc
     log("aes10: bootstrapper ready; warm-up run")

@@ -81,6 +81,8 @@ typedef struct aesfhe_params {
     int32_t threads;        /* host threads (oracle only; 0 = default) */
     uint64_t seed;          /* engine seed: all key / encryption randomness derives from it */
     const uint64_t *primes; /* optional explicit chain q_0..q_L,p_0..p_{K-1} (NULL = generate) */
+    uint64_t seed_ext[3];   /* with seed: the 256-bit ChaCha20 key of every random stream
+                               (seed, ext[0], ext[1], ext[2]); zeros for a reproducible 64-bit seed */
 } aesfhe_params;
 
 /* ---- diagnostics ---------------------------------------------------------------------- */

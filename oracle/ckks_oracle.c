@@ -160,7 +160,55 @@ static unsigned brv(unsigned x, int bits) {
 }
 
 /* ------------------------------------------------------------------------------------------ */
-/* PRNG: counter-based, shared bit-for-bit with the HIP engine                 */
+/* PRNG: counter-based, shared bit-for-bit with the HIP engine: rnd(K, label, idx)
+ * = 64-bit word idx mod 8 of the ChaCha20 block (20 rounds, RFC 7539 quarter round; the original
+ * 64-bit counter / 64-bit nonce layout) under the engine's 256-bit key K, nonce = label, counter =
+ * idx / 8.  A one-block cache per thread serves the sequential loops (7 of 8 words).             */
+#define CC_ROTL(x, n) (((x) << (n)) | ((x) >> (32 - (n))))
+#define CC_QR(a, b, c, d)                                   \
+    do {                                                    \
+        a += b; d ^= a; d = CC_ROTL(d, 16);                 \
+        c += d; b ^= c; b = CC_ROTL(b, 12);                 \
+        a += b; d ^= a; d = CC_ROTL(d, 8);                  \
+        c += d; b ^= c; b = CC_ROTL(b, 7);                  \
+    } while (0)
+static void chacha20_block(const uint32_t k[8], u64 label, u64 ctr, uint32_t out[16]) {
+    uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, k[0], k[1], k[2], k[3],
+                      k[4], k[5], k[6], k[7], (uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)label,
+                      (uint32_t)(label >> 32)};
+    uint32_t w[16];
+    for (int i = 0; i < 16; i++) w[i] = x[i];
+    for (int r = 0; r < 10; r++) {
+        CC_QR(w[0], w[4], w[8], w[12]);
+        CC_QR(w[1], w[5], w[9], w[13]);
+        CC_QR(w[2], w[6], w[10], w[14]);
+        CC_QR(w[3], w[7], w[11], w[15]);
+        CC_QR(w[0], w[5], w[10], w[15]);
+        CC_QR(w[1], w[6], w[11], w[12]);
+        CC_QR(w[2], w[7], w[8], w[13]);
+        CC_QR(w[3], w[4], w[9], w[14]);
+    }
+    for (int i = 0; i < 16; i++) out[i] = w[i] + x[i];
+}
+static __thread struct {
+    const uint32_t* k;
+    u64 label, ctr;
+    int valid;
+    uint32_t w[16];
+} cc_cache;
+static u64 rnd(const uint32_t k[8], u64 label, u64 idx) {
+    const u64 ctr = idx >> 3;
+    if (!cc_cache.valid || cc_cache.k != k || cc_cache.label != label || cc_cache.ctr != ctr) {
+        chacha20_block(k, label, ctr, cc_cache.w);
+        cc_cache.k = k;
+        cc_cache.label = label;
+        cc_cache.ctr = ctr;
+        cc_cache.valid = 1;
+    }
+    const int j = (int)(idx & 7);
+    return (u64)cc_cache.w[2 * j] | ((u64)cc_cache.w[2 * j + 1] << 32);
+}
+/* stream labels: SplitMix64 mixing of key seeds, purposes and nonces (public domain separators) */
 static inline u64 mix64(u64 z) {
     z += 0x9E3779B97F4A7C15ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -168,7 +216,6 @@ static inline u64 mix64(u64 z) {
     return z ^ (z >> 31);
 }
 static inline u64 derive(u64 a, u64 b) { return mix64(a ^ mix64(b)); }
-static inline u64 rnd(u64 key, u64 idx) { return mix64(key ^ (idx * 0xD1B54A32D192ED03ULL)); }
 static inline i64 ternary(u64 r) {
     u64 t = r % 3;
     return t == 0 ? 0 : (t == 1 ? 1 : -1);
@@ -191,6 +238,7 @@ struct aesfhe_engine {
     u64 ninv[MAXP], ninvp[MAXP];
     u64 iroot[MAXP]; /* psi^{N/2}: a square root of -1 */
     u64 seed;
+    uint32_t ck[8]; /* ChaCha20 key of every random stream */
     int threads;
     int profiling;
     double prof_ms[3];
@@ -408,6 +456,13 @@ int aesfhe_engine_create(const aesfhe_params *pp, aesfhe_engine **out) {
     e->np = e->L + 1 + e->K;
     e->dnum = (e->L + 1 + e->K - 1) / e->K;
     e->seed = pp->seed;
+    {
+        const u64 w[4] = {pp->seed, pp->seed_ext[0], pp->seed_ext[1], pp->seed_ext[2]};
+        for (int i = 0; i < 4; i++) {
+            e->ck[2 * i] = (uint32_t)w[i];
+            e->ck[2 * i + 1] = (uint32_t)(w[i] >> 32);
+        }
+    }
     e->threads = pp->threads;
 #ifdef _OPENMP
     /* per-engine thread count (num_threads on every parallel loop): never the process-wide
@@ -724,7 +779,7 @@ int aesfhe_key_secret(aesfhe_engine *e, uint64_t seed, aesfhe_key **out) {
     k->data = malloc(sizeof(u64) * (size_t)e->np * e->N);
     i64 *s = malloc(sizeof(i64) * e->N);
     u64 key = derive(k->keyseed, 1);
-    for (int i = 0; i < e->N; i++) s[i] = ternary(rnd(key, (u64)i));
+    for (int i = 0; i < e->N; i++) s[i] = ternary(rnd(e->ck, key, (u64)i));
 #pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int p = 0; p < e->np; p++) coeffs_to_ntt(e, s, k->data + (size_t)p * e->N, p);
     free(s);
@@ -741,7 +796,7 @@ int aesfhe_key_public(aesfhe_engine *e, const aesfhe_key *sk, aesfhe_key **out) 
     k->data = malloc(sizeof(u64) * 2 * (size_t)nq * N);
     u64 ka = derive(sk->keyseed, 2), ke = derive(sk->keyseed, 3);
     i64 *ee = malloc(sizeof(i64) * N);
-    for (int i = 0; i < N; i++) ee[i] = cbd21(rnd(ke, (u64)i));
+    for (int i = 0; i < N; i++) ee[i] = cbd21(rnd(e->ck, ke, (u64)i));
 #pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int p = 0; p < nq; p++) {
         u64 *b = k->data + (size_t)p * N, *a = k->data + ((size_t)nq + p) * N;
@@ -750,7 +805,7 @@ int aesfhe_key_public(aesfhe_engine *e, const aesfhe_key *sk, aesfhe_key **out) 
         u64 *et = malloc(sizeof(u64) * N);
         coeffs_to_ntt(e, ee, et, p);
         for (int j = 0; j < N; j++) {
-            a[j] = uniform_mod(rnd(ka, (u64)p * N + j), q);
+            a[j] = uniform_mod(rnd(e->ck, ka, (u64)p * N + j), q);
             b[j] = add_mod(sub_mod(0, mul_mod(a[j], s[j], &e->mont[p]), q), et[j], q);
         }
         free(et);
@@ -794,7 +849,7 @@ static aesfhe_key *make_ksk_t(aesfhe_engine *e, const u64 *starget, u64 keyseed,
     for (int d = 0; d < e->dnum; d++) {
         u64 ka = derive(base, 2 * (u64)d), ke = derive(base, 2 * (u64)d + 1);
         i64 *ee = malloc(sizeof(i64) * N);
-        for (int i = 0; i < N; i++) ee[i] = cbd21(rnd(ke, (u64)i));
+        for (int i = 0; i < N; i++) ee[i] = cbd21(rnd(e->ck, ke, (u64)i));
         int lo = d * e->K, hi = lo + e->K; /* digit primes [lo, hi) intersect [0, nq) */
 #pragma omp parallel for schedule(static) num_threads(e->threads)
         for (int p = 0; p < np; p++) {
@@ -806,7 +861,7 @@ static aesfhe_key *make_ksk_t(aesfhe_engine *e, const u64 *starget, u64 keyseed,
             coeffs_to_ntt(e, ee, et, p);
             int indigit = (p < nq) && p >= lo && p < hi;
             for (int j = 0; j < N; j++) {
-                a[j] = uniform_mod(rnd(ka, (u64)p * N + j), q);
+                a[j] = uniform_mod(rnd(e->ck, ka, (u64)p * N + j), q);
                 u64 v = add_mod(sub_mod(0, mul_mod(a[j], s[j], &e->mont[p]), q), et[j], q);
                 if (indigit)
                     v = add_mod(v, mul_mod(Pmod[p], sprime[(size_t)p * N + j], &e->mont[p]), q);
@@ -846,11 +901,11 @@ int aesfhe_key_secret_sparse(aesfhe_engine *e, uint64_t seed, int32_t hw, aesfhe
     for (int i = 0; i < N; i++) idx[i] = i;
     const u64 key = derive(k->keyseed, 9);
     for (int i = 0; i < hw; i++) {
-        const int j = i + (int)(rnd(key, (u64)i) % (u64)(N - i));
+        const int j = i + (int)(rnd(e->ck, key, (u64)i) % (u64)(N - i));
         const int t = idx[i];
         idx[i] = idx[j];
         idx[j] = t;
-        s[idx[i]] = (rnd(key, (u64)N + i) & 1) ? -1 : 1;
+        s[idx[i]] = (rnd(e->ck, key, (u64)N + i) & 1) ? -1 : 1;
     }
 #pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int p = 0; p < e->np; p++) coeffs_to_ntt(e, s, k->data + (size_t)p * N, p);
@@ -909,11 +964,9 @@ int aesfhe_encrypt(aesfhe_engine *e, const aesfhe_key *key, const int64_t *co, i
         u64 k0 = derive(base, 3 * (u64)b), k1 = derive(base, 3 * (u64)b + 1),
             k2 = derive(base, 3 * (u64)b + 2);
         i64 *v = malloc(sizeof(i64) * N), *e0 = malloc(sizeof(i64) * N), *e1 = malloc(sizeof(i64) * N);
-        for (int i = 0; i < N; i++) {
-            v[i] = ternary(rnd(k0, (u64)i));
-            e0[i] = cbd21(rnd(k1, (u64)i));
-            e1[i] = cbd21(rnd(k2, (u64)i));
-        }
+        for (int i = 0; i < N; i++) v[i] = ternary(rnd(e->ck, k0, (u64)i));  /* one stream per loop: */
+        for (int i = 0; i < N; i++) e0[i] = cbd21(rnd(e->ck, k1, (u64)i));   /* the block cache     */
+        for (int i = 0; i < N; i++) e1[i] = cbd21(rnd(e->ck, k2, (u64)i));   /* serves 7 of 8 words */
         const i64 *m = co + (size_t)b * N;
 #pragma omp parallel for schedule(static) num_threads(e->threads)
         for (int p = 0; p <= level; p++) {
@@ -936,7 +989,7 @@ int aesfhe_encrypt(aesfhe_engine *e, const aesfhe_key *key, const int64_t *co, i
             } else {
                 const u64 *s = key->data + (size_t)p * N;
                 for (int j = 0; j < N; j++) {
-                    u64 a = uniform_mod(rnd(k0, (u64)p * N + j), q);
+                    u64 a = uniform_mod(rnd(e->ck, k0, (u64)p * N + j), q);
                     c1[j] = a;
                     c0[j] = add_mod(add_mod(sub_mod(0, mul_mod(a, s[j], &e->mont[p]), q), te[j], q), tm[j], q);
                 }

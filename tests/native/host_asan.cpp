@@ -9,7 +9,30 @@
 
 using namespace aesfhe;
 
+// RFC 7539 section 2.3.2 block-function vector: key 00..1f, block count 1, nonce 00 00 00 09 00 00
+// 00 4a 00 00 00 00 -- in this 64-bit counter / 64-bit nonce layout: ctr = 1 | 0x09000000 << 32,
+// label = 0x4a000000.
+static int chacha_kat() {
+    ChaKey K;
+    for (int i = 0; i < 8; i++)
+        K.k[i] = (uint32_t)(4 * i) | (uint32_t)(4 * i + 1) << 8 | (uint32_t)(4 * i + 2) << 16 | (uint32_t)(4 * i + 3) << 24;
+    const uint32_t want[16] = {0xe4e7f110, 0x15593bd1, 0x1fdd0f50, 0xc47120a3, 0xc7f4d1c7, 0x0368c033,
+                               0x9aaa2204, 0x4e6cd4c3, 0x466482d2, 0x09aa9f07, 0x05d7c214, 0xa2028bd9,
+                               0xd19c12b5, 0xb94e16de, 0xe883d0cb, 0x4e3c50a2};
+    uint32_t o[16];
+    chacha20_block(K, 0x4a000000ULL, 1ULL | (0x09000000ULL << 32), o);
+    for (int i = 0; i < 16; i++)
+        if (o[i] != want[i]) return 1;
+    // rnd: word idx mod 8 of block idx / 8
+    const u64 r = rnd(K, 0x4a000000ULL, ((1ULL | (0x09000000ULL << 32)) << 3) + 2);
+    return r == ((u64)want[4] | (u64)want[5] << 32) ? 0 : 2;
+}
+
 int main() {
+    if (int rc = chacha_kat()) {
+        std::printf("chacha20 KAT failed (%d)\n", rc);
+        return 10 + rc;
+    }
     for (int logN = 10; logN <= 17; logN++) {
         const int N = 1 << logN, L = logN >= 16 ? 30 : 8, K = logN >= 16 ? 10 : 3;
         Chain c = make_chain(logN, L, K, 50, 50, 40);

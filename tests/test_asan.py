@@ -28,3 +28,14 @@ def test_host_codec_asan(tmp_path):
                     str(ROOT / "tests" / "native" / "host_asan.cpp")], check=True)
     r = subprocess.run([str(exe)], env=ENV, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "host_asan ok" in r.stdout, r.stderr[-4000:]
+
+
+def test_oracle_chacha_kat(tmp_path):
+    """The oracle's ChaCha20 stream against RFC 7539's block vector; the engine's
+    host copy is checked in host_asan.cpp, and GPU-vs-oracle key equality (test_gpu_parity) ties
+    the device kernels to both."""
+    exe = tmp_path / "chacha_kat"
+    subprocess.run(["gcc", "-std=gnu11", "-O1", "-fopenmp", "-fsanitize=address,undefined", "-o", str(exe),
+                    str(ROOT / "tests" / "native" / "oracle_chacha_kat.c"), "-lm"], check=True)
+    r = subprocess.run([str(exe)], env=ENV, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "oracle chacha ok" in r.stdout, (r.returncode, r.stderr[-2000:])
