@@ -79,108 +79,133 @@ extern "C" const char* aesfhe_backend_name(void) { return "hip-gfx950"; }
 // -----------------------------------------------------------------------------------------------
 // engine state
 struct Pool {
-    // Size classes: exact (256 B granularity) up to 1 MiB, then 8 classes per octave (<= 12.5%
-    // slack), so ciphertexts of neighbouring levels / batch sizes share blocks.  A failed
-    // hipMalloc first takes a cached block of up to twice the class, then frees the cached blocks
-    // of the least recently used classes (one device sync) until the allocation fits: the sizes
-    // of a finished phase (bootstrapping's Q u P buffers during the rounds, the rounds' during a
-    // refresh) go first, the working set stays cached.  A soft cap (95 % of the device memory
-    // free at engine creation) keeps the device out of failing hipMallocs, which are slow.
-    std::map<size_t, std::vector<void*>> free_;
-    std::unordered_map<void*, size_t> cls_;  // live block -> its class
-    std::unordered_map<size_t, uint64_t> used_;  // class -> last get/put tick
-    uint64_t tick = 0;
+    // Chunked best-fit arena.  Device memory is taken from HIP in large chunks (default 16384
+    // limbs, i.e. 8 GiB at N = 2^16; a larger request gets a chunk of its own) and carved by
+    // best fit with 256-B granularity; a freed block merges with its free neighbours of the same
+    // chunk.  Every size shares every chunk, so the memory held tracks the peak live set plus
+    // fragmentation instead of the sum of per-size-class peaks (the size-class pool this replaces
+    // held 250 GB for 64 GB live in the bench round and thrashed -- hipFree / hipMalloc + device
+    // syncs inside the timed region -- on the N = 2^17 ten-round run).  All work is enqueued on
+    // the engine's one stream, so a block freed by the host is reused only by later stream-ordered
+    // work (as before).  trim() returns the chunks that hold no live block.
+    static constexpr size_t kAlign = 256;
+    size_t chunk_bytes = (size_t)1 << 33;
+    std::map<char*, size_t> chunks_;                  // base -> size
+    std::map<char*, size_t> free_addr_;               // free block -> size (address order)
+    std::multimap<size_t, char*> free_size_;          // size -> free block (best fit)
+    std::unordered_map<void*, size_t> live_;          // live block -> size
     size_t held = 0, live = 0;
-    int64_t mallocs = 0, trims = 0, reuse_larger = 0;
-    static size_t size_class(size_t b) {
-        b = (b + 255) & ~(size_t)255;
-        if (b <= ((size_t)1 << 20)) return b;
-        const int lg = 63 - __builtin_clzll(b);
-        const size_t step = (size_t)1 << (lg - 3);
-        return (b + step - 1) & ~(step - 1);
+    int64_t mallocs = 0, trims = 0, reuse_larger = 0;  // reuse_larger: blocks split off a larger free one
+    size_t cap = 0;  // unused (kept for the stats ABI); chunk allocation failures are handled below
+    void add_free(char* p, size_t n) {
+        free_addr_[p] = n;
+        free_size_.insert({n, p});
     }
-    void* take(std::map<size_t, std::vector<void*>>::iterator it) {
-        void* p = it->second.back();
-        it->second.pop_back();
-        cls_[p] = it->first;
-        live += it->first;
-        used_[it->first] = ++tick;
-        return p;
-    }
-    size_t cap = 0;  // soft limit on held bytes (0: none); set from the device size at creation
-    // free the cached blocks of the least recently used classes (one device sync) until held +
-    // need <= target or nothing is cached; returns whether anything was freed
-    bool trim_lru(size_t need, size_t target) {
-        std::vector<std::pair<uint64_t, size_t>> order;  // (last use, class) of cached classes
-        for (auto& kv : free_)
-            if (!kv.second.empty()) order.push_back({used_[kv.first], kv.first});
-        if (order.empty()) return false;
-        std::sort(order.begin(), order.end());
-        hipDeviceSynchronize();
-        trims++;
-        for (size_t k = 0; k < order.size() && held + need > target; k++) {
-            auto& v = free_[order[k].second];
-            for (void* q : v) {
-                hipFree(q);
-                held -= order[k].second;
+    void del_free(char* p, size_t n) {
+        free_addr_.erase(p);
+        auto r = free_size_.equal_range(n);
+        for (auto it = r.first; it != r.second; ++it)
+            if (it->second == p) {
+                free_size_.erase(it);
+                return;
             }
-            v.clear();
+    }
+    char* chunk_of(char* p) {
+        auto it = chunks_.upper_bound(p);
+        return it == chunks_.begin() ? nullptr : std::prev(it)->first;
+    }
+    bool new_chunk(size_t need) {
+        size_t want = std::max(chunk_bytes, need);
+        void* p = nullptr;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess && want > need) {  // nearly full: release empty chunks, then the exact need
+            (void)hipGetLastError();
+            trim();
+            want = need;
+            e = hipMalloc(&p, want);
         }
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        mallocs++;
+        held += want;
+        chunks_[(char*)p] = want;
+        add_free((char*)p, want);
         return true;
     }
     void* get(size_t bytes) {
-        const size_t c = size_class(bytes);
-        auto it = free_.find(c);
-        if (it != free_.end() && !it->second.empty()) return take(it);
-        // a cached block of a slightly larger class (<= 25 % waste) before a new allocation: the
-        // sum of per-class peaks otherwise grows far past the peak live set
-        for (auto j = free_.upper_bound(c); j != free_.end() && j->first <= c + c / 4; ++j)
-            if (!j->second.empty()) { reuse_larger++; return take(j); }
-        void* p = nullptr;
-        hipError_t e = hipErrorOutOfMemory;
-        // near the soft cap a new block would only push the device into failing hipMallocs (slow
-        // under ROCm): reuse a cached block of up to twice the class, else release LRU classes
-        // down to 80 % of the cap in one go
-        if (cap && held + c > cap) {
-            for (auto j = free_.lower_bound(c); j != free_.end() && j->first <= 2 * c; ++j)
-                if (!j->second.empty()) { reuse_larger++; return take(j); }
-            trim_lru(c, cap / 5 * 4);
+        const size_t n = std::max(kAlign, (bytes + kAlign - 1) & ~(kAlign - 1));
+        auto it = free_size_.lower_bound(n);
+        if (it == free_size_.end()) {
+            if (!new_chunk(n)) throw_err(AESFHE_ENOMEM, "device allocation of %zu bytes failed (%zu held, %zu live)", n, held, live);
+            it = free_size_.lower_bound(n);
         }
-        e = hipMalloc(&p, c);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            for (auto j = free_.lower_bound(c); j != free_.end() && j->first <= 2 * c; ++j)
-                if (!j->second.empty()) { reuse_larger++; return take(j); }
-            while (e != hipSuccess && trim_lru(c, held > c ? held - c : 0)) {
-                e = hipMalloc(&p, c);
-                if (e != hipSuccess) (void)hipGetLastError();
-            }
-            if (e != hipSuccess) throw_err(AESFHE_ENOMEM, "hipMalloc(%zu) failed", c);
+        char* p = it->second;
+        const size_t have = it->first;
+        free_size_.erase(it);
+        free_addr_.erase(p);
+        if (have > n) {
+            add_free(p + n, have - n);
+            reuse_larger++;
         }
-        mallocs++;
-        held += c;
-        live += c;
-        cls_[p] = c;
-        used_[c] = ++tick;
+        live_[p] = n;
+        live += n;
         return p;
     }
-    void put(void* p, size_t) {
-        if (!p) return;
-        auto it = cls_.find(p);
-        if (it == cls_.end()) return;
-        free_[it->second].push_back(p);
-        live -= it->second;
-        used_[it->second] = ++tick;
-        cls_.erase(it);
+    void put(void* vp, size_t) {
+        if (!vp) return;
+        auto lt = live_.find(vp);
+        if (lt == live_.end()) return;
+        char* p = (char*)vp;
+        size_t n = lt->second;
+        live_.erase(lt);
+        live -= n;
+        char* ch = chunk_of(p);
+        // merge with the free block after p, then with the one before (same chunk only)
+        auto nx = free_addr_.find(p + n);
+        if (nx != free_addr_.end() && chunk_of(nx->first) == ch) {
+            const size_t m = nx->second;
+            del_free(p + n, m);
+            n += m;
+        }
+        auto pv = free_addr_.lower_bound(p);
+        if (pv != free_addr_.begin()) {
+            --pv;
+            if (pv->first + pv->second == p && chunk_of(pv->first) == ch) {
+                char* q = pv->first;
+                const size_t m = pv->second;
+                del_free(q, m);
+                p = q;
+                n += m;
+            }
+        }
+        add_free(p, n);
     }
+    // return every chunk without a live block to HIP (one device sync)
     void trim() {
         hipDeviceSynchronize();
-        for (auto& kv : free_)
-            for (void* p : kv.second) {
-                hipFree(p);
-                held -= kv.first;
+        trims++;
+        for (auto it = chunks_.begin(); it != chunks_.end();) {
+            auto f = free_addr_.find(it->first);
+            if (f != free_addr_.end() && f->second == it->second) {
+                del_free(it->first, it->second);
+                hipFree(it->first);
+                held -= it->second;
+                it = chunks_.erase(it);
+            } else {
+                ++it;
             }
-        free_.clear();
+        }
+    }
+    void release_all() {  // engine teardown: no live block remains
+        hipDeviceSynchronize();
+        for (auto& kv : chunks_) hipFree(kv.first);
+        chunks_.clear();
+        free_addr_.clear();
+        free_size_.clear();
+        live_.clear();
+        held = live = 0;
     }
 };
 
@@ -746,12 +771,8 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
     HIPC(hipSetDevice(e->device));
     HIPC(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     build_tables(e.get());
-    {
-        size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess) e->pool.cap = fr / 100 * 95;
-        const char* cs = getenv("AESFHE_POOL_CAP_GB");  // override (tests / several engines per device)
-        if (cs) e->pool.cap = (size_t)(atof(cs) * 1e9);
-    }
+    // arena chunks of 16384 limbs (8 GiB at N = 2^16), at least 256 MiB
+    e->pool.chunk_bytes = std::max((size_t)1 << 28, ((size_t)16384 * 8) << e->logN);
     HIPC(hipMalloc(&e->ring_d, e->ring_size));
     HIPC(hipHostMalloc((void**)&e->ring_h, e->ring_size, hipHostMallocDefault));
     *out = e.release();
@@ -781,7 +802,7 @@ static void engine_teardown(aesfhe_engine* e) {
         hipEventDestroy(r.b);
     }
     for (auto ev : e->spare) hipEventDestroy(ev);
-    e->pool.trim();
+    e->pool.release_all();
     void* ptrs[] = {e->q, e->psi, e->ipsi, e->ninv, e->qinv, e->psif, e->ipsif, e->ninvf, e->rtwf, e->irtwf,
                     e->mu_hatinv, e->mu_hat, e->md_phatinv, e->md_phat, e->md_pinv, e->rs_inv,
                     e->rs_mod, e->pmod, e->mu_hatinvf, e->mu_hatf, e->md_phatinvf, e->md_phatf,

@@ -80,17 +80,18 @@ constexpr int kPadF = 17;  // LDS row stride (8 B words) of the 16 x 16 transpos
 // 256 rows) pairs the two 256-row halves in registers; each half is then an independent
 // 256-point column transform whose stage-m twiddles sit at m (2 + h) + group (half h, group
 // within the half), so the R = 256 code runs on each half with the index multiplier 2 + h.
-template <int R = 256>
-__global__ __launch_bounds__(256) void k_nttf_fwd_cols(Span src, Span dst, Tabs T) {
+// (the body takes the 16-column block bx of span limb by and LDS s[256 * kPadF], twq[R]; a
+// caller that loops over blocks separates them with a workgroup barrier)
+template <int R>
+__device__ __forceinline__ void nttf_fwd_cols_body(const Span& src, const Span& dst, const Tabs& T, int bx, int by,
+                                                   double* s, double* twq) {
     static_assert(R == 256 || R == 512, "rows of 256: N = 2^16 or 2^17");
     constexpr int H = R / 256;
-    __shared__ double s[256 * kPadF];
-    __shared__ double twq[R];
     int pid;
-    const u64* in = span_ptr(src, blockIdx.y, T.logN, T.Lp1, pid);
-    u64* out = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
+    const u64* in = span_ptr(src, by, T.logN, T.Lp1, pid);
+    u64* out = span_ptr(dst, by, T.logN, T.Lp1, pid);
     const int tid = threadIdx.x, cl = tid & 15, b = tid >> 4;
-    const int c = blockIdx.x * 16 + cl;
+    const int c = bx * 16 + cl;
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* tg = T.psif + ((long)pid << T.logN);
@@ -147,6 +148,12 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_cols(Span src, Span dst, Tabs 
 #pragma unroll
         for (int bb = 0; bb < 16; bb++) st_d(&out[(h * 256 + ap * 16 + bb) * 256 + c], xh[bb]);
     }
+}
+template <int R = 256>
+__global__ __launch_bounds__(256) void k_nttf_fwd_cols(Span src, Span dst, Tabs T) {
+    __shared__ double s[256 * kPadF];
+    __shared__ double twq[R];
+    nttf_fwd_cols_body<R>(src, dst, T, blockIdx.x, blockIdx.y, s, twq);
 }
 
 // ModDown finish fused into the row pass of the conv NTT (key switch): limb y of
@@ -221,13 +228,14 @@ __device__ __forceinline__ int row_tile_idx(int e) {
 // Forward, row pass: stages m = 256..32768 within rows of 256 contiguous elements; raw doubles
 // in, canonical u64 out (FIN: the ModDown finish above).  Workgroup = 16 rows [r0, r0+16);
 // lane (b, rl) = (tid & 15, tid >> 4).
-template <bool FIN, int R = 256>
-__global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFin fin) {
-    __shared__ double s[16 * 16 * kPadF];
+// (body: the 16-row block bx of span limb by, LDS s[16 * 16 * kPadF])
+template <bool FIN, int R>
+__device__ __forceinline__ void nttf_fwd_rows_body(const Span& dst, const Tabs& T, const RowFin& fin, int bx, int by,
+                                                   double* s) {
     int pid;
-    u64* io = span_ptr(dst, blockIdx.y, T.logN, T.Lp1, pid);
+    u64* io = span_ptr(dst, by, T.logN, T.Lp1, pid);
     const int tid = threadIdx.x, b = tid & 15, rl = tid >> 4;
-    const int row = blockIdx.x * 16 + rl;
+    const int row = bx * 16 + rl;
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* W = T.psif + ((long)pid << T.logN);
@@ -241,15 +249,15 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
     for (int bb = 0; bb < 16; bb++) sr[ap * kPadF + bb] = __longlong_as_double((long long)fcanon(x[bb], q, qi));
     __syncthreads();
     if (!FIN) {
-        u64* base = io + (long)blockIdx.x * 16 * 256;
+        u64* base = io + (long)bx * 16 * 256;
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
             __builtin_nontemporal_store((u64)__double_as_longlong(s[row_tile_idx(e)]), &base[e]);
         }
     } else {
-        const int y = blockIdx.y, p = y / fin.nl, i = y - p * fin.nl, bb = p >> 1, c = p & 1;
-        const long off = ((long)i << T.logN) + (long)blockIdx.x * 16 * 256;
+        const int y = by, p = y / fin.nl, i = y - p * fin.nl, bb = p >> 1, c = p & 1;
+        const long off = ((long)i << T.logN) + (long)bx * 16 * 256;
         const u64* ap = fin.acc + (long)bb * fin.abs_ + (long)c * fin.acs + off;
         const u64* dp = fin.addend.ptr && c < fin.addend.np ? fin.addend.ptr + (long)bb * fin.addend.bs + (long)c * fin.addend.ps + off : nullptr;
         u64* op = fin.out + (long)bb * fin.obs + (long)c * fin.ops + off;
@@ -263,6 +271,11 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
             __builtin_nontemporal_store(fcanon(v, q, qi), &op[e]);  // streaming
         }
     }
+}
+template <bool FIN, int R = 256>
+__global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFin fin) {
+    __shared__ double s[16 * 16 * kPadF];
+    nttf_fwd_rows_body<FIN, R>(dst, T, fin, blockIdx.x, blockIdx.y, s);
 }
 
 // Inverse, row pass (Gentleman-Sande, distances 1..128 within rows): canonical u64 in (src),
