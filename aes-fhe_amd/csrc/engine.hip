@@ -964,7 +964,7 @@ static aesfhe_key* key_new(aesfhe_engine* e, int kind, size_t words) {
 static void sample_small_ntt(aesfhe_engine* e, u64* dst, int nprimes, u64 key, int kind) {
     Span s = span_s(dst, 0, nprimes, std::min(nprimes, e->Lp1), 0, e->Lp1);
     s.pstride = (long)nprimes * e->N;
-    hipLaunchKernelGGL(k_sample_small, dim3(e->N / 256, nprimes), dim3(256), 0, e->stream, s, e->ck, key, kind, e->q, e->logN, e->Lp1);
+    hipLaunchKernelGGL(k_sample_small, dim3((e->N / 8 + 255) / 256), dim3(256), 0, e->stream, s, e->ck, key, kind, e->q, e->logN, e->Lp1, nprimes);
     ntt(e, s, s, nprimes, false);
 }
 
@@ -986,7 +986,7 @@ extern "C" int aesfhe_key_public(aesfhe_engine* e, const aesfhe_key* sk, aesfhe_
     u64* b = k->d;
     u64* a = k->d + (size_t)nq * N;
     Span sa = span_s(a, 0, nq, nq, 0, e->Lp1);
-    hipLaunchKernelGGL(k_sample_uniform, dim3(N / 256, nq), dim3(256), 0, e->stream, sa, e->ck, derive(sk->keyseed, 2), e->q, e->logN, e->Lp1);
+    hipLaunchKernelGGL(k_sample_uniform, dim3((N / 8 + 255) / 256, nq), dim3(256), 0, e->stream, sa, e->ck, derive(sk->keyseed, 2), e->q, e->logN, e->Lp1);
     Tmp et(e, (size_t)nq * N);
     sample_small_ntt(e, et.p, nq, derive(sk->keyseed, 3), 1);
     hipLaunchKernelGGL(k_key_combine, dim3(N / 256, nq), dim3(256), 0, e->stream, a, sk->d, et.p, (const u64*)nullptr, (const u64*)nullptr, 0, 0, b, e->q, e->qinv, e->logN);
@@ -1010,7 +1010,7 @@ static aesfhe_key* make_ksk_t(aesfhe_engine* e, const u64* starget, u64 keyseed,
         u64* kb = k->d + ((size_t)d * 2 + 0) * np * N;
         u64* ka = k->d + ((size_t)d * 2 + 1) * np * N;
         Span sa = span_s(ka, 0, np, e->Lp1, 0, e->Lp1);
-        hipLaunchKernelGGL(k_sample_uniform, dim3(N / 256, np), dim3(256), 0, e->stream, sa, e->ck, derive(base, 2 * (u64)d), e->q, e->logN, e->Lp1);
+        hipLaunchKernelGGL(k_sample_uniform, dim3((N / 8 + 255) / 256, np), dim3(256), 0, e->stream, sa, e->ck, derive(base, 2 * (u64)d), e->q, e->logN, e->Lp1);
         sample_small_ntt(e, et.p, np, derive(base, 2 * (u64)d + 1), 1);
         int lo = d * e->K, hi = std::min(lo + e->K, e->Lp1);
         hipLaunchKernelGGL(k_key_combine, dim3(N / 256, np), dim3(256), 0, e->stream, (const u64*)ka, starget, et.p, sprime, e->pmod, lo, hi, kb, e->q, e->qinv, e->logN);
@@ -1307,10 +1307,10 @@ extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int
         u64* vb = vem.p + (size_t)b * 4 * step;
         Span sv = span_s(vb, 0, nl, nl, 0, e->Lp1), se0 = span_s(vb + step, 0, nl, nl, 0, e->Lp1), se1 = span_s(vb + 2 * step, 0, nl, nl, 0, e->Lp1);
         if (key->kind == 1)
-            hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, sv, e->ck, k0, 0, e->q, e->logN, e->Lp1);
-        hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, se0, e->ck, k1, 1, e->q, e->logN, e->Lp1);
+            hipLaunchKernelGGL(k_sample_small, dim3((N / 8 + 255) / 256), dim3(256), 0, e->stream, sv, e->ck, k0, 0, e->q, e->logN, e->Lp1, nl);
+        hipLaunchKernelGGL(k_sample_small, dim3((N / 8 + 255) / 256), dim3(256), 0, e->stream, se0, e->ck, k1, 1, e->q, e->logN, e->Lp1, nl);
         if (key->kind == 1)
-            hipLaunchKernelGGL(k_sample_small, dim3(N / 256, nl), dim3(256), 0, e->stream, se1, e->ck, k2, 1, e->q, e->logN, e->Lp1);
+            hipLaunchKernelGGL(k_sample_small, dim3((N / 8 + 255) / 256), dim3(256), 0, e->stream, se1, e->ck, k2, 1, e->q, e->logN, e->Lp1, nl);
         hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, nl, 1), dim3(256), 0, e->stream, (const i64*)(dco.p + (size_t)b * N), vb + 3 * step, nl, e->q, e->logN);
     }
     // NTT everything: B * 4 groups of nl limbs (pid = limb index)
@@ -1322,7 +1322,7 @@ extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int
         hipLaunchKernelGGL(k_enc_pk, dim3(N / 256, nl, B), dim3(256), 0, e->stream, (const u64*)vem.p, pk0, pk1, c->d, nl, e->q, e->qinv, e->logN);
     } else {
         u64* dk = upload_small(e, k0s.data(), k0s.size());
-        hipLaunchKernelGGL(k_enc_sk, dim3(N / 256, nl, B), dim3(256), 0, e->stream, (const u64*)vem.p, (const u64*)key->d, c->d, nl, e->q, e->qinv, e->ck, (const u64*)dk, e->logN);
+        hipLaunchKernelGGL(k_enc_sk, dim3((N / 8 + 255) / 256, nl, B), dim3(256), 0, e->stream, (const u64*)vem.p, (const u64*)key->d, c->d, nl, e->q, e->qinv, e->ck, (const u64*)dk, e->logN);
     }
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(e->stream));  // host coefficient buffer may be reused by caller
@@ -2623,11 +2623,20 @@ extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, in
     for (int j = 0; j < ny - 1; j++)
         if (yb[j]->B != B && yb[j]->B != 1) throw_err(AESFHE_EARG, "batch mismatch");
     if (l < 2) throw_err(AESFHE_ELEVEL, "no level left for a bivariate polynomial");
+    // wfac bounds an inner sum a = w_0 c0 + sum_j w_j y'_j (c0 < q, |y'| <= q/2 + 1) by wfac * q:
+    // a limb takes the exact-FMA kernel (no folds) when wfac * q < 2^52, else the folding one
+    double wfac = 1.0;
     for (int t = 0; t < m; t++)
         for (int i = 0; i < nx; i++) {
             long sum = 0;
-            for (int j = 0; j < ny; j++) sum += std::labs((long)w[((size_t)t * nx + i) * ny + j]);
+            double f = 0.0;
+            for (int j = 0; j < ny; j++) {
+                const long a = std::labs((long)w[((size_t)t * nx + i) * ny + j]);
+                sum += a;
+                f += j == 0 ? (double)a : 0.5 * (double)a + 1e-3 * (double)a;
+            }
             if (sum > 512) throw_err(AESFHE_EARG, "poly2_int: sum of |w| over a row exceeds 512");
+            wfac = std::max(wfac, f);
         }
     const int nl = l + 1, N = e->N;
     const double* D = e->chain.scale.data();
@@ -2727,10 +2736,15 @@ extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, in
             ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml));
             constexpr int mo = 4;  // outputs per launch (8: 219 VGPRs, 2 waves, measured slower)
             for (int t0 = 0; t0 < ml; t0 += mo)
-                for (int la = 0; la < nl;) {  // runs of limbs of one prime-size class
-                    const bool big = e->chain.q[la] >= (1ULL << 42);
+                for (int la = 0; la < nl;) {  // runs of limbs of one kernel class
+                    // a < 2^52 and the unfolded tensor sums (a + 2 (nx - 1) products of <= 1.5 q) < 2^53
+                    auto is_big = [&](int li) {
+                        const double q = (double)e->chain.q[li];
+                        return wfac * q >= 0x1p52 * 0.999 || (wfac + 3.0 * nx) * q >= 0x1p53 * 0.999;
+                    };
+                    const bool big = is_big(la);
                     int lb = la + 1;
-                    while (lb < nl && (e->chain.q[lb] >= (1ULL << 42)) == big) lb++;
+                    while (lb < nl && is_big(lb) == big) lb++;
                     auto kern = big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max, mo> : k_poly2_int<true, 0, mo>)
                                     : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max, mo> : k_poly2_int<false, 0, mo>);
                     hipLaunchKernelGGL(kern, dim3(N / 256, lb - la, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny,

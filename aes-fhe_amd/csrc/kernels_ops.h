@@ -581,25 +581,53 @@ __global__ void k_galois(Span src, Span dst, u64 g, int logN, int Lp1) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// sampling.  Uniform residues directly in the NTT domain, index pid*N + k.
+// sampling.  Uniform residues directly in the NTT domain, index pid*N + k.  A
+// thread draws one ChaCha20 block = the 8 words of k = 8t .. 8t + 7.  grid (ceil(N / 2048), limbs)
 __global__ void k_sample_uniform(Span dst, ChaKey K, u64 key, const u64* __restrict__ qall, int logN,
                                  int Lp1) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int k0 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (k0 >= (1 << logN)) return;
     int pid;
     u64* out = span_ptr(dst, blockIdx.y, logN, Lp1, pid);
-    out[k] = __umul64hi(rnd(K, key, ((u64)pid << logN) + k), qall[pid]);
+    uint32_t o[16];
+    chacha20_block(K, key, (((u64)pid << logN) + k0) >> 3, o);
+    const u64 q = qall[pid];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+        ulonglong2 v;
+        v.x = __umul64hi((u64)o[2 * e] | ((u64)o[2 * e + 1] << 32), q);
+        v.y = __umul64hi((u64)o[2 * e + 2] | ((u64)o[2 * e + 3] << 32), q);
+        *(ulonglong2*)&out[k0 + e] = v;
+    }
 }
 
-// small coefficient polynomial (kind 0 ternary, 1 CBD-21) -> residues of every limb (coef form)
+// small coefficient polynomial (kind 0 ternary, 1 CBD-21) -> residues of the span's limbs 0..nlim-1
+// (coefficient form): one ChaCha20 block per thread (8 coefficients), written to every limb.
+// grid ceil(N / 2048)
 __global__ void k_sample_small(Span dst, ChaKey K, u64 key, int kind, const u64* __restrict__ qall,
-                               int logN, int Lp1) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    int pid;
-    u64* out = span_ptr(dst, blockIdx.y, logN, Lp1, pid);
-    const u64 r = rnd(K, key, (u64)k);
-    const i64 v = kind == 0 ? ternary(r) : cbd21(r);
-    const u64 q = qall[pid];
-    out[k] = v >= 0 ? (u64)v : q - (u64)(-v);
+                               int logN, int Lp1, int nlim) {
+    const int k0 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (k0 >= (1 << logN)) return;
+    uint32_t o[16];
+    chacha20_block(K, key, (u64)k0 >> 3, o);
+    i64 v[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        const u64 r = (u64)o[2 * e] | ((u64)o[2 * e + 1] << 32);
+        v[e] = kind == 0 ? ternary(r) : cbd21(r);
+    }
+    for (int y = 0; y < nlim; y++) {
+        int pid;
+        u64* out = span_ptr(dst, y, logN, Lp1, pid);
+        const u64 q = qall[pid];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+            ulonglong2 w;
+            w.x = v[e] >= 0 ? (u64)v[e] : q - (u64)(-v[e]);
+            w.y = v[e + 1] >= 0 ? (u64)v[e + 1] : q - (u64)(-v[e + 1]);
+            *(ulonglong2*)&out[k0 + e] = w;
+        }
+    }
 }
 
 // signed 64-bit coefficients (device copy of host input) -> residues ; grid (N/256, nl, B)
@@ -650,22 +678,29 @@ __global__ void k_enc_pk(const u64* __restrict__ vem, const u64* __restrict__ pk
     c[step] = add_m(mul_m(v, pk1[lo], q, qi), e1, q);
 }
 
-// secret-key encryption: c1 = a (uniform, NTT), c0 = -a s + e0 + m ; vem as above with v unused
+// secret-key encryption: c1 = a (uniform, NTT), c0 = -a s + e0 + m ; vem as above with v unused.
+// A thread takes 8 consecutive k (one ChaCha20 block of a).  grid (ceil(N / 2048), l+1, B)
 __global__ void k_enc_sk(const u64* __restrict__ vem, const u64* __restrict__ s,
                          u64* __restrict__ ct, int nl, const u64* __restrict__ qs,
                          const double* __restrict__ qinv, ChaKey K, const u64* __restrict__ keys, int logN) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int k0 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    if (k0 >= (1 << logN)) return;
     const int l = blockIdx.y, bb = blockIdx.z;
     const u64 q = qs[l];
     const double qi = qinv[l];
-    const long lo = ((long)l << logN) + k;
     const long step = (long)nl << logN;
-    const u64* base = vem + (long)bb * 4 * step + lo;
-    u64 e0 = base[step], m = base[3 * step];
-    u64 a = __umul64hi(rnd(K, keys[bb], ((u64)l << logN) + k), q);
-    u64* c = ct + (long)bb * 2 * step + lo;
-    c[step] = a;
-    c[0] = add_m(add_m(sub_m(0, mul_m(a, s[lo], q, qi), q), e0, q), m, q);
+    uint32_t o[16];
+    chacha20_block(K, keys[bb], (((u64)l << logN) + k0) >> 3, o);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        const long lo = ((long)l << logN) + k0 + e;
+        const u64* base = vem + (long)bb * 4 * step + lo;
+        const u64 e0 = base[step], m = base[3 * step];
+        const u64 a = __umul64hi((u64)o[2 * e] | ((u64)o[2 * e + 1] << 32), q);
+        u64* c = ct + (long)bb * 2 * step + lo;
+        c[step] = a;
+        c[0] = add_m(add_m(sub_m(0, mul_m(a, s[lo], q, qi), q), e0, q), m, q);
+    }
 }
 
 // limb-0 decryption combine: t[b][k] = c0 + c1 s (+ c2 s^2) ; grid (N/256, 1, B)
@@ -790,9 +825,10 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
 // The H factor lives on the y basis: y'_j = H(c, cy(j)) * y_j for the current x class c (x is
 // sorted by class; entering class c multiplies y' by Rt[c][cy(j)] = H(c,cy) H(c-1,cy)^{-1}, or
 // H(0,cy) for c = 0), so every inner sum is a_i = c0 * w_i0 + sum_j w_ij y'_j with small integer
-// weights: exact fp64 FMAs for primes below 2^42 (|a| <= (wsum+1) q < 2^52, host-checked), no
-// folding; the tensor accumulators stay below 2^49 without folding.  Larger primes (q_0) use
-// remainder products and fold.  Wt: [mtot][nx][ny] doubles (scalar loads), Rt: [nl][cxn][cyn]
+// weights: exact fp64 FMAs with no folding where |a| <= (|w_0| + sum_j |w_j| / 2) q < 2^52 (the host
+// picks the kernel per limb from the actual weights: every limb of a 40-44-bit chain for the AES
+// S-box's |64 W| <= 8), the tensor accumulators staying below 2^53.  Other limbs (the 50-bit q_0)
+// use remainder products and fold.  Wt: [mtot][nx][ny] doubles (scalar loads), Rt: [nl][cxn][cyn]
 // {w, w/q}, C0: [nl][cxn] = H(c, 0) as doubles, xstart[c]..xstart[c+1]: the i of class c.  BIG: the q >= 2^42 path; the host launches
 // each run of limbs of one size class (limbs l0 .. l0 + gridDim.y - 1 of nl).  grid (N/256, run, B)
 // NY > 0: ny fixed at compile time (the weight loads are then unconditional and issued together;

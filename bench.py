@@ -246,7 +246,7 @@ def config_legs(args, eng, drv):
         ok = None
         if args.check:
             ok = bool(np.array_equal(zeta_decode(eng.decrypt(res, sk), modulus=256), T.SBOX[x]))
-        c2[name] = {"value": round(2048 / t, 1), "unit": "blocks/s", "ms": round(t * 1e3, 2),
+        c2[name] = {"value": round(eng.slot_count / 16 / t, 1), "unit": "blocks/s", "ms": round(t * 1e3, 2),
                     "verified": ok, "level_drop": ct.level - res.level}
     out["config2_subbytes"] = c2
     # config 3: ShiftRows + MixColumns, byte-major Zeta-16 nibble pair (2048 blocks per ct)
@@ -351,9 +351,49 @@ def cpu_baseline(args):
                       f"{n_blk} blocks at N=2^{args.log_n}, L={args.max_level}, K={args.special_primes}: "
                       f"{t:.1f} s, FIPS-verified")}
     if args.cpu_extended:
+        log("cpu baseline: oracle round at 8 threads (the reference's thread_count default)")
         _, t8, ok8 = round_time(8)
         rec["threads_8"] = {"value": round(n_blk / t8, 2), "s": round(t8, 1), "verified": ok8}
+        log("cpu baseline: configs 2 and 3 on the oracle")
+        rec["configs"] = cpu_config_legs(args, lib, threads)
     return rec
+
+
+def cpu_config_legs(args, lib, threads):
+    """BASELINE configs 2 and 3 on the CPU oracle with the same services and op order as the GPU
+    legs (config_legs): SubBytes via the reference-order sbox_service.sub_bytes_array of one
+    ciphertext, and the nibble-domain ShiftRows + MixColumns of one ciphertext pair."""
+    from types import SimpleNamespace
+
+    from aes_xor_fhe import aes_tables as T
+    from aes_xor_fhe.aes_round import AESRoundEngine
+    from aes_xor_fhe.fhe import Engine
+    from aes_xor_fhe.sbox.sbox_service import SBoxService
+    from aes_xor_fhe.utils import zeta_decode, zeta_encode
+    eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes,
+                 scale_bits=args.scale_bits, thread_count=threads, seed=SEED, _lib=lib)
+    sk = eng.create_secret_key(1)
+    pk, rlk, cjk = eng.create_public_key(sk), eng.create_relinearization_key(sk), eng.create_conjugation_key(sk)
+    out = {}
+    sb = SBoxService(SimpleNamespace(engine=eng, relinearization_key=rlk))
+    x = np.random.default_rng(1).integers(0, 256, eng.slot_count)
+    ct = eng.encrypt(zeta_encode(x, modulus=256), pk)
+    t0 = time.perf_counter()
+    res = sb.sub_bytes_array(ct)
+    t = time.perf_counter() - t0
+    ok = bool(np.array_equal(zeta_decode(eng.decrypt(res, sk), modulus=256), T.SBOX[x]))
+    out["config2_subbytes_reference_order"] = {"value": round(eng.slot_count / 16 / t, 2), "unit": "blocks/s", "s": round(t, 1),
+                                               "verified": ok, "threads": threads}
+    R = AESRoundEngine(eng, sk, pk, rlk, cjk)
+    blocks = np.random.default_rng(2026).integers(0, 256, (1, R.n_blk, 16), dtype=np.uint8)
+    h, l = R.encrypt_blocks(blocks)
+    t0 = time.perf_counter()
+    res = R.mix_columns(R.shift_mix_terms(h), R.shift_mix_terms(l))
+    t = time.perf_counter() - t0
+    ok = bool(np.array_equal(R.decrypt_blocks(*res), T.mix_columns(T.shift_rows(blocks))))
+    out["config3_shiftrows_mixcolumns_batch_1"] = {"value": round(R.n_blk / t, 2), "unit": "blocks/s",
+                                                   "s": round(t, 1), "verified": ok, "threads": threads}
+    return out
 
 
 def main():

@@ -165,10 +165,13 @@ def test_poly2_bit_exact(product_lib, oracle_lib, gpu_available):
     np.testing.assert_allclose(dec, want, atol=1e-4)
 
 
-def test_poly2_int_bit_exact(product_lib, oracle_lib, gpu_available):
+@pytest.mark.parametrize("scale_bits", [40, 44])
+def test_poly2_int_bit_exact(product_lib, oracle_lib, gpu_available, scale_bits):
     """Integer-weight bivariate evaluation: 6 outputs (two chunks), a zero output, mixed basis
-    levels (power bases), a broadcast basis element, negative weights."""
-    g, o = _pair(product_lib, oracle_lib, **SMALL)
+    levels (power bases), a broadcast basis element, negative weights.  Scale 44 (config 5's
+    chain): the 44-bit limbs take the exact-FMA kernel chosen from the weight bound, q_0 the
+    folding one."""
+    g, o = _pair(product_lib, oracle_lib, **dict(SMALL, scale_bits=scale_bits))
     kg, ko = _keys(g), _keys(o)
     rng = np.random.default_rng(8)
     zx = np.exp(-2j * np.pi * rng.integers(0, 16, (2, g.slot_count)) / 16)
