@@ -198,6 +198,15 @@ struct Pool {
             }
         }
     }
+    // turn the live block p (exactly parts * part bytes, part a multiple of kAlign) into `parts`
+    // live blocks of `part` bytes each, freed independently (zero-copy split of a batched result)
+    void split(void* p, int parts, size_t part) {
+        auto lt = live_.find(p);
+        if (lt == live_.end() || part % kAlign || lt->second != (size_t)parts * part)
+            throw_err(AESFHE_EARG, "pool split of a block that is not %d x %zu bytes", parts, part);
+        live_.erase(lt);
+        for (int t = 0; t < parts; t++) live_[(char*)p + (size_t)t * part] = part;
+    }
     void release_all() {  // engine teardown: no live block remains
         hipDeviceSynchronize();
         for (auto& kv : chunks_) hipFree(kv.first);
@@ -389,6 +398,30 @@ static aesfhe_ct* ct_new(aesfhe_engine* e, int B, int np, int level) {
     c->bytes = (size_t)B * np * (level + 1) * e->N * 8;
     c->d = (u64*)e->pool.get(c->bytes);
     return c;
+}
+
+// The m outputs of a batched result r (batch m * B, output t = elements t*B .. t*B + B - 1) as m
+// ciphertexts of batch B sharing r's device block (split in the pool, no copy); r is consumed.
+static std::vector<aesfhe_ct*> ct_split_batch(aesfhe_engine* e, aesfhe_ct* r, int m) {
+    const int B = r->B / m;
+    const size_t part = (size_t)B * r->np * (r->level + 1) * e->N * 8;
+    e->pool.split(r->d, m, part);
+    std::vector<aesfhe_ct*> out(m);
+    for (int t = 0; t < m; t++) {
+        auto* c = new aesfhe_ct;
+        c->eng = e;
+        e->refs++;
+        c->B = B;
+        c->np = r->np;
+        c->level = r->level;
+        c->is_zero = 0;
+        c->bytes = part;
+        c->d = (u64*)((char*)r->d + (size_t)t * part);
+        out[t] = c;
+    }
+    r->d = nullptr;  // the blocks now belong to the parts
+    aesfhe_ct_free(r);
+    return out;
 }
 
 static aesfhe_ct* ct_zero_new(aesfhe_engine* e, int B, int np, int level) {
@@ -2583,13 +2616,8 @@ extern "C" int aesfhe_poly2(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_
         HIPC(hipGetLastError());
         aesfhe_ct* r2 = relin_rescale(e, d3, rlk, 2);
         aesfhe_ct_free(d3);
-        const size_t per_out = (size_t)B * 2 * (l - 1) * N;  // words of one output (batch B, level l-2)
-        for (int t = 0; t < ml; t++) {
-            aesfhe_ct* o = ct_new(e, B, 2, l - 2);
-            HIPC(hipMemcpyAsync(o->d, r2->d + t * per_out, per_out * 8, hipMemcpyDeviceToDevice, e->stream));
-            outs[live[t]] = o;
-        }
-        aesfhe_ct_free(r2);
+        std::vector<aesfhe_ct*> parts = ct_split_batch(e, r2, ml);  // no copies
+        for (int t = 0; t < ml; t++) outs[live[t]] = parts[t];
     }
     for (int t = 0; t < m; t++)
         if (!outs[t]) outs[t] = ct_zero_new(e, B, 2, l - 2);
@@ -2755,13 +2783,8 @@ extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, in
         HIPC(hipGetLastError());
         aesfhe_ct* r2 = relin_rescale(e, d3, rlk, 2);
         aesfhe_ct_free(d3);
-        const size_t per_out = (size_t)B * 2 * (l - 1) * N;
-        for (int t = 0; t < ml; t++) {
-            aesfhe_ct* o = ct_new(e, B, 2, l - 2);
-            HIPC(hipMemcpyAsync(o->d, r2->d + t * per_out, per_out * 8, hipMemcpyDeviceToDevice, e->stream));
-            outs[live[t]] = o;
-        }
-        aesfhe_ct_free(r2);
+        std::vector<aesfhe_ct*> parts = ct_split_batch(e, r2, ml);  // no copies
+        for (int t = 0; t < ml; t++) outs[live[t]] = parts[t];
     }
     for (int t = 0; t < m; t++)
         if (!outs[t]) outs[t] = ct_zero_new(e, B, 2, l - 2);

@@ -29,6 +29,15 @@ namespace aesfhe {
 // conflict-free for the A / B / C patterns.
 __device__ __forceinline__ int r8p(int e) { return e + (e >> 3); }
 
+// A row (and its LDS region) belongs to 32 lanes of ONE wave, so the layout exchanges need only
+// wave-level ordering, not a workgroup barrier: LDS instructions of a wave complete in issue
+// order, and the fence + wave barrier stop the compiler from moving the accesses across.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // rt: 256 + row when W is the limb's global psi table, 1 when W is the row's own LDS copy
 // (entry ml + j = the table's ml rt + j, stages ml = 1 .. 128).
 __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, double* sr, int L, int rt,
@@ -53,7 +62,7 @@ __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, doub
     }
 #pragma unroll
     for (int r = 0; r < 8; r++) sr[r8p(L + 32 * r)] = x[r];
-    __syncthreads();
+    wave_lds_sync();
     const int eb = 32 * (L >> 2) + (L & 3);
 #pragma unroll
     for (int r = 0; r < 8; r++) x[r] = sr[r8p(eb + 4 * r)];
@@ -73,10 +82,10 @@ __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, doub
             for (int k = 0; k < h; k++) ct_f(x[j * 2 * h + k], x[j * 2 * h + k + h], wq, q);
         }
     }
-    __syncthreads();  // every lane has read its B elements
+    wave_lds_sync();  // every lane has read its B elements
 #pragma unroll
     for (int r = 0; r < 8; r++) sr[r8p(eb + 4 * r)] = x[r];
-    __syncthreads();
+    wave_lds_sync();
 #pragma unroll
     for (int r = 0; r < 8; r++) x[r] = sr[r8p(8 * L + r)];
     // C: ml = 64 (distance 2, j = 2L + (r >> 2)), ml = 128 (distance 1, j = 4L + (r >> 1))
@@ -97,13 +106,13 @@ __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, doub
 #pragma unroll
         for (int j = 0; j < 4; j++) ct_f(x[2 * j], x[2 * j + 1], W[base + j], q);
     }
-    __syncthreads();  // every lane has read its C elements
+    wave_lds_sync();  // every lane has read its C elements
 #pragma unroll
     for (int r = 0; r < 8; r++) sr[r8p(8 * L + r)] = big ? fred(x[r], q, qi) : x[r];
-    __syncthreads();
+    wave_lds_sync();
 #pragma unroll
     for (int r = 0; r < 8; r++) x[r] = sr[r8p(L + 32 * r)];  // back to A
-    __syncthreads();  // the next digit rewrites sr
+    wave_lds_sync();  // the next digit rewrites sr
 }
 
 // grid: 8 * ceil(B / G) * (ne * (R / 8) / 8) blocks of 256 (8 rows x 32 lanes; R = N / 256 rows:
@@ -146,7 +155,7 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
             tw[e] = W[(long)ml * (R + row) + (e - ml)];
         }
     }
-    __syncthreads();
+    wave_lds_sync();  // the row's twiddles: written and read by its own 32 lanes
     const long roff = ((long)t << LOGN) + (long)row * 256 + L;  // element (row, L + 32 r) at roff + 32 r
     double a0[G][8], a1[G][8];
 #pragma unroll

@@ -74,6 +74,17 @@ __device__ __forceinline__ void st_d(u64* p, double v) { __builtin_nontemporal_s
 
 constexpr int kPadF = 17;  // LDS row stride (8 B words) of the 16 x 16 transpose tiles
 
+// Row passes: a row and its LDS tile belong to 16 lanes of one wave (lane (b, rl) = (tid & 15,
+// tid >> 4): wave w holds rows 4w .. 4w + 3), and the coalesced copy-in / copy-out below move
+// only the wave's own 4 rows, so the exchanges need wave-level ordering, not a workgroup barrier
+// (LDS instructions of a wave complete in issue order; the fences and the wave barrier keep the
+// compiler from moving accesses across).
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Forward, column pass: the first log2(R) stages on columns of stride 256 (R = N / 256 rows:
 // 256 for N = 2^16, 512 for N = 2^17); canonical u64 in, raw doubles out.  Workgroup = 16
 // columns [c0, c0+16); lane (cl, b) = (tid & 15, tid >> 4).  R = 512: the first stage (distance
@@ -197,7 +208,7 @@ __device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, doub
     }
 #pragma unroll
     for (int a = 0; a < 16; a++) sr[a * kPadF + b] = x[a];
-    __syncthreads();
+    wave_sync_lds();
     const int ap = b;
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) x[bb] = sr[ap * kPadF + bb];
@@ -247,12 +258,14 @@ __device__ __forceinline__ void nttf_fwd_rows_body(const Span& dst, const Tabs& 
     // coalesced store through LDS: canonical residues, then row-major copy-out
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) sr[ap * kPadF + bb] = __longlong_as_double((long long)fcanon(x[bb], q, qi));
-    __syncthreads();
+    wave_sync_lds();
+    // wave w stores its rows 4w .. 4w + 3: element e = 1024 w + 64 k + lane of the 16 x 256 tile
+    const int e0 = (tid >> 6) * 1024 + (tid & 63);
     if (!FIN) {
         u64* base = io + (long)bx * 16 * 256;
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-            const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
+            const int e = e0 + 64 * k;
             __builtin_nontemporal_store((u64)__double_as_longlong(s[row_tile_idx(e)]), &base[e]);
         }
     } else {
@@ -264,8 +277,8 @@ __device__ __forceinline__ void nttf_fwd_rows_body(const Span& dst, const Tabs& 
         const double f = fin.dinvf[i], w = tw_w(f, q);
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-            const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
-            const double conv = u2d((u64)__double_as_longlong(s[r * 16 * kPadF + (cc >> 4) * kPadF + (cc & 15)]));
+            const int e = e0 + 64 * k;
+            const double conv = u2d((u64)__double_as_longlong(s[row_tile_idx(e)]));
             double v = fmul_rem(u2d(ap[e]) - conv, w, f, q);
             if (dp) v += u2d(dp[e]);
             __builtin_nontemporal_store(fcanon(v, q, qi), &op[e]);  // streaming
@@ -292,12 +305,15 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
     const bool big = q >= kBigPrime;
     const double* W = T.ipsif + ((long)pid << T.logN);
     const u64* gb = in + (long)blockIdx.x * 16 * 256;
+    {  // wave w loads its rows 4w .. 4w + 3 (coalesced), element e = 1024 w + 64 k + lane
+        const int e0 = (tid >> 6) * 1024 + (tid & 63);
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int e = k * 256 + tid, r = e >> 8, cc = e & 255;
-        s[r * 16 * kPadF + (cc >> 4) * kPadF + (cc & 15)] = u2d(gb[e]);
+        for (int k = 0; k < 16; k++) {
+            const int e = e0 + 64 * k;
+            s[row_tile_idx(e)] = u2d(gb[e]);
+        }
     }
-    __syncthreads();
+    wave_sync_lds();
     double* sr = s + rl * 16 * kPadF;
     const int ap = b;
     double x[16];
@@ -323,7 +339,7 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
     else stages_lo(std::false_type{});
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) sr[ap * kPadF + bb] = x[bb];
-    __syncthreads();
+    wave_sync_lds();
 #pragma unroll
     for (int a = 0; a < 16; a++) x[a] = sr[a * kPadF + b];
     auto stages_hi = [&](auto fold) {
