@@ -219,7 +219,8 @@ class Bootstrapper:
         p = q T_g + r with T_{g+j} = 2 T_g T_j - T_{g-j}, so q_0 = c_g, q_j = 2 c_{g+j},
         r_{g-j} -= c_{g+j}; leaves (degree < b) are one lincomb of T_1..T_{b-1}.  For deg 31,
         b = 8: 11 ciphertext products (T_2..T_8, T_16, three splits) instead of 30, same depth
-        ceil(log2(deg + 1)) + 1."""
+        ceil(log2(deg + 1)) + 1, and 10 relinearisations (the top split's product shares one
+        with its remainder's)."""
         e = self.e
         cheb = self.cheb if coeffs is None else coeffs
         deg = len(cheb) - 1
@@ -240,6 +241,16 @@ class Bootstrapper:
 
         baby = 1 << max(1, (deg + 1).bit_length() // 2)  # 8 for deg 31, 4 for deg 15
 
+        # ev returns the value as (pairs, lin, c0) = sum a_i b_i + lin + c0 with the products not
+        # yet relinearised: a node's own giant product joins its remainder's pending products, so
+        # the products summed into one value share ONE relinearisation + rescale (Engine.dot) --
+        # deg 31: 2 giant relinearisations instead of 3, same depth.
+        def materialize(pairs, lin, c0):
+            out = e.dot([a for a, _ in pairs], [b for _, b in pairs], self.rlk) if pairs else None
+            if lin is not None:
+                out = lin if out is None else e.add(out, lin)
+            return out, c0
+
         def ev(c):
             d = len(c) - 1
             while d > 0 and abs(c[d]) < 1e-14:
@@ -247,7 +258,7 @@ class Bootstrapper:
             if d < baby:
                 ks = [k for k in range(1, d + 1) if abs(c[k]) > 1e-14]
                 out = e.lincomb([tk(k) for k in ks], [complex(c[k]) for k in ks]) if ks else None
-                return out, complex(c[0])
+                return [], out, complex(c[0])
             g = baby
             while 2 * g <= d:
                 g *= 2
@@ -257,18 +268,15 @@ class Bootstrapper:
             for jj in range(1, d - g + 1):
                 q[jj] = 2.0 * c[g + jj]
                 r[g - jj] -= c[g + jj]
-            qc, q0 = ev(q)
-            rc, r0 = ev(r)
+            qc, q0 = materialize(*ev(q))
+            rp, rl, r0 = ev(r)
             qt = e.add(qc, q0) if qc is not None else None
             if qt is None:
                 prod = e.multiply(tk(g), q0)
-                return (prod if rc is None else e.add(prod, rc)), r0
-            if rc is not None and rc.level >= min(qt.level, tk(g).level):
-                return e.multiply_fma(qt, tk(g), self.rlk, c=rc, gamma=1.0), r0
-            prod = e.multiply(qt, tk(g), self.rlk)
-            return (prod if rc is None else e.add(prod, rc)), r0
+                return rp, (prod if rl is None else e.add(prod, rl)), r0
+            return [(qt, tk(g))] + rp, rl, r0
 
-        out, c0 = ev(list(cheb))
+        out, c0 = materialize(*ev(list(cheb)))
         T.clear()  # ev / tk form a closure cycle: release the T_k now, not at the next gc pass
         return e.add(out, c0)
 

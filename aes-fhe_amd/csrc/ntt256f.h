@@ -184,12 +184,16 @@ struct RowFin {
 // row = r0 + rl from rp (raw doubles, stride-16 gather), 4 stages in registers, LDS transpose
 // through sr = s + rl * 16 * kPadF, 4 stages.  On return lane ap = b holds elements
 // ap * 16 + bb (bb = 0..15) of its row, lazily reduced (ranges: file header).
-template <int RR>
-__device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, double* sr, int b, int row,
-                                            const double* W, const double* R, double q, double qi,
-                                            bool big) {
+__device__ __forceinline__ void row_ntt_load(double (&x)[16], const u64* rp, int b) {
 #pragma unroll
     for (int a = 0; a < 16; a++) x[a] = ld_d(&rp[a * 16 + b]);
+}
+// the 8 stages on x as loaded by row_ntt_load (the split lets a caller issue its own epilogue
+// loads between the two, behind the row's loads)
+template <int RR>
+__device__ __forceinline__ void row_ntt_fwd_stages(double (&x)[16], double* sr, int b, int row,
+                                                   const double* W, const double* R, double q, double qi,
+                                                   bool big) {
 #pragma unroll
     for (int st = 0; st < 4; st++) {
         const int ml = 1 << st, h = 8 >> st;
@@ -229,6 +233,13 @@ __device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, doub
         }
     }
 }
+template <int RR>
+__device__ __forceinline__ void row_ntt_fwd(double (&x)[16], const u64* rp, double* sr, int b, int row,
+                                            const double* W, const double* R, double q, double qi,
+                                            bool big) {
+    row_ntt_load(x, rp, b);
+    row_ntt_fwd_stages<RR>(x, sr, b, row, W, R, q, qi, big);
+}
 // element e = k * 256 + tid (k = 0..15) of the workgroup's 16 x 256 tile, as stored by lane
 // (ap, rl) at sr[ap * kPadF + bb]: the coalesced read-out order of the row passes
 __device__ __forceinline__ int row_tile_idx(int e) {
@@ -254,13 +265,24 @@ __device__ __forceinline__ void nttf_fwd_rows_body(const Span& dst, const Tabs& 
     double x[16];
     double* sr = s + rl * 16 * kPadF;
     const int ap = b;
-    row_ntt_fwd<R>(x, io + (long)row * 256, sr, b, row, W, Rf, q, qi, big);
+    // wave w stores its rows 4w .. 4w + 3: element e = 1024 w + 64 k + lane of the 16 x 256 tile
+    const int e0 = (tid >> 6) * 1024 + (tid & 63);
+    row_ntt_load(x, io + (long)row * 256, b);
+    // FIN: the accumulator words of this lane's output elements are requested right behind the
+    // row's loads, so they arrive while the row transform computes
+    u64 accw[FIN ? 16 : 1];
+    if (FIN) {
+        const int p = by / fin.nl, i = by - p * fin.nl;
+        const u64* apf = fin.acc + (long)(p >> 1) * fin.abs_ + (long)(p & 1) * fin.acs + ((long)i << T.logN) +
+                         (long)bx * 16 * 256;
+#pragma unroll
+        for (int k = 0; k < (FIN ? 16 : 1); k++) accw[k] = apf[e0 + 64 * k];
+    }
+    row_ntt_fwd_stages<R>(x, sr, b, row, W, Rf, q, qi, big);
     // coalesced store through LDS: canonical residues, then row-major copy-out
 #pragma unroll
     for (int bb = 0; bb < 16; bb++) sr[ap * kPadF + bb] = __longlong_as_double((long long)fcanon(x[bb], q, qi));
     wave_sync_lds();
-    // wave w stores its rows 4w .. 4w + 3: element e = 1024 w + 64 k + lane of the 16 x 256 tile
-    const int e0 = (tid >> 6) * 1024 + (tid & 63);
     if (!FIN) {
         u64* base = io + (long)bx * 16 * 256;
 #pragma unroll
@@ -271,7 +293,6 @@ __device__ __forceinline__ void nttf_fwd_rows_body(const Span& dst, const Tabs& 
     } else {
         const int y = by, p = y / fin.nl, i = y - p * fin.nl, bb = p >> 1, c = p & 1;
         const long off = ((long)i << T.logN) + (long)bx * 16 * 256;
-        const u64* ap = fin.acc + (long)bb * fin.abs_ + (long)c * fin.acs + off;
         const u64* dp = fin.addend.ptr && c < fin.addend.np ? fin.addend.ptr + (long)bb * fin.addend.bs + (long)c * fin.addend.ps + off : nullptr;
         u64* op = fin.out + (long)bb * fin.obs + (long)c * fin.ops + off;
         const double f = fin.dinvf[i], w = tw_w(f, q);
@@ -279,7 +300,7 @@ __device__ __forceinline__ void nttf_fwd_rows_body(const Span& dst, const Tabs& 
         for (int k = 0; k < 16; k++) {
             const int e = e0 + 64 * k;
             const double conv = u2d((u64)__double_as_longlong(s[row_tile_idx(e)]));
-            double v = fmul_rem(u2d(ap[e]) - conv, w, f, q);
+            double v = fmul_rem(u2d(accw[FIN ? k : 0]) - conv, w, f, q);
             if (dp) v += u2d(dp[e]);
             __builtin_nontemporal_store(fcanon(v, q, qi), &op[e]);  // streaming
         }

@@ -53,10 +53,10 @@ PEAK_HBM_GBS = 8000.0
 METRIC = "AES-128 blocks/sec (homomorphic full round) at N=2^16, L=30; 1/2/4/8 MI355X"
 SEED = 0x5EED5EED  # shared by every rank: identical keys without key traffic
 
-PMC_FILE = ROOT / "profiles" / "r01" / "pmc" / "ntt_traffic.json"
+PMC_FILE = ROOT / "profiles" / "r02" / "pmc" / "ntt_traffic.json"
 PMC_NOTE = ("HBM bytes per NTT launch = algorithmic bytes x the HBM/algorithmic ratio measured by "
             "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 calibration) + WRITE_SIZE on the same NTT kernels "
-            "at the same parameters (profiles/r01/pmc/ntt_traffic.json)")
+            "at the same parameters (profiles/r02/pmc/ntt_traffic.json)")
 
 
 _T0 = time.perf_counter()
