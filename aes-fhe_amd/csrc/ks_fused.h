@@ -11,7 +11,8 @@
 //
 // Ranges: the row NTT (table twiddles) leaves |x| <= 17q for q < 2^42 (folded to q/2 + 1 for larger primes
 // before the product); fmul_rem(x, key) lies in (-1.5q, 1.5q) (on-the-fly key quotient), so the
-// beta <= 12 products sum below 18q < 2^47 for small primes; big primes fold every 4 digits.
+// beta <= 12 products plus the folded initial term (<= q/2 + 1) sum below 19q < 2^47 for small
+// primes; big primes fold every 4 digits (< 6.5q < 2^53).
 #pragma once
 #include "kernels_ops.h"
 #include "ntt256f.h"
@@ -157,11 +158,33 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
     }
     wave_lds_sync();  // the row's twiddles: written and read by its own 32 lanes
     const long roff = ((long)t << LOGN) + (long)row * 256 + L;  // element (row, L + 32 r) at roff + 32 r
+    // the accumulators start from the epilogue terms (P * addend, the previous acc), so their
+    // loads are issued first and land while the digits compute; folded to |x| <= q/2 + 1
     double a0[G][8], a1[G][8];
 #pragma unroll
-    for (int g = 0; g < G; g++)
+    for (int g = 0; g < G; g++) {
+        const int bb = b0 + g;
 #pragma unroll
         for (int r = 0; r < 8; r++) a0[g][r] = a1[g][r] = 0.0;
+        if (bb >= B) continue;
+        if (pmodf && t <= l) {
+            const double f = pmodf[t], w = tw_w(f, q);
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const int kk = row * 256 + L + 32 * r;
+                a0[g][r] = fmul_rem(u2d(opnd_get(addend, bb, 0, t, kk, LOGN)), w, f, q);
+                a1[g][r] = fmul_rem(u2d(opnd_get(addend, bb, 1, t, kk, LOGN)), w, f, q);
+            }
+        }
+        if (accum) {
+            const u64* o0 = acc + (long)bb * abs_ + roff;
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                a0[g][r] = fred(a0[g][r] + u2d(o0[32 * r]), q, qi);
+                a1[g][r] = fred(a1[g][r] + u2d(o0[acs + 32 * r]), q, qi);
+            }
+        }
+    }
 #pragma unroll 1
     for (int j = 0; j < beta; j++) {
         // the key digit's words are loaded first: they arrive while the row NTT computes
@@ -207,20 +230,10 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
         const int bb = b0 + g;
         if (bb >= B) break;
         u64* o0 = acc + (long)bb * abs_ + roff;
-        if (pmodf && t <= l) {
-            const double f = pmodf[t], w = tw_w(f, q);
-#pragma unroll
-            for (int r = 0; r < 8; r++) {
-                const int kk = row * 256 + L + 32 * r;
-                a0[g][r] = fred(a0[g][r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 0, t, kk, LOGN)), w, f, q);
-                a1[g][r] = fred(a1[g][r], q, qi) + fmul_rem(u2d(opnd_get(addend, bb, 1, t, kk, LOGN)), w, f, q);
-            }
-        }
 #pragma unroll
         for (int r = 0; r < 8; r++) {
-            const double p0 = accum ? u2d(o0[32 * r]) : 0.0, p1 = accum ? u2d(o0[acs + 32 * r]) : 0.0;
-            __builtin_nontemporal_store(fcanon(a0[g][r] + p0, q, qi), &o0[32 * r]);  // streaming
-            __builtin_nontemporal_store(fcanon(a1[g][r] + p1, q, qi), &o0[acs + 32 * r]);
+            __builtin_nontemporal_store(fcanon(a0[g][r], q, qi), &o0[32 * r]);  // streaming
+            __builtin_nontemporal_store(fcanon(a1[g][r], q, qi), &o0[acs + 32 * r]);
         }
     }
 }
