@@ -1,3 +1,6 @@
+// NOTE: a measurement record (round 1: the integer passes of the removed ntt256.h against the fp64
+// passes, and the copy kernel that calibrated FETCH_SIZE); it no longer builds (ntt256.h was
+// removed with the env-switched integer path in round 2).  Its results are quoted in DESIGN.md 4.1.
 // NTT pass microbenchmark (dev tool): each N=2^16 pass kernel over 248 limbs, real vs
 // load/store-only (NTT_NOCOMPUTE) builds, to separate memory time from arithmetic time.
 #include <hip/hip_runtime.h>
