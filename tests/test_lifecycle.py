@@ -156,3 +156,56 @@ def test_device_transfer_gpu(product_lib, gpu_available):
         torch.cuda.synchronize()
         return t, t.data_ptr()
     _device_roundtrip(product_lib, dev)
+
+
+@pytest.mark.gpu
+def test_device_arena_reuse_gpu(product_lib, gpu_available):
+    """The chunked best-fit arena (engine.hip Pool): ciphertexts of many sizes created and freed
+    in random order leave every byte reusable (live returns to its baseline, no new chunk for a
+    repeat of the same workload), split batched results (poly2 outputs) free independently, and
+    trim returns the empty chunks; values stay intact throughout."""
+    e = Engine(_lib=product_lib, log_n=12, max_level=8, special_primes=3, seed=5)
+    sk = e.create_secret_key(1)
+    pk, rlk = e.create_public_key(sk), e.create_relinearization_key(sk)
+    rng = np.random.default_rng(9)
+    z = np.exp(2j * np.pi * rng.integers(0, 16, e.slot_count) / 16)
+    w = e.encrypt(z, pk)
+    w = e.multiply(w, w, rlk)  # anything materialised on first use exists before the baseline
+    del w
+    gc.collect()
+    e.synchronize()
+    base = e.pool_stats()["live"]
+
+    def workload():
+        cts = [e.encrypt(z, pk, level=int(rng.integers(1, 9))) for _ in range(40)]
+        cts += [e.concat([cts[i]] * int(rng.integers(1, 5))) for i in range(10)]
+        prods = [e.multiply(cts[i], cts[i + 1], rlk) for i in range(0, 20, 2)]
+        for i in rng.permutation(len(cts)):
+            cts[i] = None
+        np.testing.assert_allclose(e.decrypt(prods[3], sk), z * z, atol=1e-4)
+        del prods, cts
+        gc.collect()
+        e.synchronize()
+
+    workload()
+    after1 = e.pool_stats()
+    assert after1["live"] == base, (after1, base)
+    workload()
+    after2 = e.pool_stats()
+    assert after2["live"] == base and after2["mallocs"] == after1["mallocs"], (after1, after2)
+    # split results: poly2_int outputs share one block; freed in any order they merge back
+    xb = e.make_power_basis(e.encrypt(z, pk), 3, rlk)
+    yb = e.make_power_basis(e.encrypt(z, pk), 3, rlk)
+    W = rng.integers(-4, 5, (4, 4, 4))
+    outs = e.poly2_int(xb, yb, W, 64, rlk)
+    want = sum(W[2, i, j] / 64 * z ** i * z ** j for i in range(4) for j in range(4))
+    np.testing.assert_allclose(e.decrypt(outs[2], sk), want, atol=1e-3)
+    for i in (1, 3, 0, 2):
+        outs[i] = None
+    del xb, yb, outs
+    gc.collect()
+    e.synchronize()
+    assert e.pool_stats()["live"] == base
+    held = e.pool_stats()["held"]
+    e.pool_trim()
+    assert e.pool_stats()["held"] <= held
