@@ -41,10 +41,16 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // rt: 256 + row when W is the limb's global psi table, 1 when W is the row's own LDS copy
 // (entry ml + j = the table's ml rt + j, stages ml = 1 .. 128).
+__device__ __forceinline__ void row_ntt8_stages(double (&x)[8], double* sr, int L, int rt, const double* W, double q,
+                                                double qi, bool big);
 __device__ __forceinline__ void row_ntt8_fwd(double (&x)[8], const u64* rp, double* sr, int L, int rt,
                                              const double* W, double q, double qi, bool big) {
 #pragma unroll
     for (int r = 0; r < 8; r++) x[r] = ld_d(&rp[L + 32 * r]);
+    row_ntt8_stages(x, sr, L, rt, W, q, qi, big);
+}
+__device__ __forceinline__ void row_ntt8_stages(double (&x)[8], double* sr, int L, int rt, const double* W, double q,
+                                                double qi, bool big) {
     // A: ml = 1, 2, 4 (global stages 0..2 of the pass); twiddle j = r >> (3 - st)
 #pragma unroll
     for (int st = 0; st < 3; st++) {
