@@ -121,10 +121,15 @@ class AESRowRound:
         for a in range(4):
             for b in range(a + 1, 4):
                 m[(1 << a) | (1 << b)] = self.mul(b4[a], b4[b])
-        m[0b0111] = self.mul(m[0b0011], b4[2])
-        m[0b1011] = self.mul(m[0b0011], b4[3])
-        m[0b1101] = self.mul(m[0b0101], b4[3])
-        m[0b1110] = self.mul(m[0b0110], b4[3])
+        # the triples multiply a pair (one level down) by a single bit: the engine would align
+        # b4[3] to the pairs' level three times over, so it (and b4[2]) is level-downed once here
+        # -- the same operation the multiply would run, bit for bit
+        lv = min(m[0b0011].level, m[0b0101].level, m[0b0110].level)
+        b2, b3 = (c if c.level <= lv else self.e.level_down(c, lv) for c in (b4[2], b4[3]))
+        m[0b0111] = self.mul(m[0b0011], b2)
+        m[0b1011] = self.mul(m[0b0011], b3)
+        m[0b1101] = self.mul(m[0b0101], b3)
+        m[0b1110] = self.mul(m[0b0110], b3)
         m[0b1111] = self.mul(m[0b0011], m[0b1100])
         return m
 
