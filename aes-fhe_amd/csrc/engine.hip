@@ -516,7 +516,7 @@ static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse
     {
         ProfScope ps(e, FAM_NTT, by);
         if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_cols<R>, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
-        else hipLaunchKernelGGL(k_nttf_inv_rows<R>, dim3(R / 16, total), dim3(256), 0, e->stream, src, dst, T);
+        else hipLaunchKernelGGL((k_nttf_inv_rows<R, false>), dim3(R / 16, total), dim3(256), 0, e->stream, src, dst, T, Span{});
     }
     ProfScope ps(e, FAM_NTT, by);
     if (!inverse) hipLaunchKernelGGL((k_nttf_fwd_rows_t<false, R>), dim3(R / 16, total), dim3(256), 0, e->stream, dst, T, RowFin{});
@@ -525,6 +525,23 @@ static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse
 
 // the N = 2^16 / 2^17 fp64 passes with fused epilogues (ModDown finish, key-switch inner product)
 static bool fused_ntt(const aesfhe_engine* e) { return e->logN == 16 || e->logN == 17; }
+
+// inverse NTT of the product a (x) b (two canonical operand spans of one shape) into dst, the
+// product formed in the row pass's copy-in (fused_ntt engines)
+static void intt_prod(aesfhe_engine* e, Span a, Span b, Span dst, int total) {
+    if (total <= 0) return;
+    Tabs T = e->tabs();
+    const double by = 8.0 * e->N * (double)total;
+    {
+        ProfScope ps(e, FAM_NTT, 2.0 * by);  // two operands read
+        if (e->logN == 16) hipLaunchKernelGGL((k_nttf_inv_rows<256, true>), dim3(16, total), dim3(256), 0, e->stream, a, dst, T, b);
+        else hipLaunchKernelGGL((k_nttf_inv_rows<512, true>), dim3(32, total), dim3(256), 0, e->stream, a, dst, T, b);
+    }
+    ProfScope ps(e, FAM_NTT, by);
+    if (e->logN == 16) hipLaunchKernelGGL(k_nttf_inv_cols<256>, dim3(16, total), dim3(256), 0, e->stream, dst, T);
+    else hipLaunchKernelGGL(k_nttf_inv_cols<512>, dim3(16, total), dim3(256), 0, e->stream, dst, T);
+    HIPC(hipGetLastError());
+}
 
 // the fp64 column pass alone (the extension limbs and the conv of a ModDown, whose row passes run
 // fused with their consumers)
@@ -1758,14 +1775,22 @@ static int ks_beta(const aesfhe_engine* e, int l) {
 // ext holds ks_beta(l) * B * (l+1+K) limbs.  Shared by every key in aesfhe_rotate_hoisted.
 // cols_only (fused_ntt engines): the extension limbs get only the NTT column pass; the row pass
 // runs inside k_nttf_rows_ks together with the inner product (ks_fused.h).
-static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64* ext, bool cols_only = false) {
+// pa, pb (fused_ntt engines): the input is poly 1 of each, multiplied (d2 = a1 b1 of a product)
+static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64* ext, bool cols_only = false,
+                     const Opnd* pa = nullptr, const Opnd* pb = nullptr) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long lN = (long)(l + 1) * N, neN = (long)ne * N;
     const int beta = ks_beta(e, l);
     Tmp dc(e, (size_t)B * lN);
     // 1. INTT copy of the input
-    Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1), sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
-    ntt(e, sd, sdc, B * (l + 1), true);
+    Span sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
+    if (pa) {
+        intt_prod(e, span_s((u64*)pa->ptr + pa->ps, pa->bs, l + 1, l + 1, 0, e->Lp1),
+                  span_s((u64*)pb->ptr + pb->ps, pb->bs, l + 1, l + 1, 0, e->Lp1), sdc, B * (l + 1));
+    } else {
+        Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1);
+        ntt(e, sd, sdc, B * (l + 1), true);
+    }
     for (int j = 0; j < beta; j++) {
         const int lo = j * K, hi = std::min(lo + K, l + 1), alpha = hi - lo;
         const size_t set = (size_t)j * K + (alpha - 1);
@@ -1800,20 +1825,28 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
 // acc instead of overwriting it (the lazy-ModDown sums of aesfhe_linear_bsgs).  ext_cols: ext
 // holds column-pass intermediates (ks_modup cols_only) and the inner product runs in the fused
 // row pass k_nttf_rows_ks.
+// pb (ext_cols, pmod, no accum): relinearisation of the product addend (x) pb (k_nttf_rows_ks
+// PROD; d unused).
 static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, int B, int l,
-                         const aesfhe_key* k, Opnd addend, bool pmod, u64* acc, bool ext_cols, bool accum = false) {
+                         const aesfhe_key* k, Opnd addend, bool pmod, u64* acc, bool ext_cols, bool accum = false,
+                         const Opnd* pb = nullptr) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long neN = (long)ne * N;
     const int beta = ks_beta(e, l);
     const double* pm = pmod ? (const double*)e->pmodf : (const double*)nullptr;
+    if (pb && (!ext_cols || !pmod || accum)) throw_err(AESFHE_EARG, "product key switch needs the fused combined path");
     if (ext_cols) {
         // row pass of every extension limb (credited half an NTT per limb: 8 N B) + the inner product
-        // (key read once per call, accumulators written; ext never leaves the chip)
+        // (key read once per call, accumulators written; ext never leaves the chip) + the Q-limb
+        // operands: the own digit's d limbs and the addend (PROD: a0, a1, b0, b1)
         const int nown = std::min(l + 1, beta * K);
-        ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))));
+        const double opw = pb ? 4.0 * (l + 1) : (double)nown + (pmod && addend.ptr ? (double)addend.np * (l + 1) : 0.0);
+        ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown + opw) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))));
         const int R = N / 256, blocks = 8 * B * (ne * (R / 8) / 8);
-        auto kern = R == 256 ? k_nttf_rows_ks<1, 256> : k_nttf_rows_ks<1, 512>;
-        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum);
+        const Opnd none{nullptr, 0, 0, 0};
+        auto kern = pb ? (R == 256 ? k_nttf_rows_ks<1, 256, true> : k_nttf_rows_ks<1, 512, true>)
+                       : (R == 256 ? k_nttf_rows_ks<1, 256, false> : k_nttf_rows_ks<1, 512, false>);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum, pb ? *pb : none);
     } else {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B * (accum ? 2 : 1)));
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
@@ -1895,6 +1928,23 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
     ks_apply(e, d, dbs, ext.p, B, l, k, addend, o, r, fuse);
 }
 
+// relinearisation + r >= 1 rescales of the product a (x) b without a tensor ciphertext
+// (fused_ntt engines, combined ModDown + rescale): d2 = a1 b1 is formed in the INTT's copy-in,
+// d0, d1 and the own digit's d2 term in the prologue of k_nttf_rows_ks (PROD).  Same residues
+// as tensor_ct + relin_rescale; the 3-polynomial tensor (3 limbs written, 3 read back, per
+// Q limb) never reaches HBM.
+static void keyswitch_prod(aesfhe_engine* e, const Opnd& pa, const Opnd& pb, int B, int l, const aesfhe_key* k,
+                           aesfhe_ct* o, int r) {
+    if (!fused_ntt(e) || r < 1 || pa.np != 2 || pb.np != 2 || !pa.ptr || !pb.ptr)
+        throw_err(AESFHE_EARG, "product key switch outside the fused combined path");
+    const long neN = (long)(l + 1 + e->K) * e->N;
+    Tmp ext(e, (size_t)ks_beta(e, l) * B * neN);
+    ks_modup(e, nullptr, 0, B, l, ext.p, true, &pa, &pb);
+    Tmp acc(e, (size_t)B * 2 * neN);
+    ks_inner_acc(e, nullptr, 0, ext.p, B, l, k, pa, true, acc.p, true, false, &pb);
+    moddown_acc(e, acc.p, B, l, r, Opnd{nullptr, 0, 0, 0}, o);
+}
+
 static aesfhe_ct* relin_ct(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_key* rlk) {
     const int l = c->level;
     aesfhe_ct* r = ct_new(e, c->B, 2, l);
@@ -1967,6 +2017,16 @@ static aesfhe_ct* mul_ct(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* 
     Aligned A, Bv;
     align_to(e, a, l, A);
     align_to(e, b, l, Bv);
+    if (fused_ntt(e) && e->K + 1 <= kMdrMaxE) {
+        aesfhe_ct* r = ct_new(e, B, 2, l - 1);
+        try {
+            keyswitch_prod(e, opnd(A.v, B), opnd(Bv.v, B), B, l, rlk, r, 1);
+        } catch (...) {
+            aesfhe_ct_free(r);
+            throw;
+        }
+        return r;
+    }
     aesfhe_ct* t = tensor_ct(e, A.v, Bv.v, B);
     aesfhe_ct* r = relin_rescale(e, t, rlk, 1);
     aesfhe_ct_free(t);

@@ -128,13 +128,20 @@ __device__ __forceinline__ void row_ntt8_stages(double (&x)[8], double* sr, int 
 // are dealt to one XCD (blocks x, x + 8, ...) so the key rows they share are L2 hits.  G batch
 // elements per workgroup share each key word loaded (G = 2 halves the key reads, the largest
 // load stream of the kernel, at the price of a second pair of accumulators).
-template <int G, int R = 256>
+//
+// PROD (relinearisation of a ciphertext product a (x) b, combined ModDown + rescale): no tensor
+// ciphertext exists.  On the Q limbs the prologue reads a0, a1, b0, b1 and forms d0 = a0 b0,
+// d1 = a0 b1 + a1 b0 (the addend, times P) and d2 = a1 b1 (the own digit's limb, times its key
+// words), so the own digit is skipped in the loop; addend = a, d = unused, pb = b.  Products
+// by fmul_rem with the on-the-fly quotient, as the key products: congruent, not canonical,
+// |x| < 3q before the P / key product.
+template <int G, int R = 256, bool PROD = false>
 __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64* __restrict__ d, long dbs,
                                                       const u64* __restrict__ ext, long exs, long exj,
                                                       const u64* __restrict__ key, long kdig, long kcomp,
                                                       u64* __restrict__ acc, long abs_, long acs, int B,
                                                       int beta, int K, int l, int ne, Tabs T, Opnd addend,
-                                                      const double* __restrict__ pmodf, int accum) {
+                                                      const double* __restrict__ pmodf, int accum, Opnd pb) {
     // one LDS array (row transposes, then the 8 rows' twiddles -- see row_ntt8_fwd's rt)
     __shared__ double s[8 * 288 + 8 * 256];
     const int nbg = (B + G - 1) / G;
@@ -173,7 +180,27 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
 #pragma unroll
         for (int r = 0; r < 8; r++) a0[g][r] = a1[g][r] = 0.0;
         if (bb >= B) continue;
-        if (pmodf && t <= l) {
+        if (PROD && t <= l) {
+            const double f = pmodf[t], w = tw_w(f, q);
+            const u64* kp = key + (long)own * kdig + ((long)pid << LOGN) + (long)row * 256 + L;
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const int kk = row * 256 + L + 32 * r;
+                const double x0 = u2d(opnd_get(addend, bb, 0, t, kk, LOGN)), x1 = u2d(opnd_get(addend, bb, 1, t, kk, LOGN));
+                const double y0 = u2d(opnd_get(pb, bb, 0, t, kk, LOGN)), y1 = u2d(opnd_get(pb, bb, 1, t, kk, LOGN));
+                const double kb = u2d(kp[32 * r]), ka = u2d(kp[32 * r + kcomp]);
+                const double y0q = y0 * qi, y1q = y1 * qi;
+                const double p0 = fmul_rem(x0, y0, y0q, q);
+                const double p1 = fmul_rem(x0, y1, y1q, q) + fmul_rem(x1, y0, y0q, q);
+                const double p2 = fmul_rem(x1, y1, y1q, q);
+                a0[g][r] = fmul_rem(p0, w, f, q) + fmul_rem(p2, kb, kb * qi, q);
+                a1[g][r] = fmul_rem(p1, w, f, q) + fmul_rem(p2, ka, ka * qi, q);
+                if (big) {
+                    a0[g][r] = fred(a0[g][r], q, qi);
+                    a1[g][r] = fred(a1[g][r], q, qi);
+                }
+            }
+        } else if (!PROD && pmodf && t <= l) {
             const double f = pmodf[t], w = tw_w(f, q);
 #pragma unroll
             for (int r = 0; r < 8; r++) {
@@ -191,8 +218,10 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
             }
         }
     }
+    int nsum = 0;  // digits summed since the last fold (big primes fold every 4)
 #pragma unroll 1
     for (int j = 0; j < beta; j++) {
+        if (PROD && j == own) continue;  // in the prologue (block-uniform)
         // the key digit's words are loaded first: they arrive while the row NTT computes
         const u64* kp = key + (long)j * kdig + ((long)pid << LOGN) + (long)row * 256 + L;
         u64 kbw[8], kaw[8];
@@ -221,7 +250,7 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
                 a1[g][r] += fmul_rem(v[r], ka, ka * qi, q);
             }
         }
-        if (big && (j & 3) == 3) {
+        if (big && (++nsum & 3) == 0) {
 #pragma unroll
             for (int g = 0; g < G; g++)
 #pragma unroll

@@ -313,9 +313,11 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
 }
 
 // Inverse, row pass (Gentleman-Sande, distances 1..128 within rows): canonical u64 in (src),
-// raw doubles out (dst).
-template <int RR = 256>
-__global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Tabs T) {
+// raw doubles out (dst).  PROD: the input is the product src (x) src2 mod q of two canonical
+// operands (the d2 = a1 b1 term of a ciphertext product, computed here instead of being written
+// by a tensor kernel and read back; src2 has src's shape).
+template <int RR = 256, bool PROD = false>
+__global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Tabs T, Span src2) {
     __shared__ double s[16 * 16 * kPadF];
     int pid;
     const u64* in = span_ptr(src, blockIdx.y, T.logN, T.Lp1, pid);
@@ -328,10 +330,21 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
     const u64* gb = in + (long)blockIdx.x * 16 * 256;
     {  // wave w loads its rows 4w .. 4w + 3 (coalesced), element e = 1024 w + 64 k + lane
         const int e0 = (tid >> 6) * 1024 + (tid & 63);
+        if (PROD) {
+            int pid2;
+            const u64* gb2 = span_ptr(src2, blockIdx.y, T.logN, T.Lp1, pid2) + (long)blockIdx.x * 16 * 256;
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int e = e0 + 64 * k;
-            s[row_tile_idx(e)] = u2d(gb[e]);
+            for (int k = 0; k < 16; k++) {
+                const int e = e0 + 64 * k;
+                const double y = u2d(gb2[e]);
+                s[row_tile_idx(e)] = u2d(fcanon(fmul_rem(u2d(gb[e]), y, y * qi, q), q, qi));
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int e = e0 + 64 * k;
+                s[row_tile_idx(e)] = u2d(gb[e]);
+            }
         }
     }
     wave_sync_lds();
