@@ -252,3 +252,31 @@ def test_linear_bsgs_bit_exact(product_lib, oracle_lib, gpu_available, kw):
                for d, tl in plan)
     assert outs[0][0].level == kw["max_level"] - 1
     np.testing.assert_allclose(g.decrypt(outs[0][0], outs[0][1]), want, atol=1e-5)
+
+
+@pytest.mark.parametrize("log_n", [16, 17])
+def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
+    """The fused-NTT engines' ciphertext product (N = 2^16 / 2^17: d2 = a1 b1 formed in the INTT
+    copy-in, d0 / d1 and the own digit's term in the key-switch prologue; no tensor ciphertext):
+    K = 3 over 7 limbs (a partial last digit), a batch x broadcast product at mismatched levels
+    (one operand level-downed first), a square, and products at every level down to 1 -- all
+    residue for residue against the oracle's tensor + relinearise + rescale."""
+    kw = dict(log_n=log_n, max_level=6, special_primes=3, seed=21)
+    g, o = _pair(product_lib, oracle_lib, **kw)
+    rng = np.random.default_rng(9)
+    z = rng.uniform(-1, 1, (3, g.slot_count))
+    w = rng.uniform(-1, 1, g.slot_count)
+    res, sks = [], []
+    for eng in (g, o):
+        k = _keys(eng)
+        a, b = eng.encrypt(z, k["pk"], level=6), eng.encrypt(w, k["pk"], level=5)
+        out = [eng.multiply(a, b, k["rlk"]), eng.multiply(b, a, k["rlk"]), eng.multiply(b, b, k["rlk"])]
+        x = a
+        while x.level >= 1:
+            x = eng.multiply(x, a, k["rlk"])
+            out.append(x)
+        res.append(out)
+        sks.append(k["sk"])
+    for cg, co in zip(*res):
+        _same(g, o, cg, co)
+    np.testing.assert_allclose(g.decrypt(res[0][0], sks[0]), z * w, atol=1e-5)
