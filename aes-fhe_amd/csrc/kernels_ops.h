@@ -22,9 +22,13 @@ struct Opnd {
     int np;
 };
 
+// Absent operands read this zero word: the address is selected, not the load, so a kernel's
+// operand loads carry no branch and issue together (a branch per opnd_get put every load
+// behind its own wait).
+__device__ const u64 kZeroWord = 0;
 __device__ __forceinline__ u64 opnd_get(const Opnd& o, int b, int p, int l, int k, int logN) {
-    if (!o.ptr || p >= o.np) return 0;
-    return o.ptr[(long)b * o.bs + (long)p * o.ps + ((long)l << logN) + k];
+    const bool has = o.ptr && p < o.np;
+    return *(has ? o.ptr + (long)b * o.bs + (long)p * o.ps + ((long)l << logN) + k : &kZeroWord);
 }
 
 struct Out {

@@ -180,14 +180,18 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
 #pragma unroll
         for (int r = 0; r < 8; r++) a0[g][r] = a1[g][r] = 0.0;
         if (bb >= B) continue;
+        // operand words at (limb t, row, L + 32 r): base pointers formed once (block-uniform
+        // checks), so the 8 loads of each stream issue together (an opnd_get per element put
+        // every load behind its own branch and serialised the prologue)
         if (PROD && t <= l) {
             const double f = pmodf[t], w = tw_w(f, q);
             const u64* kp = key + (long)own * kdig + ((long)pid << LOGN) + (long)row * 256 + L;
+            const u64* xa = addend.ptr + (long)bb * addend.bs + roff;
+            const u64* xb = pb.ptr + (long)bb * pb.bs + roff;
 #pragma unroll
             for (int r = 0; r < 8; r++) {
-                const int kk = row * 256 + L + 32 * r;
-                const double x0 = u2d(opnd_get(addend, bb, 0, t, kk, LOGN)), x1 = u2d(opnd_get(addend, bb, 1, t, kk, LOGN));
-                const double y0 = u2d(opnd_get(pb, bb, 0, t, kk, LOGN)), y1 = u2d(opnd_get(pb, bb, 1, t, kk, LOGN));
+                const double x0 = u2d(xa[32 * r]), x1 = u2d(xa[addend.ps + 32 * r]);
+                const double y0 = u2d(xb[32 * r]), y1 = u2d(xb[pb.ps + 32 * r]);
                 const double kb = u2d(kp[32 * r]), ka = u2d(kp[32 * r + kcomp]);
                 const double y0q = y0 * qi, y1q = y1 * qi;
                 const double p0 = fmul_rem(x0, y0, y0q, q);
@@ -200,13 +204,16 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
                     a1[g][r] = fred(a1[g][r], q, qi);
                 }
             }
-        } else if (!PROD && pmodf && t <= l) {
+        } else if (!PROD && pmodf && t <= l && addend.ptr) {
             const double f = pmodf[t], w = tw_w(f, q);
+            const u64* xa = addend.ptr + (long)bb * addend.bs + roff;
+            if (addend.np > 0) {
 #pragma unroll
-            for (int r = 0; r < 8; r++) {
-                const int kk = row * 256 + L + 32 * r;
-                a0[g][r] = fmul_rem(u2d(opnd_get(addend, bb, 0, t, kk, LOGN)), w, f, q);
-                a1[g][r] = fmul_rem(u2d(opnd_get(addend, bb, 1, t, kk, LOGN)), w, f, q);
+                for (int r = 0; r < 8; r++) a0[g][r] = fmul_rem(u2d(xa[32 * r]), w, f, q);
+            }
+            if (addend.np > 1) {
+#pragma unroll
+                for (int r = 0; r < 8; r++) a1[g][r] = fmul_rem(u2d(xa[addend.ps + 32 * r]), w, f, q);
             }
         }
         if (accum) {
