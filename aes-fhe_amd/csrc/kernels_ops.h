@@ -25,12 +25,7 @@ struct Opnd {
 // Absent operands read this zero word: the address is selected, not the load, so a kernel's
 // operand loads carry no branch and issue together (a branch per opnd_get put every load
 // behind its own wait).
-__device__ u64 kZeroWord = 0;  // global address space: the selected pointer stays a global (not flat) load
-// A load through a pointer read from a device array (generic to the compiler): as a global load,
-// not a flat one (flat loads also count on lgkmcnt, so every scalar-constant wait in the same
-// kernel waited for them too).
-typedef const u64 __attribute__((address_space(1)))* gptr_t;
-__device__ __forceinline__ u64 ldg(const u64* p) { return *(gptr_t)p; }
+__device__ const u64 kZeroWord = 0;
 __device__ __forceinline__ u64 opnd_get(const Opnd& o, int b, int p, int l, int k, int logN) {
     const bool has = o.ptr && p < o.np;
     return *(has ? o.ptr + (long)b * o.bs + (long)p * o.ps + ((long)l << logN) + k : &kZeroWord);
@@ -163,7 +158,7 @@ __global__ void k_lincomb(const u64* const* __restrict__ ptrs, const long* __res
 #pragma unroll
         for (int c = 0; c < 8; c++) {
             const int i = i0 + c;
-            v[c] = ldg((i < n && p < npi[i]) ? ptrs[i] + (long)bb * bstr[i] + (long)p * pss[i] + off : &kZeroWord);
+            v[c] = (i < n && p < npi[i]) ? ptrs[i][(long)bb * bstr[i] + (long)p * pss[i] + off] : 0;
         }
 #pragma unroll
         for (int c = 0; c < 8; c++) {
@@ -194,7 +189,7 @@ __global__ void k_lincomb_many(const u64* const* __restrict__ ptrs, const long* 
     u64 v[kManyMax];
 #pragma unroll
     for (int j = 0; j < kManyMax; j++)
-        v[j] = ldg((j < n && p < npi[j]) ? ptrs[j] + (long)bb * bstr[j] + (long)p * pss[j] + off : &kZeroWord);
+        v[j] = (j < n && p < npi[j]) ? ptrs[j][(long)bb * bstr[j] + (long)p * pss[j] + off] : 0;
     u64* o = out + (long)bb * obs + ((long)p * nl << logN) + off;
     for (int i = 0; i < m; i++) {
         u64 acc = 0;
@@ -225,7 +220,7 @@ __global__ void k_dot(const u64* const* __restrict__ ap, const long* __restrict_
     for (int i = 0; i < n; i++) {
         const u64* a = ap[i] + (long)bb * abs_[i] + off;
         const u64* b = bp[i] + (long)bb * bbs[i] + off;
-        const u64 a0 = ldg(a), a1 = ldg(a + ps), b0 = ldg(b), b1 = ldg(b + ps);
+        const u64 a0 = a[0], a1 = a[ps], b0 = b[0], b1 = b[ps];
         d0 += mul_m(a0, b0, q, qi);
         d1 += mul_m(a0, b1, q, qi) + mul_m(a1, b0, q, qi);
         d2 += mul_m(a1, b1, q, qi);
@@ -429,12 +424,11 @@ __global__ void k_ks_inner_multi(const u64* __restrict__ d, long dbs, const u64*
         for (int ii = 0; ii < KC; ii++) {
 #pragma unroll
             for (int j = 0; j < BM; j++) {
-                kb[ii][j] = ka[ii][j] = 0.0;
-                if (i0 + ii < nk && j < beta) {
-                    const long ko = (long)j * kdig + ((long)pid << logN) + k;
-                    kb[ii][j] = u2d(ldg(keys[i0 + ii] + ko));
-                    ka[ii][j] = u2d(ldg(keys[i0 + ii] + ko + kcomp));
-                }
+                // absent keys / digits read the zero word (address select, no branch per load)
+                const bool ok = i0 + ii < nk && j < beta;
+                const u64* kp = keys[ok ? i0 + ii : 0] + (long)j * kdig + ((long)pid << logN) + k;
+                kb[ii][j] = u2d(*(ok ? kp : &kZeroWord));
+                ka[ii][j] = u2d(*(ok ? kp + kcomp : &kZeroWord));
             }
         }
 #pragma unroll 1
@@ -442,9 +436,9 @@ __global__ void k_ks_inner_multi(const u64* __restrict__ d, long dbs, const u64*
             double e[BM];
 #pragma unroll
             for (int j = 0; j < BM; j++)
-                e[j] = j < beta ? u2d((j == own) ? d[(long)bb * dbs + ((long)t << logN) + k]
-                                                 : ext[(long)j * exj + (long)bb * exs + ((long)t << logN) + k])
-                                : 0.0;
+                e[j] = u2d(*(j >= beta ? &kZeroWord
+                             : (j == own) ? d + (long)bb * dbs + ((long)t << logN) + k
+                                          : ext + (long)j * exj + (long)bb * exs + ((long)t << logN) + k));
             double ad0 = 0.0, ad1 = 0.0;
             if (pm) {
                 ad0 = fmul_rem(u2d(opnd_get(addend, bb, 0, t, k, logN)), fw, f, q);
@@ -766,8 +760,8 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
         y0[j] = y1[j] = 0.0;
         if (j < ny - 1) {
             const u64* p = yp[j] + (long)bb * ybs[j] + off;
-            y0[j] = u2d(ldg(p));
-            y1[j] = u2d(ldg(p + yps[j]));
+            y0[j] = u2d(p[0]);
+            y1[j] = u2d(p[yps[j]]);
         }
     }
     double d0[kPoly2Out], d1[kPoly2Out], d2[kPoly2Out];
@@ -779,8 +773,8 @@ __global__ void __launch_bounds__(256) k_poly2(const u64* const* __restrict__ xp
         double xa = 0.0, xb = 0.0;
         if (i > 0) {
             const u64* p = xp[i - 1] + (long)bb * xbs[i - 1] + off;
-            xa = u2d(ldg(p));
-            xb = u2d(ldg(p + xps[i - 1]));
+            xa = u2d(p[0]);
+            xb = u2d(p[xps[i - 1]]);
         }
 #pragma unroll
         for (int t = 0; t < kPoly2Out; t++) {
@@ -872,8 +866,8 @@ __global__ void __launch_bounds__(256, MO > 4 ? 2 : 3) k_poly2_int(const u64* co
             if (j < nyv - 1) {
                 const u64* p = yp[j] + (long)bb * ybs[j] + off;
                 const TwD r = Rc[ycls[j + 1]];
-                y0[j] = fred(fmul_rem_r(u2d(ldg(p)), r.w, r.wq, q), q, qi);
-                y1[j] = fred(fmul_rem_r(u2d(ldg(p + yps[j])), r.w, r.wq, q), q, qi);
+                y0[j] = fred(fmul_rem_r(u2d(p[0]), r.w, r.wq, q), q, qi);
+                y1[j] = fred(fmul_rem_r(u2d(p[yps[j]]), r.w, r.wq, q), q, qi);
             }
         }
         const double c0 = C0[(size_t)l * cxn + c];
@@ -882,8 +876,8 @@ __global__ void __launch_bounds__(256, MO > 4 ? 2 : 3) k_poly2_int(const u64* co
         double xa = 0.0, xb = 0.0;
         if (i > 0) {
             const u64* p = xp[i - 1] + (long)bb * xbs[i - 1] + off;
-            xa = u2d(ldg(p));
-            xb = u2d(ldg(p + xps[i - 1]));
+            xa = u2d(p[0]);
+            xb = u2d(p[xps[i - 1]]);
         }
 #pragma unroll
         for (int t = 0; t < MO; t++) {
@@ -976,8 +970,8 @@ __global__ void k_dot_pt(const u64* const* __restrict__ cp, const long* __restri
         double cv[8], wv[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            cv[u] = u2d(ldg(cp[i + u] + (long)bb * cbs[i + u] + (long)p * cps + off));
-            wv[u] = u2d(ldg(pp[i + u] + off));
+            cv[u] = u2d(cp[i + u][(long)bb * cbs[i + u] + (long)p * cps + off]);
+            wv[u] = u2d(pp[i + u][off]);
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
@@ -986,8 +980,8 @@ __global__ void k_dot_pt(const u64* const* __restrict__ cp, const long* __restri
         }
     }
     for (; i < n; i++) {
-        const double c = u2d(ldg(cp[i] + (long)bb * cbs[i] + (long)p * cps + off));
-        const double w = u2d(ldg(pp[i] + off));
+        const double c = u2d(cp[i][(long)bb * cbs[i] + (long)p * cps + off]);
+        const double w = u2d(pp[i][off]);
         acc += fmul_rem(c, w, w * qi, q);
         if ((i & 3) == 3) acc = fred(acc, q, qi);
     }
@@ -1056,7 +1050,7 @@ __global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64*
         if (g > 1) src = __brev((unsigned)((((g * ek) & (M - 1)) - 1) >> 1)) >> (32 - logN);
         double e[BCT];
 #pragma unroll
-        for (int u = 0; u < BCT; u++) e[u] = u2d(ldg(ep[i] + base[u] + src));
+        for (int u = 0; u < BCT; u++) e[u] = u2d(ep[i][base[u] + src]);
         // every giant's plaintext word is requested before the first product (a load behind
         // each pointer test serialised the GM loads)
         const u64* pj[GM];
@@ -1064,7 +1058,7 @@ __global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64*
 #pragma unroll
         for (int j = 0; j < GM; j++) pj[j] = j < ng ? pt[j * nb + i] : nullptr;
 #pragma unroll
-        for (int j = 0; j < GM; j++) wv[j] = u2d(ldg(pj[j] ? pj[j] + po : &kZeroWord));
+        for (int j = 0; j < GM; j++) wv[j] = pj[j] ? u2d(pj[j][po]) : 0.0;
 #pragma unroll
         for (int j = 0; j < GM; j++) {
             if (pj[j]) {
