@@ -677,7 +677,9 @@ static void build_tables(aesfhe_engine* e) {
                     for (int i2 = lo; i2 < hi; i2++)
                         if (i2 != i) h = h_mulmod(h, Q[i2] % qt, qt);
                     hhat[(set * K + (i - lo)) * np + pid] = h;
-                    hhatf[(set * K + (i - lo)) * np + pid] = TwD{(double)h, (double)h / (double)qt};
+                    // [set][target pid][i]: a target's alpha constants are contiguous (one
+                    // scalar base, immediate offsets in k_modup)
+                    hhatf[(set * np + pid) * K + (i - lo)] = TwD{(double)h, (double)h / (double)qt};
                 }
             }
         }
@@ -701,7 +703,7 @@ static void build_tables(aesfhe_engine* e) {
             for (int k2 = 0; k2 < K; k2++)
                 if (k2 != k) h = h_mulmod(h, Q[Lp1 + k2] % qi, qi);
             hphat[(size_t)k * Lp1 + i] = h;
-            hphatf[(size_t)k * Lp1 + i] = TwD{(double)h, (double)h / (double)qi};
+            hphatf[(size_t)i * K + k] = TwD{(double)h, (double)h / (double)qi};  // [target i][source k]
         }
     }
     for (int i = 0; i < Lp1; i++) {
@@ -728,7 +730,7 @@ static void build_tables(aesfhe_engine* e) {
     }
     // combined ModDown + rescale: E = {q_{l-r+1}..q_l, p_0..p_{K-1}} (acc limb order), D = prod E
     //   mdr_invf[(r-1, l)][j]       = (D/e_j)^{-1} mod e_j, as w/e_j
-    //   mdr_hatf[(r-1, l)][j][i]    = (D/e_j) mod q_i, as {w, w/q_i}   (i <= l - r)
+    //   mdr_hatf[(r-1, l)][i][j]    = (D/e_j) mod q_i, as {w, w/q_i}   (i <= l - r)
     //   mdr_dinv[(r-1, l)][i] (+f)  = D^{-1} mod q_i
     {
         const size_t cells = (size_t)kMdrMaxR * Lp1;
@@ -754,7 +756,7 @@ static void build_tables(aesfhe_engine* e) {
                         u64 h = 1;
                         for (size_t j2 = 0; j2 < E.size(); j2++)
                             if (j2 != j) h = h_mulmod(h, Q[E[j2]] % qi, qi);
-                        hhatf[(cell * kMdrMaxE + j) * Lp1 + i] = TwD{(double)h, (double)h / (double)qi};
+                        hhatf[(cell * Lp1 + i) * kMdrMaxE + j] = TwD{(double)h, (double)h / (double)qi};  // [cell][target i][source j]
                     }
                 }
                 for (int i = 0; i <= l - r; i++) {
@@ -1801,7 +1803,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
             if (alpha < 1 || alpha > 16) throw_err(AESFHE_EUNSUPPORTED, "ModUp digit width outside 1..16");
             AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, 1, B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
                               (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
-                              e->np, e->q, e->qinv, e->Lp1, e->logN);
+                              K, e->q, e->qinv, e->Lp1, e->logN);
         }
         HIPC(hipGetLastError());
         auto fwd = [&](Span sp, int total) {
@@ -1872,6 +1874,7 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
     const size_t cell = r ? (size_t)(r - 1) * e->Lp1 + l : 0;
     const double* invf = r ? e->mdr_invf + cell * kMdrMaxE : e->md_phatinvf;
     const TwD* hatf = r ? e->mdr_hatf + cell * kMdrMaxE * e->Lp1 : e->md_phatf;
+    const int hs = r ? kMdrMaxE : K;  // hatf row stride (sources of one target)
     const u64* dinv = r ? e->mdr_dinv + cell * e->Lp1 : e->md_pinv;
     const double* dinvf = r ? e->mdr_dinvf + cell * e->Lp1 : e->md_pinvf;
     Tmp conv(e, (size_t)B * 2 * kN);
@@ -1880,7 +1883,7 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
         if (K + r < 1 || K + r > 16) throw_err(AESFHE_EUNSUPPORTED, "ModDown source width outside 1..16");
         AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, 1, B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN,
                            invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv,
-                           r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN);
+                           r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN, hs);
     }
     HIPC(hipGetLastError());
     Span sc = span_s(conv.p, kN, lk + 1, lk + 1, 0, e->Lp1);

@@ -281,7 +281,8 @@ __global__ void k_rescale_finish_g(const u64* __restrict__ c, long cps, const u6
 // the extended basis (Q_l then P), exact fp64 arithmetic (kernels.h fmul_rem):
 //   y_i = [x_i * qhat_i^{-1}]_{q_i} in [0, q_i) (canonical, so the multiple of Q that the fast
 //   conversion adds is the oracle's), ext[t] = sum_i y_i * (qhat_i mod p_t) mod p_t.
-// Constants: hatinv as w/q (w = rint(wq * q) is exact), hat as {w, w/q}.  grid (N/256,
+// Constants: hatinv as w/q (w = rint(wq * q) is exact), hat as {w, w/q}, [target pid][i] with
+// row stride hs.  grid (N/256,
 // ceil(ne/16), B): each thread converts one coefficient into up to 16 target limbs.
 // A = alpha (digit width) as a template parameter: the per-target constant loads are then
 // unconditional and the compiler issues all A of them before the first use (with a runtime
@@ -289,7 +290,7 @@ __global__ void k_rescale_finish_g(const u64* __restrict__ c, long cps, const u6
 template <int A, int C>  // C coefficients per thread (k + 256 c): every constant fetched serves C
 __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ ext, long exs,
                         int lo, int l, int ne, const double* __restrict__ hatinvf,
-                        const TwD* __restrict__ hat, int np, const u64* __restrict__ qall,
+                        const TwD* __restrict__ hat, int hs, const u64* __restrict__ qall,
                         const double* __restrict__ qinvall, int Lp1, int logN) {
     const int k = blockIdx.x * (256 * C) + threadIdx.x;
     const int bb = blockIdx.z;
@@ -313,7 +314,7 @@ __global__ void k_modup(const u64* __restrict__ dc, long dcs, u64* __restrict__ 
         const double qt = (double)qall[pid], qti = qinvall[pid];
         TwD f[A];
 #pragma unroll
-        for (int i = 0; i < A; i++) f[i] = hat[i * np + pid];
+        for (int i = 0; i < A; i++) f[i] = hat[pid * hs + i];  // [target][source]: contiguous
         double acc[C];
 #pragma unroll
         for (int c = 0; c < C; c++) acc[c] = 0.0;
@@ -478,7 +479,7 @@ __global__ void k_ks_inner_multi(const u64* __restrict__ d, long dbs, const u64*
 // r >= 1 makes the conversion exact: v = rint(sum_j y_j * (1/e_j)) (fp64, j in order) counts the
 // multiples of D in sum_j y_j (D/e_j), and conv[i] -= v * (D mod q_i), so the division rounds to
 // nearest like a plain rescale (einv[j] = 1/e_j, dmodf[i] = (D mod q_i)/q_i).
-// invf[j]: w/q table, hat[j * Lp1 + i]: {w, w/q}.  grid (N/256, ceil((l-r+1)/16), B*2)
+// invf[j]: w/q table, hat[i * hs + j]: {w, w/q}.  grid (N/256, ceil((l-r+1)/16), B*2)
 // NE = K + r (dropped limbs) as a template parameter, for the same reason as k_modup's A.
 template <int NE>
 __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int l, int r,
@@ -486,7 +487,7 @@ __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int 
                           const double* __restrict__ invf, const TwD* __restrict__ hat,
                           const double* __restrict__ einv, const double* __restrict__ dmodf,
                           int Lp1, const u64* __restrict__ qall, const double* __restrict__ qinvall,
-                          int logN) {
+                          int logN, int hs) {
     // two coefficients per thread (k, k + 256), as k_modup
     const int k = blockIdx.x * 512 + threadIdx.x;
     const int bb = blockIdx.z >> 1, c = blockIdx.z & 1;
@@ -520,7 +521,7 @@ __global__ void k_moddown(const u64* __restrict__ acc, long abs_, long acs, int 
         const double fd = dmodf[i], wd = tw_w(fd, q);
         TwD f[NE];
 #pragma unroll
-        for (int j = 0; j < NE; j++) f[j] = hat[j * Lp1 + i];
+        for (int j = 0; j < NE; j++) f[j] = hat[i * hs + j];  // [target][source]: contiguous
         double sum = fmul_rem(-v, wd, fd, q), sum2 = fmul_rem(-v2, wd, fd, q);
         const bool fold = q >= kBigPrime;  // as k_modup: small targets sum NE + 1 terms unfolded
 #pragma unroll
