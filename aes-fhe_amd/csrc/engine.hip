@@ -516,7 +516,7 @@ static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse
     {
         ProfScope ps(e, FAM_NTT, by);
         if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_cols<R>, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
-        else hipLaunchKernelGGL((k_nttf_inv_rows<R, false>), dim3(R / 16, total), dim3(256), 0, e->stream, src, dst, T, Span{});
+        else hipLaunchKernelGGL((k_nttf_inv_rows<R, false>), dim3(R / 16, total), dim3(256), 0, e->stream, src, dst, T, Span{}, (const u64*)nullptr);
     }
     ProfScope ps(e, FAM_NTT, by);
     if (!inverse) hipLaunchKernelGGL((k_nttf_fwd_rows_t<false, R>), dim3(R / 16, total), dim3(256), 0, e->stream, dst, T, RowFin{});
@@ -528,14 +528,19 @@ static bool fused_ntt(const aesfhe_engine* e) { return e->logN == 16 || e->logN 
 
 // inverse NTT of the product a (x) b (two canonical operand spans of one shape) into dst, the
 // product formed in the row pass's copy-in (fused_ntt engines)
-static void intt_prod(aesfhe_engine* e, Span a, Span b, Span dst, int total) {
+static void intt_prod(aesfhe_engine* e, Span a, Span b, Span dst, int total, const u64* fac) {
     if (total <= 0) return;
     Tabs T = e->tabs();
     const double by = 8.0 * e->N * (double)total;
     {
         ProfScope ps(e, FAM_NTT, 2.0 * by);  // two operands read
-        if (e->logN == 16) hipLaunchKernelGGL((k_nttf_inv_rows<256, true>), dim3(16, total), dim3(256), 0, e->stream, a, dst, T, b);
-        else hipLaunchKernelGGL((k_nttf_inv_rows<512, true>), dim3(32, total), dim3(256), 0, e->stream, a, dst, T, b);
+        if (e->logN == 16) {
+            if (fac) hipLaunchKernelGGL((k_nttf_inv_rows<256, true, true>), dim3(16, total), dim3(256), 0, e->stream, a, dst, T, b, fac);
+            else hipLaunchKernelGGL((k_nttf_inv_rows<256, true, false>), dim3(16, total), dim3(256), 0, e->stream, a, dst, T, b, fac);
+        } else {
+            if (fac) hipLaunchKernelGGL((k_nttf_inv_rows<512, true, true>), dim3(32, total), dim3(256), 0, e->stream, a, dst, T, b, fac);
+            else hipLaunchKernelGGL((k_nttf_inv_rows<512, true, false>), dim3(32, total), dim3(256), 0, e->stream, a, dst, T, b, fac);
+        }
     }
     ProfScope ps(e, FAM_NTT, by);
     if (e->logN == 16) hipLaunchKernelGGL(k_nttf_inv_cols<256>, dim3(16, total), dim3(256), 0, e->stream, dst, T);
@@ -1779,7 +1784,7 @@ static int ks_beta(const aesfhe_engine* e, int l) {
 // runs inside k_nttf_rows_ks together with the inner product (ks_fused.h).
 // pa, pb (fused_ntt engines): the input is poly 1 of each, multiplied (d2 = a1 b1 of a product)
 static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64* ext, bool cols_only = false,
-                     const Opnd* pa = nullptr, const Opnd* pb = nullptr) {
+                     const Opnd* pa = nullptr, const Opnd* pb = nullptr, const u64* fac = nullptr) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long lN = (long)(l + 1) * N, neN = (long)ne * N;
     const int beta = ks_beta(e, l);
@@ -1788,7 +1793,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
     Span sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
     if (pa) {
         intt_prod(e, span_s((u64*)pa->ptr + pa->ps, pa->bs, l + 1, l + 1, 0, e->Lp1),
-                  span_s((u64*)pb->ptr + pb->ps, pb->bs, l + 1, l + 1, 0, e->Lp1), sdc, B * (l + 1));
+                  span_s((u64*)pb->ptr + pb->ps, pb->bs, l + 1, l + 1, 0, e->Lp1), sdc, B * (l + 1), fac);
     } else {
         Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1);
         ntt(e, sd, sdc, B * (l + 1), true);
@@ -1831,7 +1836,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
 // PROD; d unused).
 static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, int B, int l,
                          const aesfhe_key* k, Opnd addend, bool pmod, u64* acc, bool ext_cols, bool accum = false,
-                         const Opnd* pb = nullptr) {
+                         const Opnd* pb = nullptr, const u64* fac = nullptr, const Opnd* pc = nullptr) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long neN = (long)ne * N;
     const int beta = ks_beta(e, l);
@@ -1842,13 +1847,14 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
         // (key read once per call, accumulators written; ext never leaves the chip) + the Q-limb
         // operands: the own digit's d limbs and the addend (PROD: a0, a1, b0, b1)
         const int nown = std::min(l + 1, beta * K);
-        const double opw = pb ? 4.0 * (l + 1) : (double)nown + (pmod && addend.ptr ? (double)addend.np * (l + 1) : 0.0);
+        const double opw = pb ? (4.0 + (pc && pc->ptr ? 2.0 : 0.0)) * (l + 1)
+                              : (double)nown + (pmod && addend.ptr ? (double)addend.np * (l + 1) : 0.0);
         ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown + opw) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))));
         const int R = N / 256, blocks = 8 * B * (ne * (R / 8) / 8);
         const Opnd none{nullptr, 0, 0, 0};
         auto kern = pb ? (R == 256 ? k_nttf_rows_ks<1, 256, true> : k_nttf_rows_ks<1, 512, true>)
                        : (R == 256 ? k_nttf_rows_ks<1, 256, false> : k_nttf_rows_ks<1, 512, false>);
-        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum, pb ? *pb : none);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum, pb ? *pb : none, fac, pc ? *pc : none);
     } else {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B * (accum ? 2 : 1)));
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
@@ -1936,15 +1942,17 @@ static void keyswitch(aesfhe_engine* e, const u64* d, long dbs, int B, int l, co
 // d0, d1 and the own digit's d2 term in the prologue of k_nttf_rows_ks (PROD).  Same residues
 // as tensor_ct + relin_rescale; the 3-polynomial tensor (3 limbs written, 3 read back, per
 // Q limb) never reaches HBM.
+// fac / pc (optional): the multiply-add of aesfhe_mul_fma, per-prime {alpha, C, K} (device) and
+// the addend ciphertext c (truncated to level l).
 static void keyswitch_prod(aesfhe_engine* e, const Opnd& pa, const Opnd& pb, int B, int l, const aesfhe_key* k,
-                           aesfhe_ct* o, int r) {
+                           aesfhe_ct* o, int r, const u64* fac = nullptr, const Opnd* pc = nullptr) {
     if (!fused_ntt(e) || r < 1 || pa.np != 2 || pb.np != 2 || !pa.ptr || !pb.ptr)
         throw_err(AESFHE_EARG, "product key switch outside the fused combined path");
     const long neN = (long)(l + 1 + e->K) * e->N;
     Tmp ext(e, (size_t)ks_beta(e, l) * B * neN);
-    ks_modup(e, nullptr, 0, B, l, ext.p, true, &pa, &pb);
+    ks_modup(e, nullptr, 0, B, l, ext.p, true, &pa, &pb, fac);
     Tmp acc(e, (size_t)B * 2 * neN);
-    ks_inner_acc(e, nullptr, 0, ext.p, B, l, k, pa, true, acc.p, true, false, &pb);
+    ks_inner_acc(e, nullptr, 0, ext.p, B, l, k, pa, true, acc.p, true, false, &pb, fac, pc);
     moddown_acc(e, acc.p, B, l, r, Opnd{nullptr, 0, 0, 0}, o);
 }
 
@@ -2082,6 +2090,18 @@ extern "C" int aesfhe_mul_fma(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe
     }
     u64* dfac = upload_small(e, fac.data(), fac.size());
     const Opnd none{nullptr, 0, 0, 0};
+    if (prod && fused_ntt(e) && e->K + 1 <= kMdrMaxE) {  // tensor-free (keyswitch_prod with the fma factors)
+        aesfhe_ct* r = ct_new(e, B, 2, l - 1);
+        try {
+            const Opnd oc = hasc ? opnd(trunc_view(c, l), B) : none;
+            keyswitch_prod(e, opnd(A.v, B), opnd(Bv.v, B), B, l, rlk, r, 1, dfac, &oc);
+        } catch (...) {
+            aesfhe_ct_free(r);
+            throw;
+        }
+        *out = r;
+        return AESFHE_OK;
+    }
     aesfhe_ct* t = ct_new(e, B, 3, l);
     {
         ProfScope ps(e, FAM_EW, 0);

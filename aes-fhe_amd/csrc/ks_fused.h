@@ -134,14 +134,17 @@ __device__ __forceinline__ void row_ntt8_stages(double (&x)[8], double* sr, int 
 // d1 = a0 b1 + a1 b0 (the addend, times P) and d2 = a1 b1 (the own digit's limb, times its key
 // words), so the own digit is skipped in the loop; addend = a, d = unused, pb = b.  Products
 // by fmul_rem with the on-the-fly quotient, as the key products: congruent, not canonical,
-// |x| < 3q before the P / key product.
+// |x| < 3q before the P / key product.  fac (optional; aesfhe_mul_fma): per-prime {alpha, C, K};
+// the product becomes alpha (a (x) b) + C (c0, c1, 0) + (K, 0, 0) (pc = c, absent: no C term),
+// |x| < 4.5q + K before the P / key product.
 template <int G, int R = 256, bool PROD = false>
 __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64* __restrict__ d, long dbs,
                                                       const u64* __restrict__ ext, long exs, long exj,
                                                       const u64* __restrict__ key, long kdig, long kcomp,
                                                       u64* __restrict__ acc, long abs_, long acs, int B,
                                                       int beta, int K, int l, int ne, Tabs T, Opnd addend,
-                                                      const double* __restrict__ pmodf, int accum, Opnd pb) {
+                                                      const double* __restrict__ pmodf, int accum, Opnd pb,
+                                                      const u64* __restrict__ fac, Opnd pc) {
     // one LDS array (row transposes, then the 8 rows' twiddles -- see row_ntt8_fwd's rt)
     __shared__ double s[8 * 288 + 8 * 256];
     const int nbg = (B + G - 1) / G;
@@ -188,15 +191,27 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
             const u64* kp = key + (long)own * kdig + ((long)pid << LOGN) + (long)row * 256 + L;
             const u64* xa = addend.ptr + (long)bb * addend.bs + roff;
             const u64* xb = pb.ptr + (long)bb * pb.bs + roff;
+            const u64* xc = pc.ptr ? pc.ptr + (long)bb * pc.bs + roff : xb;
+            const double fal = fac ? (double)fac[3 * t] : 0.0, fC = fac ? (double)fac[3 * t + 1] : 0.0,
+                         fK = fac ? (double)fac[3 * t + 2] : 0.0;
 #pragma unroll
             for (int r = 0; r < 8; r++) {
                 const double x0 = u2d(xa[32 * r]), x1 = u2d(xa[addend.ps + 32 * r]);
                 const double y0 = u2d(xb[32 * r]), y1 = u2d(xb[pb.ps + 32 * r]);
                 const double kb = u2d(kp[32 * r]), ka = u2d(kp[32 * r + kcomp]);
                 const double y0q = y0 * qi, y1q = y1 * qi;
-                const double p0 = fmul_rem(x0, y0, y0q, q);
-                const double p1 = fmul_rem(x0, y1, y1q, q) + fmul_rem(x1, y0, y0q, q);
-                const double p2 = fmul_rem(x1, y1, y1q, q);
+                double p0 = fmul_rem(x0, y0, y0q, q);
+                double p1 = fmul_rem(x0, y1, y1q, q) + fmul_rem(x1, y0, y0q, q);
+                double p2 = fmul_rem(x1, y1, y1q, q);
+                if (fac) {  // multiply-add: alpha (a (x) b) + C (c0, c1, 0) + (K, 0, 0)
+                    p0 = fmul_rem(p0, fal, fal * qi, q) + fK;
+                    p1 = fmul_rem(p1, fal, fal * qi, q);
+                    p2 = fmul_rem(p2, fal, fal * qi, q);
+                    if (pc.ptr) {
+                        p0 += fmul_rem(u2d(xc[32 * r]), fC, fC * qi, q);
+                        p1 += fmul_rem(u2d(xc[pc.ps + 32 * r]), fC, fC * qi, q);
+                    }
+                }
                 a0[g][r] = fmul_rem(p0, w, f, q) + fmul_rem(p2, kb, kb * qi, q);
                 a1[g][r] = fmul_rem(p1, w, f, q) + fmul_rem(p2, ka, ka * qi, q);
                 if (big) {

@@ -316,8 +316,11 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_rows_t(Span dst, Tabs T, RowFi
 // raw doubles out (dst).  PROD: the input is the product src (x) src2 mod q of two canonical
 // operands (the d2 = a1 b1 term of a ciphertext product, computed here instead of being written
 // by a tensor kernel and read back; src2 has src's shape).
-template <int RR = 256, bool PROD = false>
-__global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Tabs T, Span src2) {
+// FMA (with PROD): fac holds the per-prime {alpha, C, K} of a fused multiply-add (aesfhe_mul_fma)
+// and the product is alpha (src (x) src2).
+template <int RR = 256, bool PROD = false, bool FMA = false>
+__global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Tabs T, Span src2,
+                                                          const u64* __restrict__ fac) {
     __shared__ double s[16 * 16 * kPadF];
     int pid;
     const u64* in = span_ptr(src, blockIdx.y, T.logN, T.Lp1, pid);
@@ -333,11 +336,14 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
         if (PROD) {
             int pid2;
             const u64* gb2 = span_ptr(src2, blockIdx.y, T.logN, T.Lp1, pid2) + (long)blockIdx.x * 16 * 256;
+            const double al = FMA ? (double)fac[3 * pid] : 0.0;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 const int e = e0 + 64 * k;
                 const double y = u2d(gb2[e]);
-                s[row_tile_idx(e)] = u2d(fcanon(fmul_rem(u2d(gb[e]), y, y * qi, q), q, qi));
+                double v = fmul_rem(u2d(gb[e]), y, y * qi, q);
+                if (FMA) v = fmul_rem(v, al, al * qi, q);
+                s[row_tile_idx(e)] = u2d(fcanon(v, q, qi));
             }
         } else {
 #pragma unroll

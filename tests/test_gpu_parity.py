@@ -259,8 +259,9 @@ def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
     """The fused-NTT engines' ciphertext product (N = 2^16 / 2^17: d2 = a1 b1 formed in the INTT
     copy-in, d0 / d1 and the own digit's term in the key-switch prologue; no tensor ciphertext):
     K = 3 over 7 limbs (a partial last digit), a batch x broadcast product at mismatched levels
-    (one operand level-downed first), a square, and products at every level down to 1 -- all
-    residue for residue against the oracle's tensor + relinearise + rescale."""
+    (one operand level-downed first), a square, fused multiply-adds (alpha, a higher-level addend,
+    beta) and products at every level down to 1 -- all residue for residue against the oracle's
+    tensor + relinearise + rescale."""
     kw = dict(log_n=log_n, max_level=6, special_primes=3, seed=21)
     g, o = _pair(product_lib, oracle_lib, **kw)
     rng = np.random.default_rng(9)
@@ -270,7 +271,11 @@ def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
     for eng in (g, o):
         k = _keys(eng)
         a, b = eng.encrypt(z, k["pk"], level=6), eng.encrypt(w, k["pk"], level=5)
-        out = [eng.multiply(a, b, k["rlk"]), eng.multiply(b, a, k["rlk"]), eng.multiply(b, b, k["rlk"])]
+        out = [eng.multiply(a, b, k["rlk"]), eng.multiply(b, a, k["rlk"]), eng.multiply(b, b, k["rlk"]),
+               # fused multiply-adds (Chebyshev / double-angle steps): alpha, c at a higher level, beta
+               eng.multiply_fma(a, b, k["rlk"], alpha=2, c=a, gamma=-1.0, beta=-1.0),
+               eng.multiply_fma(b, b, k["rlk"], alpha=2, beta=-1.0),
+               eng.multiply_fma(b, a, k["rlk"], alpha=-3, c=b, gamma=0.5)]
         x = a
         while x.level >= 1:
             x = eng.multiply(x, a, k["rlk"])
