@@ -19,8 +19,12 @@ def load(path, counter):
             continue
         name = r["Kernel_Name"]
         for k in NTT:
-            if k.split("<")[0] in name and (("<" not in k) or k.split("<")[1][:-1] in name):
-                per[k].append((int(r["Grid_Size"]), float(r["Counter_Value"]) * 1024.0))
+            base = k.split("<")[0]
+            if (base + "<" + k.split("<")[1][:-1] if "<" in k else base) in name:
+                # the product INTT (k_nttf_inv_rows<R, true, ...>) reads two operands: 16 N
+                # algorithmic bytes per limb (bench.py / engine ProfScope credit it the same)
+                w = 2.0 if base == "k_nttf_inv_rows" and ", true" in name.split("(")[0] else 1.0
+                per[k].append((int(r["Grid_Size"]), float(r["Counter_Value"]) * 1024.0, w))
     return per
 
 
@@ -32,9 +36,9 @@ def main():
     for k in NTT:
         if not f.get(k):
             continue
-        rd = [2.0 * v for _, v in f[k]]
-        wr = [v for _, v in w.get(k, [])] or [0.0]
-        a = sum(8.0 * N * g / 4096 for g, _ in f[k])
+        rd = [2.0 * v for _, v, _ in f[k]]
+        wr = [v for _, v, _ in w.get(k, [])] or [0.0]
+        a = sum(8.0 * N * g / 4096 * x for g, _, x in f[k])
         hbm += sum(rd) + sum(wr) * len(rd) / len(wr)
         alg += a
         launches += len(rd)
