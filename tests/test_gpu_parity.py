@@ -285,3 +285,36 @@ def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
     for cg, co in zip(*res):
         _same(g, o, cg, co)
     np.testing.assert_allclose(g.decrypt(res[0][0], sks[0]), z * w, atol=1e-5)
+
+
+@pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=4, special_primes=2, seed=5)],
+                         ids=["n4096", "n65536"])
+def test_switching_key_export_bit_exact(product_lib, oracle_lib, gpu_available, kw):
+    """Relinearisation, conjugation and hoisted rotation keys: aesfhe_key_export returns
+    residues equal to the oracle's, and a saved + loaded key relinearises to the same residues."""
+    import ctypes as C
+    g, o = _pair(product_lib, oracle_lib, **kw)
+
+    def words(eng, key):
+        kind, gal, seed, n = C.c_int32(), C.c_uint64(), C.c_uint64(), C.c_int64()
+        eng._check(eng._lib.key_export(eng._h, key._h, C.byref(kind), C.byref(gal), C.byref(seed), C.byref(n), None))
+        out = np.empty(n.value, np.uint64)
+        eng._check(eng._lib.key_export(eng._h, key._h, C.byref(kind), C.byref(gal), C.byref(seed), C.byref(n),
+                                       out.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return out
+
+    kg, ko = _keys(g), _keys(o)
+    for name in ("rlk", "cjk"):
+        np.testing.assert_array_equal(words(g, kg[name]), words(o, ko[name]))
+    hg = g.create_hoisted_rotation_key(kg["sk"], -3)
+    ho = o.create_hoisted_rotation_key(ko["sk"], -3)
+    np.testing.assert_array_equal(words(g, hg), words(o, ho))
+    import tempfile, os
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "rlk.bin")
+        g.save(kg["rlk"], path)
+        rl2 = g.load(path)
+    rng = np.random.default_rng(12)
+    z = rng.uniform(-1, 1, g.slot_count)
+    cg, co = g.encrypt(z, kg["pk"]), o.encrypt(z, ko["pk"])
+    _same(g, o, g.multiply(cg, cg, rl2), o.multiply(co, co, ko["rlk"]))
