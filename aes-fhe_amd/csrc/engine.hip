@@ -1433,8 +1433,25 @@ extern "C" int aesfhe_decrypt(aesfhe_engine* e, const aesfhe_key* sk, const aesf
 // -----------------------------------------------------------------------------------------------
 // core primitives
 // rescale a view (level l >= 1) into a new ct at level l-1
-static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in) {
+// C != 1: rescale of C * in (the exact-scale level-down, level_down_view), the constant folded
+// into the spread (top limb) and the finish (every kept limb) instead of a k_mul_const pass.
+static void const_factors(aesfhe_engine* e, int64_t A, int64_t Bc, int nl, std::vector<u64>& f, std::vector<double>& ff);
+static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) {
     const int N = e->N, l = in.level, P = in.B * in.np;
+    const bool sc = C != 1;
+    u64* df = nullptr;
+    double* dff = nullptr;
+    u64 ctop = 1;
+    double ctopf = 0.0;
+    if (sc) {
+        std::vector<u64> f;
+        std::vector<double> ff;
+        const_factors(e, C, 0, l + 1, f, ff);
+        ctop = f[2 * l];
+        ctopf = ff[2 * l];
+        df = upload_small(e, f.data(), f.size());
+        dff = upload_small(e, ff.data(), ff.size());
+    }
     aesfhe_ct* r = ct_new(e, in.B, in.np, l - 1);
     Tmp x(e, (size_t)P * N), t(e, (size_t)P * l * N);
     // INTT of limb l of every poly: source poly p of batch b at d + b*bs + p*ps + l*N
@@ -1443,11 +1460,13 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in) {
     Span dx = span_s(x.p, N, 1, 1, l, e->Lp1);
     if (in.bs != (long)in.np * in.ps && in.B > 1) throw_err(AESFHE_EARG, "rescale of non-compact view");
     ntt(e, src, dx, P, true);
-    hipLaunchKernelGGL(k_rescale_spread, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN);
+    if (sc) hipLaunchKernelGGL(k_rescale_spread<true>, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN, ctop, ctopf);
+    else hipLaunchKernelGGL(k_rescale_spread<false>, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN, ctop, ctopf);
     Span st = span_s(t.p, (long)l * N, l, l, 0, e->Lp1);
     ntt(e, st, st, P * l, false);
     Opnd c = opnd(in, in.B);
-    hipLaunchKernelGGL(k_rescale_finish, dim3(N / 256, l, P), dim3(256), 0, e->stream, c, (const u64*)t.p, out_of(r), in.np, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN);
+    if (sc) hipLaunchKernelGGL(k_rescale_finish<true>, dim3(N / 256, l, P), dim3(256), 0, e->stream, c, (const u64*)t.p, out_of(r), in.np, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN, (const u64*)df, (const double*)dff);
+    else hipLaunchKernelGGL(k_rescale_finish<false>, dim3(N / 256, l, P), dim3(256), 0, e->stream, c, (const u64*)t.p, out_of(r), in.np, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN, (const u64*)nullptr, (const double*)nullptr);
     HIPC(hipGetLastError());
     return r;
 }
@@ -1463,7 +1482,7 @@ static std::vector<aesfhe_ct*> rescale_groups(aesfhe_engine* e, const u64* d, in
     Span src = span_s((u64*)d + (long)l * N, cps, 1, 1, l, e->Lp1);
     Span dx = span_s(x.p, N, 1, 1, l, e->Lp1);
     ntt(e, src, dx, P, true);
-    hipLaunchKernelGGL(k_rescale_spread, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN);
+    hipLaunchKernelGGL(k_rescale_spread<false>, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN, (u64)1, 0.0);
     Span st = span_s(t.p, (long)l * N, l, l, 0, e->Lp1);
     ntt(e, st, st, P * l, false);
     std::vector<u64*> op(G);
@@ -1524,11 +1543,7 @@ static aesfhe_ct* level_down_view(aesfhe_engine* e, const View& v, int lt) {
     if (v.zero) return ct_zero_new(e, v.B, v.np, lt);
     View t = truncated(v, lt + 1);
     int64_t C = llround(e->chain.scale[lt] * (double)e->chain.q[lt + 1] / e->chain.scale[v.level]);
-    aesfhe_ct* tmp = ct_new(e, v.B, v.np, lt + 1);
-    mul_const_into(e, t, C, 0, tmp, 0);
-    aesfhe_ct* r = rescale_view(e, view_of(tmp));
-    aesfhe_ct_free(tmp);
-    return r;
+    return rescale_view(e, t, C);  // C folded into the rescale's spread + finish (no k_mul_const pass)
 }
 
 // owned-or-borrowed aligned operand

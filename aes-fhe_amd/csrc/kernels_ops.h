@@ -239,26 +239,35 @@ __global__ void k_dot(const u64* const* __restrict__ ap, const long* __restrict_
 // ---------------------------------------------------------------------------------------------
 // rescale
 // t[P][i][k] = centered(x[P][k]) mod q_i for i < l ; grid (N/256, l, P)
+// SC (level-down fused into the rescale, level_down_view): the top limb is first multiplied by
+// the level-down constant sc = C mod q_l ({sc, scf = sc / q_l})
+template <bool SC = false>
 __global__ void k_rescale_spread(const u64* __restrict__ x, u64* __restrict__ t, u64 ql,
                                  const u64* __restrict__ qs, const double* __restrict__ qinv,
-                                 const u64* __restrict__ qlmod, int l, int logN) {
+                                 const u64* __restrict__ qlmod, int l, int logN, u64 sc, double scf) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = blockIdx.y, P = blockIdx.z;
     const u64 q = qs[i];
     u64 v = x[((long)P << logN) + k];
+    if (SC) v = mul_w(v, sc, scf, ql);
     u64 r = red_m(v, q, qinv[i]);
     if (v > (ql >> 1)) r = sub_m(r, qlmod[i], q);
     t[(((long)P * l + i) << logN) + k] = r;
 }
 
 // out[P][i] = (c[P][i] - t[P][i]) * q_l^{-1} ; grid (N/256, l, P) with P = b*np + p
+// SC: c is first multiplied by the level-down constant (f / ff: [2 i] = C mod q_i, w/q), the
+// residues k_mul_const would have written
+template <bool SC = false>
 __global__ void k_rescale_finish(Opnd c, const u64* __restrict__ t, Out o, int np, int l,
                                  const u64* __restrict__ qs, const u64* __restrict__ inv,
-                                 const double* __restrict__ invf, int logN) {
+                                 const double* __restrict__ invf, int logN, const u64* __restrict__ f,
+                                 const double* __restrict__ ff) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = blockIdx.y, P = blockIdx.z, bb = P / np, p = P - bb * np;
     const u64 q = qs[i];
     u64 cv = opnd_get(c, bb, p, i, k, logN);
+    if (SC) cv = mul_w(cv, f[2 * i], ff[2 * i], q);
     u64 tv = t[(((long)P * l + i) << logN) + k];
     o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)i << logN) + k] = mul_w(sub_m(cv, tv, q), inv[i], invf[i], q);
 }
