@@ -1441,6 +1441,7 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) 
     const bool sc = C != 1;
     u64* df = nullptr;
     double* dff = nullptr;
+    double* dff_c = nullptr;
     u64 ctop = 1;
     double ctopf = 0.0;
     if (sc) {
@@ -1451,6 +1452,9 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) 
         ctopf = ff[2 * l];
         df = upload_small(e, f.data(), f.size());
         dff = upload_small(e, ff.data(), ff.size());
+        std::vector<double> fc(l);  // per-limb w/q of C (RowFin::cf)
+        for (int i = 0; i < l; i++) fc[i] = ff[2 * i];
+        dff_c = upload_small(e, fc.data(), fc.size());
     }
     aesfhe_ct* r = ct_new(e, in.B, in.np, l - 1);
     Tmp x(e, (size_t)P * N), t(e, (size_t)P * l * N);
@@ -1463,6 +1467,22 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) 
     if (sc) hipLaunchKernelGGL(k_rescale_spread<true>, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN, ctop, ctopf);
     else hipLaunchKernelGGL(k_rescale_spread<false>, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN, ctop, ctopf);
     Span st = span_s(t.p, (long)l * N, l, l, 0, e->Lp1);
+    if (fused_ntt(e) && in.np == 2 && !in.zero) {
+        // the finish runs in the epilogue of t's row pass (the ModDown finish's RowFin with
+        // acc = the input, D = q_l, optional level-down constant): t never reaches HBM in NTT form
+        const int total = P * l;
+        {
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+            ntt_fwd_cols(e, st, total);
+        }
+        RowFin f{(const u64*)in.d, in.bs, in.ps, Opnd2{nullptr, 0, 0, 0}, r->d, 2L * l * N, (long)l * N,
+                 e->rs_invf + (size_t)l * e->Lp1, l, sc ? (const double*)dff_c : nullptr};
+        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total * 3.0);  // half an NTT + input read + output write
+        if (N == 65536) hipLaunchKernelGGL((k_nttf_fwd_rows_t<true, 256>), dim3(16, total), dim3(256), 0, e->stream, st, e->tabs(), f);
+        else hipLaunchKernelGGL((k_nttf_fwd_rows_t<true, 512>), dim3(32, total), dim3(256), 0, e->stream, st, e->tabs(), f);
+        HIPC(hipGetLastError());
+        return r;
+    }
     ntt(e, st, st, P * l, false);
     Opnd c = opnd(in, in.B);
     if (sc) hipLaunchKernelGGL(k_rescale_finish<true>, dim3(N / 256, l, P), dim3(256), 0, e->stream, c, (const u64*)t.p, out_of(r), in.np, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN, (const u64*)df, (const double*)dff);

@@ -178,6 +178,9 @@ struct RowFin {
     long obs, ops;
     const double* dinvf;
     int nl;
+    // optional per-limb constant on acc (w/q): out = (C_i acc - conv) D^{-1} -- the exact-scale
+    // level-down folded into a rescale (engine.hip rescale_view)
+    const double* cf;
 };
 
 // The forward row pass's 8 stages on the 16 rows of one workgroup: lane (b, rl) loads row
@@ -296,11 +299,14 @@ __device__ __forceinline__ void nttf_fwd_rows_body(const Span& dst, const Tabs& 
         const u64* dp = fin.addend.ptr && c < fin.addend.np ? fin.addend.ptr + (long)bb * fin.addend.bs + (long)c * fin.addend.ps + off : nullptr;
         u64* op = fin.out + (long)bb * fin.obs + (long)c * fin.ops + off;
         const double f = fin.dinvf[i], w = tw_w(f, q);
+        const double cf = fin.cf ? fin.cf[i] : 0.0, cw = fin.cf ? tw_w(cf, q) : 0.0;
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const int e = e0 + 64 * k;
             const double conv = u2d((u64)__double_as_longlong(s[row_tile_idx(e)]));
-            double v = fmul_rem(u2d(accw[FIN ? k : 0]) - conv, w, f, q);
+            double a = u2d(accw[FIN ? k : 0]);
+            if (fin.cf) a = fmul_rem(a, cw, cf, q);  // block-uniform
+            double v = fmul_rem(a - conv, w, f, q);
             if (dp) v += u2d(dp[e]);
             __builtin_nontemporal_store(fcanon(v, q, qi), &op[e]);  // streaming
         }
