@@ -1464,16 +1464,19 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) 
     Span dx = span_s(x.p, N, 1, 1, l, e->Lp1);
     if (in.bs != (long)in.np * in.ps && in.B > 1) throw_err(AESFHE_EARG, "rescale of non-compact view");
     ntt(e, src, dx, P, true);
-    if (sc) hipLaunchKernelGGL(k_rescale_spread<true>, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN, ctop, ctopf);
-    else hipLaunchKernelGGL(k_rescale_spread<false>, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN, ctop, ctopf);
     Span st = span_s(t.p, (long)l * N, l, l, 0, e->Lp1);
     if (fused_ntt(e) && in.np == 2 && !in.zero) {
-        // the finish runs in the epilogue of t's row pass (the ModDown finish's RowFin with
-        // acc = the input, D = q_l, optional level-down constant): t never reaches HBM in NTT form
+        // the spread runs in the copy-in of t's column pass (k_nttf_fwd_cols_spread reads the
+        // top limb x once per target limb: t is never written in coefficient form) and the finish
+        // in the epilogue of t's row pass (the ModDown finish's RowFin with acc = the input,
+        // D = q_l, optional level-down constant): t never reaches HBM in NTT form
         const int total = P * l;
         {
             ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
-            ntt_fwd_cols(e, st, total);
+            const SpreadSrc ss{(const u64*)x.p, e->chain.q[l], ctop, ctopf};
+            auto kern = N == 65536 ? (sc ? k_nttf_fwd_cols_spread<256, 2> : k_nttf_fwd_cols_spread<256, 1>)
+                                   : (sc ? k_nttf_fwd_cols_spread<512, 2> : k_nttf_fwd_cols_spread<512, 1>);
+            hipLaunchKernelGGL(kern, dim3(16, total), dim3(256), 0, e->stream, ss, st, e->tabs());
         }
         RowFin f{(const u64*)in.d, in.bs, in.ps, Opnd2{nullptr, 0, 0, 0}, r->d, 2L * l * N, (long)l * N,
                  e->rs_invf + (size_t)l * e->Lp1, l, sc ? (const double*)dff_c : nullptr};
@@ -1483,6 +1486,8 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) 
         HIPC(hipGetLastError());
         return r;
     }
+    if (sc) hipLaunchKernelGGL(k_rescale_spread<true>, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN, ctop, ctopf);
+    else hipLaunchKernelGGL(k_rescale_spread<false>, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN, ctop, ctopf);
     ntt(e, st, st, P * l, false);
     Opnd c = opnd(in, in.B);
     if (sc) hipLaunchKernelGGL(k_rescale_finish<true>, dim3(N / 256, l, P), dim3(256), 0, e->stream, c, (const u64*)t.p, out_of(r), in.np, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN, (const u64*)df, (const double*)dff);

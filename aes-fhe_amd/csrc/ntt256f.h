@@ -93,13 +93,24 @@ __device__ __forceinline__ void wave_sync_lds() {
 // within the half), so the R = 256 code runs on each half with the index multiplier 2 + h.
 // (the body takes the 16-column block bx of span limb by and LDS s[256 * kPadF], twq[R]; a
 // caller that loops over blocks separates them with a workgroup barrier)
-template <int R>
+// SPREAD (the rescale's spread in the copy-in, engine.hip rescale_view): limb y = (p, i) of dst
+// is not read from a span but formed from poly p's dropped top limb x[p] (canonical mod q_l, INTT
+// form): centered(x) mod q_i, canonical -- the residues k_rescale_spread wrote, so the pass's
+// output is unchanged while the spread's l-limb write + read-back is gone (x[p] is read once per
+// target limb, the same 16-column strip by the same XCD each time: bx's XCD is fixed).  SPREAD 2:
+// x is first multiplied by the level-down constant sc mod q_l (scf = sc / q_l).
+struct SpreadSrc {
+    const u64* x;
+    u64 ql, sc;
+    double scf;
+};
+template <int R, int SPREAD = 0>
 __device__ __forceinline__ void nttf_fwd_cols_body(const Span& src, const Span& dst, const Tabs& T, int bx, int by,
-                                                   double* s, double* twq) {
+                                                   double* s, double* twq, const SpreadSrc& ss = SpreadSrc{}) {
     static_assert(R == 256 || R == 512, "rows of 256: N = 2^16 or 2^17");
     constexpr int H = R / 256;
     int pid;
-    const u64* in = span_ptr(src, by, T.logN, T.Lp1, pid);
+    const u64* in = SPREAD ? ss.x + ((long)(by / dst.nl) << T.logN) : span_ptr(src, by, T.logN, T.Lp1, pid);
     u64* out = span_ptr(dst, by, T.logN, T.Lp1, pid);
     const int tid = threadIdx.x, cl = tid & 15, b = tid >> 4;
     const int c = bx * 16 + cl;
@@ -112,7 +123,17 @@ __device__ __forceinline__ void nttf_fwd_cols_body(const Span& src, const Span& 
 #pragma unroll
     for (int h = 0; h < H; h++)
 #pragma unroll
-        for (int a = 0; a < 16; a++) x[16 * h + a] = u2d(in[(h * 256 + a * 16 + b) * 256 + c]);
+        for (int a = 0; a < 16; a++) {
+            const u64 v = in[(h * 256 + a * 16 + b) * 256 + c];
+            if constexpr (SPREAD == 0) {
+                x[16 * h + a] = u2d(v);
+            } else {
+                const u64 w = SPREAD == 2 ? mul_w(v, ss.sc, ss.scf, ss.ql) : v;
+                double d = u2d(w) - (w > (ss.ql >> 1) ? (double)ss.ql : 0.0);  // centered, exact
+                d = fred(d, q, qi);
+                x[16 * h + a] = d < 0.0 ? d + q : d;
+            }
+        }
     __syncthreads();
     if (H == 2) {  // stage m = 1 across the halves: canonical in, (-q, 2q) out
         const double w = tg[1];
@@ -165,6 +186,12 @@ __global__ __launch_bounds__(256) void k_nttf_fwd_cols(Span src, Span dst, Tabs 
     __shared__ double s[256 * kPadF];
     __shared__ double twq[R];
     nttf_fwd_cols_body<R>(src, dst, T, blockIdx.x, blockIdx.y, s, twq);
+}
+template <int R, int SPREAD>
+__global__ __launch_bounds__(256) void k_nttf_fwd_cols_spread(SpreadSrc ss, Span dst, Tabs T) {
+    __shared__ double s[256 * kPadF];
+    __shared__ double twq[R];
+    nttf_fwd_cols_body<R, SPREAD>(dst, dst, T, blockIdx.x, blockIdx.y, s, twq, ss);
 }
 
 // ModDown finish fused into the row pass of the conv NTT (key switch): limb y of

@@ -275,7 +275,11 @@ def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
                # fused multiply-adds (Chebyshev / double-angle steps): alpha, c at a higher level, beta
                eng.multiply_fma(a, b, k["rlk"], alpha=2, c=a, gamma=-1.0, beta=-1.0),
                eng.multiply_fma(b, b, k["rlk"], alpha=2, beta=-1.0),
-               eng.multiply_fma(b, a, k["rlk"], alpha=-3, c=b, gamma=0.5)]
+               eng.multiply_fma(b, a, k["rlk"], alpha=-3, c=b, gamma=0.5),
+               # rescales through the spread-fused column pass: constant products (plain
+               # rescale) and exact-scale level-downs by one and by several levels
+               eng.multiply(a, 0.37), eng.multiply(b, -1.5),
+               eng.level_down(a, 5), eng.level_down(a, 2), eng.level_down(b, 1)]
         x = a
         while x.level >= 1:
             x = eng.multiply(x, a, k["rlk"])
