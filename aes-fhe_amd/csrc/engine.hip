@@ -1473,7 +1473,7 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) 
         const int total = P * l;
         {
             ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
-            const SpreadSrc ss{(const u64*)x.p, e->chain.q[l], ctop, ctopf};
+            const SpreadSrc ss{(const u64*)x.p, (long)N, e->chain.q[l], ctop, ctopf};
             auto kern = N == 65536 ? (sc ? k_nttf_fwd_cols_spread<256, 2> : k_nttf_fwd_cols_spread<256, 1>)
                                    : (sc ? k_nttf_fwd_cols_spread<512, 2> : k_nttf_fwd_cols_spread<512, 1>);
             hipLaunchKernelGGL(kern, dim3(16, total), dim3(256), 0, e->stream, ss, st, e->tabs());
@@ -1842,6 +1842,20 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         const int lo = j * K, hi = std::min(lo + K, l + 1), alpha = hi - lo;
         const size_t set = (size_t)j * K + (alpha - 1);
         u64* exj = ext + (size_t)j * B * neN;
+        if (cols_only && alpha == 1) {
+            // one-limb digit: the conversion is x mod p_t (hat = hatinv = 1), formed in the column
+            // pass's copy-in from the digit limb itself (no k_modup<1> write + read-back)
+            const SpreadSrc ss{(const u64*)dc.p + (long)lo * N, lN, 0, 0, 0.0};
+            auto kern = N == 65536 ? k_nttf_fwd_cols_spread<256, 3> : k_nttf_fwd_cols_spread<512, 3>;
+            auto cols = [&](Span sp, int total) {
+                ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+                hipLaunchKernelGGL(kern, dim3(16, total), dim3(256), 0, e->stream, ss, sp, e->tabs());
+            };
+            if (lo > 0) cols(span_s(exj, neN, lo, lo, 0, e->Lp1), B * lo);
+            cols(span_s(exj + (long)hi * N, neN, ne - hi, (l + 1) - hi, hi, e->Lp1), B * (ne - hi));
+            HIPC(hipGetLastError());
+            continue;
+        }
         // 2. ModUp base conversion of digit j to every other limb, then NTT those limbs
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);

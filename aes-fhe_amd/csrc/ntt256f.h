@@ -98,9 +98,12 @@ __device__ __forceinline__ void wave_sync_lds() {
 // form): centered(x) mod q_i, canonical -- the residues k_rescale_spread wrote, so the pass's
 // output is unchanged while the spread's l-limb write + read-back is gone (x[p] is read once per
 // target limb, the same 16-column strip by the same XCD each time: bx's XCD is fixed).  SPREAD 2:
-// x is first multiplied by the level-down constant sc mod q_l (scf = sc / q_l).
+// x is first multiplied by the level-down constant sc mod q_l (scf = sc / q_l).  SPREAD 3: x mod
+// q_i without centring -- the ModUp of a one-limb key-switch digit (k_modup<1>: hat = hatinv = 1).
+// x of poly p at x + p * xs.
 struct SpreadSrc {
     const u64* x;
+    long xs;
     u64 ql, sc;
     double scf;
 };
@@ -110,7 +113,7 @@ __device__ __forceinline__ void nttf_fwd_cols_body(const Span& src, const Span& 
     static_assert(R == 256 || R == 512, "rows of 256: N = 2^16 or 2^17");
     constexpr int H = R / 256;
     int pid;
-    const u64* in = SPREAD ? ss.x + ((long)(by / dst.nl) << T.logN) : span_ptr(src, by, T.logN, T.Lp1, pid);
+    const u64* in = SPREAD ? ss.x + (long)(by / dst.nl) * ss.xs : span_ptr(src, by, T.logN, T.Lp1, pid);
     u64* out = span_ptr(dst, by, T.logN, T.Lp1, pid);
     const int tid = threadIdx.x, cl = tid & 15, b = tid >> 4;
     const int c = bx * 16 + cl;
@@ -129,7 +132,7 @@ __device__ __forceinline__ void nttf_fwd_cols_body(const Span& src, const Span& 
                 x[16 * h + a] = u2d(v);
             } else {
                 const u64 w = SPREAD == 2 ? mul_w(v, ss.sc, ss.scf, ss.ql) : v;
-                double d = u2d(w) - (w > (ss.ql >> 1) ? (double)ss.ql : 0.0);  // centered, exact
+                double d = u2d(w) - (SPREAD != 3 && w > (ss.ql >> 1) ? (double)ss.ql : 0.0);  // centered, exact
                 d = fred(d, q, qi);
                 x[16 * h + a] = d < 0.0 ? d + q : d;
             }
