@@ -280,6 +280,11 @@ def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
     blocks = np.random.default_rng(77).integers(0, 256, (world, drv.n_blk, 16), dtype=np.uint8)
     cts = drv.cts(drv.encrypt(blocks)) if rank == 0 else [None] * (32 if drv.layout == "rows" else 2)
     key = drv.key(rk)
+    # untimed warm-up: the first RCCL collective sets up the communicator (hundreds of ms), which
+    # is not part of the data path's rate
+    warm = scatter_ciphertext(eng, cts[0])
+    warm = gather_ciphertext(eng, warm)
+    del warm
     barrier()
     t0 = time.perf_counter()
     mine = [scatter_ciphertext(eng, c) for c in cts]
@@ -298,8 +303,15 @@ def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
     return {"sets": world, "bytes_per_rank_in": bytes_in, "scatter_ms": round(t_sc * 1e3, 2),
             "gather_ms": round(t_ga * 1e3, 2),
             "scatter_gbs_per_rank": round(bytes_in / t_sc / 1e9, 2) if t_sc else None,
-            "verified": ok, "path": "aesfhe_ct_export_device -> torch.distributed scatter/gather "
-                                    "(nccl backend = RCCL over xGMI) -> aesfhe_ct_import_device"}
+            "verified": ok, "backend": _dist_backend(),
+            "path": "aesfhe_ct_export_device -> torch.distributed scatter/gather "
+                    "(nccl backend = RCCL over xGMI; gloo when ranks share a GPU) -> aesfhe_ct_import_device",
+            "note": "after one untimed scatter + gather (communicator set-up)"}
+
+
+def _dist_backend():
+    import torch.distributed as dist
+    return dist.get_backend() if dist.is_initialized() else None
 
 
 def _cpu_model():
