@@ -1811,6 +1811,17 @@ static void launch_moddown(dim3 g, hipStream_t s, Args... args) {
     hipLaunchKernelGGL(k_moddown<NE>, g, dim3(256), 0, s, args...);
 }
 
+// target-limb groups (gridDim.y) of a base conversion over P polynomials: a thread converts its
+// two coefficients into every target of its group, so small batches (the reference services'
+// single ciphertexts) would leave most CUs idle with one group; >= 1024 workgroups of 256 threads
+// (4 per CU) otherwise, 1 group at the batched workloads (P >= 8 at N = 2^16).  The outputs do
+// not depend on the grouping (each target is computed the same way).
+static unsigned bconv_groups(int N, int P, int ntarget) {
+    const long wg = (long)(N / 512) * P;
+    const long g = (1024 + wg - 1) / wg;
+    return (unsigned)std::max(1L, std::min(g, (long)ntarget));
+}
+
 static int ks_beta(const aesfhe_engine* e, int l) {
     const int beta = (l + 1 + e->K - 1) / e->K;
     if (beta > 12) throw_err(AESFHE_EUNSUPPORTED, "more than 12 key-switch digits");
@@ -1860,7 +1871,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
             if (alpha < 1 || alpha > 16) throw_err(AESFHE_EUNSUPPORTED, "ModUp digit width outside 1..16");
-            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, 1, B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
+            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, bconv_groups(N, B, ne), B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
                               (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
                               K, e->q, e->qinv, e->Lp1, e->logN);
         }
@@ -1941,7 +1952,7 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1));
         if (K + r < 1 || K + r > 16) throw_err(AESFHE_EUNSUPPORTED, "ModDown source width outside 1..16");
-        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, 1, B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN,
+        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, bconv_groups(N, B * 2, lk + 1), B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN,
                            invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv,
                            r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN, hs);
     }
