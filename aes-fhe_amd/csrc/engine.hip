@@ -1500,6 +1500,13 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) 
 // new ciphertexts at level l-1 (one rescale pass for all groups)
 static std::vector<aesfhe_ct*> rescale_groups(aesfhe_engine* e, const u64* d, int G, int Bg, int np, int l) {
     const int N = e->N, P = G * Bg * np;
+    if (fused_ntt(e) && np == 2) {
+        // the groups are one compact batch of G * Bg ciphertexts: the fused rescale (spread in the
+        // column pass, finish in the row pass), then the output block split per group (no copies)
+        const long ps = (long)(l + 1) * N;
+        aesfhe_ct* r = rescale_view(e, View{d, G * Bg, np, l, ps, np * ps, false});
+        return G == 1 ? std::vector<aesfhe_ct*>{r} : ct_split_batch(e, r, G);
+    }
     std::vector<aesfhe_ct*> outs(G);
     for (int g = 0; g < G; g++) outs[g] = ct_new(e, Bg, np, l - 1);
     Tmp x(e, (size_t)P * N), t(e, (size_t)P * l * N);

@@ -280,6 +280,8 @@ def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
                # rescale) and exact-scale level-downs by one and by several levels
                eng.multiply(a, 0.37), eng.multiply(b, -1.5),
                eng.level_down(a, 5), eng.level_down(a, 2), eng.level_down(b, 1)]
+        # grouped rescale (lincomb_many: the groups as one batch through the fused rescale)
+        out += eng.lincomb_many([a, b, a], [[1.0, 2.0, -1.0], [0.25, 0.0, 1j], [-3.0, 0.5, 0.0]])
         x = a
         while x.level >= 1:
             x = eng.multiply(x, a, k["rlk"])
