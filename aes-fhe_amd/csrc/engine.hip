@@ -1436,7 +1436,9 @@ extern "C" int aesfhe_decrypt(aesfhe_engine* e, const aesfhe_key* sk, const aesf
 // C != 1: rescale of C * in (the exact-scale level-down, level_down_view), the constant folded
 // into the spread (top limb) and the finish (every kept limb) instead of a k_mul_const pass.
 static void const_factors(aesfhe_engine* e, int64_t A, int64_t Bc, int nl, std::vector<u64>& f, std::vector<double>& ff);
-static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) {
+// into: write the result into this caller-owned compact block (in.B x in.np polys at level l-1)
+// instead of a new ciphertext (the return value is then nullptr).
+static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1, u64* into = nullptr) {
     const int N = e->N, l = in.level, P = in.B * in.np;
     const bool sc = C != 1;
     u64* df = nullptr;
@@ -1456,7 +1458,9 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) 
         for (int i = 0; i < l; i++) fc[i] = ff[2 * i];
         dff_c = upload_small(e, fc.data(), fc.size());
     }
-    aesfhe_ct* r = ct_new(e, in.B, in.np, l - 1);
+    aesfhe_ct* r = into ? nullptr : ct_new(e, in.B, in.np, l - 1);
+    aesfhe_ct alias{e, in.B, in.np, l - 1, 0, into, 0};
+    aesfhe_ct* o = into ? &alias : r;
     Tmp x(e, (size_t)P * N), t(e, (size_t)P * l * N);
     // INTT of limb l of every poly: source poly p of batch b at d + b*bs + p*ps + l*N
     // (expressed as a Span over the flattened polys; requires bs == np*ps, true for compact views)
@@ -1478,7 +1482,7 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) 
                                    : (sc ? k_nttf_fwd_cols_spread<512, 2> : k_nttf_fwd_cols_spread<512, 1>);
             hipLaunchKernelGGL(kern, dim3(16, total), dim3(256), 0, e->stream, ss, st, e->tabs());
         }
-        RowFin f{(const u64*)in.d, in.bs, in.ps, Opnd2{nullptr, 0, 0, 0}, r->d, 2L * l * N, (long)l * N,
+        RowFin f{(const u64*)in.d, in.bs, in.ps, Opnd2{nullptr, 0, 0, 0}, o->d, 2L * l * N, (long)l * N,
                  e->rs_invf + (size_t)l * e->Lp1, l, sc ? (const double*)dff_c : nullptr};
         ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total * 3.0);  // half an NTT + input read + output write
         if (N == 65536) hipLaunchKernelGGL((k_nttf_fwd_rows_t<true, 256>), dim3(16, total), dim3(256), 0, e->stream, st, e->tabs(), f);
@@ -1490,8 +1494,8 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1) 
     else hipLaunchKernelGGL(k_rescale_spread<false>, dim3(N / 256, l, P), dim3(256), 0, e->stream, (const u64*)x.p, t.p, e->chain.q[l], e->q, e->qinv, e->rs_mod + (size_t)l * e->Lp1, l, e->logN, ctop, ctopf);
     ntt(e, st, st, P * l, false);
     Opnd c = opnd(in, in.B);
-    if (sc) hipLaunchKernelGGL(k_rescale_finish<true>, dim3(N / 256, l, P), dim3(256), 0, e->stream, c, (const u64*)t.p, out_of(r), in.np, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN, (const u64*)df, (const double*)dff);
-    else hipLaunchKernelGGL(k_rescale_finish<false>, dim3(N / 256, l, P), dim3(256), 0, e->stream, c, (const u64*)t.p, out_of(r), in.np, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN, (const u64*)nullptr, (const double*)nullptr);
+    if (sc) hipLaunchKernelGGL(k_rescale_finish<true>, dim3(N / 256, l, P), dim3(256), 0, e->stream, c, (const u64*)t.p, out_of(o), in.np, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN, (const u64*)df, (const double*)dff);
+    else hipLaunchKernelGGL(k_rescale_finish<false>, dim3(N / 256, l, P), dim3(256), 0, e->stream, c, (const u64*)t.p, out_of(o), in.np, l, e->q, e->rs_inv + (size_t)l * e->Lp1, e->rs_invf + (size_t)l * e->Lp1, e->logN, (const u64*)nullptr, (const double*)nullptr);
     HIPC(hipGetLastError());
     return r;
 }
@@ -1559,6 +1563,11 @@ static View truncated(const View& v, int level) {
     return t;
 }
 
+// exact-scale level-down constant from level `from` to `lt` < from
+static int64_t level_down_const(const aesfhe_engine* e, int from, int lt) {
+    return llround(e->chain.scale[lt] * (double)e->chain.q[lt + 1] / e->chain.scale[from]);
+}
+
 static aesfhe_ct* level_down_view(aesfhe_engine* e, const View& v, int lt) {
     if (lt == v.level) {
         aesfhe_ct* r = ct_new(e, v.B, v.np, v.level);
@@ -1574,8 +1583,7 @@ static aesfhe_ct* level_down_view(aesfhe_engine* e, const View& v, int lt) {
     }
     if (v.zero) return ct_zero_new(e, v.B, v.np, lt);
     View t = truncated(v, lt + 1);
-    int64_t C = llround(e->chain.scale[lt] * (double)e->chain.q[lt + 1] / e->chain.scale[v.level]);
-    return rescale_view(e, t, C);  // C folded into the rescale's spread + finish (no k_mul_const pass)
+    return rescale_view(e, t, level_down_const(e, v.level, lt));  // C folded into the rescale's spread + finish (no k_mul_const pass)
 }
 
 // owned-or-borrowed aligned operand
@@ -2415,6 +2423,79 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
     API_END
 }
 
+// Power basis of one ciphertext (B = 1, fused-NTT engines) by depth.  The products of depth j,
+// x^{2^j + k2} = x^{2^j} * x^{k2} for k2 = 1..m_j (m_j = min(2^j, d - 2^j)), all at level l0 - j,
+// run as ONE batched product with x^{2^j} broadcast: the relinearisation key streams once per
+// depth instead of once per product, and every launch covers m_j ciphertexts instead of one.
+// The depth-j operand block O_j holds slot s = x^{s+1} at level l0 - j (s < 2^j): its upper half
+// is depth j-1's product output, written there directly; its lower half is x^{1..2^{j-1}}
+// level-downed straight from each power's own level (one batched level-down per source depth,
+// written into the block).  O_{j+1} is split in the pool (no copies): its upper half is returned,
+// its lower half freed once depth j+1 is enqueued.  Every product and level-down is the
+// arithmetic of the sequential basis below (and of oracle/ckks_oracle.c aesfhe_power_basis), so
+// each output is bit-identical to it.
+static void power_basis_batched(aesfhe_engine* e, const aesfhe_ct* c, int d, const aesfhe_key* rlk, aesfhe_ct** outs) {
+    const int N = e->N, l0 = c->level;
+    int need = 0;
+    while ((1 << need) < d) need++;
+    auto pview = [&](const u64* p, int B, int lv) {
+        const long ps = (long)(lv + 1) * N;
+        return View{p, B, 2, lv, ps, 2 * ps, false};
+    };
+    for (int k = 0; k < d; k++) outs[k] = nullptr;
+    std::vector<aesfhe_ct*> lower, nxt;  // lower halves of O_j (temporaries), parts of O_{j+1}
+    auto drop = [&](std::vector<aesfhe_ct*>& v) {
+        for (auto* p : v) aesfhe_ct_free(p);
+        v.clear();
+    };
+    try {
+        outs[0] = ct_new(e, 1, 2, l0);
+        HIPC(hipMemcpyAsync(outs[0]->d, c->d, outs[0]->bytes, hipMemcpyDeviceToDevice, e->stream));
+        const u64* opd = c->d;  // slot 0 of O_j (depth 0: x itself)
+        for (int j = 0; j < need; j++) {
+            const int S = 1 << j, lv = l0 - j, m = std::min(2 * S, d) - S;
+            const size_t pw = (size_t)2 * (lv + 1) * N;
+            const View va = pview(opd + (size_t)(S - 1) * pw, 1, lv), vb = pview(opd, m, lv);
+            if (d > 2 * S) {  // another depth follows: the products fill the upper half of O_{j+1}
+                nxt = ct_split_batch(e, ct_new(e, 2 * S, 2, lv - 1), 2 * S);
+                aesfhe_ct alias{e, S, 2, lv - 1, 0, nxt[S]->d, 0};
+                keyswitch_prod(e, opnd(va, S), opnd(vb, S), S, lv, rlk, &alias, 1);
+                for (int t = 0; t < S; t++) outs[S + t] = nxt[S + t], nxt[S + t] = nullptr;
+                nxt.resize(S);
+                drop(lower);  // O_j's level-downed half: its last reader is enqueued
+                // O_{j+1}'s lower half: x^{1..min(S, m_{j+1})} at level lv - 1, per source depth i
+                // (x^{lo..hi} at level l0 - i) one batched level-down into the block
+                const int mnext = std::min(4 * S, d) - 2 * S;
+                for (int i = 0; i <= j; i++) {
+                    const int lo = i ? (1 << (i - 1)) + 1 : 1, hi = std::min(1 << i, mnext);
+                    if (hi < lo) break;
+                    const int sl = l0 - i;
+                    rescale_view(e, truncated(pview(outs[lo - 1]->d, hi - lo + 1, sl), lv), level_down_const(e, sl, lv - 1),
+                                 nxt[lo - 1]->d);
+                }
+                lower.swap(nxt);
+                opd = lower[0]->d;
+            } else {  // last depth: the m outputs as one block, split
+                aesfhe_ct* r = ct_new(e, m, 2, lv - 1);
+                try {
+                    keyswitch_prod(e, opnd(va, m), opnd(vb, m), m, lv, rlk, r, 1);
+                } catch (...) {
+                    aesfhe_ct_free(r);
+                    throw;
+                }
+                std::vector<aesfhe_ct*> parts = m > 1 ? ct_split_batch(e, r, m) : std::vector<aesfhe_ct*>{r};
+                for (int t = 0; t < m; t++) outs[S + t] = parts[t];
+                drop(lower);
+            }
+        }
+    } catch (...) {
+        drop(lower);
+        drop(nxt);
+        for (int k = 0; k < d; k++) aesfhe_ct_free(outs[k]), outs[k] = nullptr;
+        throw;
+    }
+}
+
 extern "C" int aesfhe_power_basis(aesfhe_engine* e, const aesfhe_ct* c, int32_t d, const aesfhe_key* rlk, aesfhe_ct** outs) {
     API_BEGIN
     if (d < 1) throw_err(AESFHE_EARG, "degree must be >= 1");
@@ -2423,6 +2504,10 @@ extern "C" int aesfhe_power_basis(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
     int need = 0;
     while ((1 << need) < d) need++;
     if (c->level < need) throw_err(AESFHE_ELEVEL, "power basis of degree %d needs %d levels, have %d", d, need, c->level);
+    if (d >= 2 && c->B == 1 && !c->is_zero && fused_ntt(e) && e->K + 1 <= kMdrMaxE) {
+        power_basis_batched(e, c, d, rlk, outs);
+        return AESFHE_OK;
+    }
     std::vector<aesfhe_ct*> pw(d + 1, nullptr);
     // memo of level-downed powers: (k, level) -> ct
     std::map<std::pair<int, int>, aesfhe_ct*> memo;

@@ -228,12 +228,14 @@ def config_legs(args, eng, drv):
     from types import SimpleNamespace
 
     from aes_xor_fhe import aes_tables as T
-    from aes_xor_fhe.aes_round import AESRoundEngine
     from aes_xor_fhe.sbox.sbox_service import SBoxService
     from aes_xor_fhe.utils import zeta_decode, zeta_encode
     sk, pk, rlk, cjk = drv.keys
     out = {}
+    legs = getattr(args, "legs", "2,3").split(",")
     # config 2: SubBytes of one ciphertext (32768 bytes = 2048 blocks), reference op order
+    if "2" not in legs:
+        return config3_leg(args, eng, drv, out) if "3" in legs else out
     ctx = SimpleNamespace(engine=eng, relinearization_key=rlk)
     sb = SBoxService(ctx)
     x = np.random.default_rng(1).integers(0, 256, eng.slot_count)
@@ -249,7 +251,15 @@ def config_legs(args, eng, drv):
         c2[name] = {"value": round(eng.slot_count / 16 / t, 1), "unit": "blocks/s", "ms": round(t * 1e3, 2),
                     "verified": ok, "level_drop": ct.level - res.level}
     out["config2_subbytes"] = c2
-    # config 3: ShiftRows + MixColumns, byte-major Zeta-16 nibble pair (2048 blocks per ct)
+    return config3_leg(args, eng, drv, out) if "3" in legs else out
+
+
+def config3_leg(args, eng, drv, out):
+    """BASELINE config 3: ShiftRows + MixColumns, byte-major Zeta-16 nibble pair (2048 blocks
+    per ct), at 1 and 8 ciphertext pairs, verified against FIPS-197."""
+    from aes_xor_fhe import aes_tables as T
+    from aes_xor_fhe.aes_round import AESRoundEngine
+    sk, pk, rlk, cjk = drv.keys
     R = AESRoundEngine(eng, sk, pk, rlk, cjk)
     c3 = {"workload": "ShiftRows+MixColumns, byte-major zeta-16 (hi, lo) nibble pair, 2048 "
                       "blocks/ct (aes_round.AESRoundEngine: rotate-mask terms + nibble XOR LUTs)"}

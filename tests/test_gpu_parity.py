@@ -324,3 +324,50 @@ def test_switching_key_export_bit_exact(product_lib, oracle_lib, gpu_available, 
     z = rng.uniform(-1, 1, g.slot_count)
     cg, co = g.encrypt(z, kg["pk"]), o.encrypt(z, ko["pk"])
     _same(g, o, g.multiply(cg, cg, rl2), o.multiply(co, co, ko["rlk"]))
+
+
+@pytest.mark.parametrize("degrees", [(2, 3, 5, 8, 13, 16, 17, 31, 33)])
+def test_power_basis_batched_bit_exact(product_lib, oracle_lib, gpu_available, degrees):
+    """aesfhe_power_basis at N = 2^16 (one ciphertext: the products of each depth run as one
+    batched product with x^{2^j} broadcast, the lower powers level-downed straight into the
+    operand block) against the oracle's sequential basis, residue for residue: full and partial
+    last depths, powers of two and their neighbours."""
+    kw = dict(log_n=16, max_level=7, special_primes=3, seed=31)
+    g, o = _pair(product_lib, oracle_lib, **kw)
+    rng = np.random.default_rng(13)
+    z = np.exp(-2j * np.pi * rng.integers(0, 256, g.slot_count) / 256)
+    res, sks = [], []
+    for eng in (g, o):
+        k = _keys(eng)
+        c = eng.encrypt(z, k["pk"], level=6)
+        res.append([eng.make_power_basis(c, d, k["rlk"]) for d in degrees])
+        sks.append(k["sk"])
+    for bg, bo, d in zip(res[0], res[1], degrees):
+        assert len(bg) == len(bo) == d
+        for cg, co in zip(bg, bo):
+            _same(g, o, cg, co)
+    top = res[0][-1]
+    np.testing.assert_allclose(g.decrypt(top[-1], sks[0]), z ** degrees[-1], atol=1e-4)
+
+
+def test_power_basis_255_full_params_bit_exact(product_lib, oracle_lib, gpu_available):
+    """The S-box's make_power_basis(ct, 255) at BASELINE.json's N = 2^16, L = 30 (K = 10, the
+    bench chain): every one of the 255 powers residue-identical to the oracle's sequential basis
+    (reference: sbox/sbox_service.py:91-93, gf_service.py:55-64)."""
+    kw = dict(log_n=16, max_level=30, special_primes=10, seed=99)
+    g, o = _pair(product_lib, oracle_lib, **kw)
+    rng = np.random.default_rng(14)
+    x = rng.integers(0, 256, g.slot_count)
+    z = np.exp(2j * np.pi * x / 256)
+    res, sks = [], []
+    for eng in (g, o):
+        k = dict(sk=eng.create_secret_key(7))
+        k["pk"] = eng.create_public_key(k["sk"])
+        k["rlk"] = eng.create_relinearization_key(k["sk"])
+        res.append(eng.make_power_basis(eng.encrypt(z, k["pk"]), 255, k["rlk"]))
+        sks.append(k["sk"])
+    for cg, co in zip(*res):
+        _same(g, o, cg, co)
+    assert [c.level for c in res[0]] == [30 - int(np.ceil(np.log2(k))) for k in range(1, 256)]
+    for p in (1, 2, 127, 128, 255):
+        np.testing.assert_allclose(g.decrypt(res[0][p - 1], sks[0]), z ** p, atol=1e-3)
