@@ -77,6 +77,12 @@ SIGNATURES = [
     ("aesfhe_encrypt", C.c_int,
      [c_eng_p, c_key_p, _P(C.c_int64), C.c_int32, C.c_int32, C.c_uint64, _P(c_ct_p)]),
     ("aesfhe_decrypt", C.c_int, [c_eng_p, c_key_p, c_ct_p, _P(C.c_int64)]),
+    ("aesfhe_encode_device", C.c_int,
+     [c_eng_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_double, C.c_void_p]),
+    ("aesfhe_decode_device", C.c_int, [c_eng_p, C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p]),
+    ("aesfhe_encrypt_device", C.c_int,
+     [c_eng_p, c_key_p, C.c_void_p, C.c_int32, C.c_int32, C.c_uint64, _P(c_ct_p)]),
+    ("aesfhe_decrypt_device", C.c_int, [c_eng_p, c_key_p, c_ct_p, C.c_void_p]),
     ("aesfhe_ct_info", C.c_int, [c_ct_p, _P(C.c_int32)]),
     ("aesfhe_ct_export", C.c_int, [c_eng_p, c_ct_p, _P(C.c_uint64)]),
     ("aesfhe_ct_import", C.c_int,
@@ -161,6 +167,7 @@ class Lib:
 
 
 _PRODUCT: Lib | None = None
+PRODUCT_BACKEND = "hip-gfx950"
 
 
 def load_product() -> Lib:
@@ -182,5 +189,11 @@ def load_product() -> Lib:
             raise RuntimeError(
                 f"aes-fhe HIP extension not found at {path}; build it with "
                 f"`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
-        _PRODUCT = Lib(path)
+        lib = Lib(path)
+        # AESFHE_LIB selects another build of the product (A/B runs), never another backend: a
+        # library that is not the gfx950 HIP engine (e.g. the CPU oracle) is refused here, so a
+        # stray setting cannot turn a GPU test or the bench into the checker comparing itself
+        if lib.backend != PRODUCT_BACKEND:
+            raise RuntimeError(f"{path} is backend {lib.backend!r}, not the product ({PRODUCT_BACKEND!r})")
+        _PRODUCT = lib
     return _PRODUCT

@@ -85,6 +85,39 @@ class AESRowRound:
                 out[:, :, r + 4 * c] = v[:, c, :]
         return out
 
+    # ---- device-resident client path (Engine.encrypt_device / decrypt_device) -----------------
+    def encrypt_blocks_device(self, blocks):
+        """encrypt_blocks for a (NB, n_blk, 16) uint8 torch tensor on the engine's client device:
+        packing, +-1 bit slicing, encoding and encryption all on the device."""
+        import torch
+        b = blocks.to(self.e.client_device)
+        nb = b.shape[0]
+        st = []
+        for r in range(4):
+            row = b[:, :, [r + 4 * c for c in range(4)]].permute(0, 2, 1).reshape(nb, self.sc).to(torch.int64)
+            st.append([self.e.encrypt_device(1.0 - 2.0 * ((row >> j) & 1).to(torch.float64), self.pk)
+                       for j in range(8)])
+        return st
+
+    def decrypt_blocks_device(self, bits):
+        """decrypt_blocks into a (NB, n_blk, 16) uint8 torch tensor on the client device."""
+        import torch
+        rows = []
+        for r in range(4):
+            acc = None
+            for j in range(8):
+                v = self.e.decrypt_device(bits[r][j], self.sk).real
+                t = (v < 0).to(torch.uint8) << j
+                acc = t if acc is None else acc | t
+            rows.append(acc)
+        nb = rows[0].shape[0]
+        out = torch.empty((nb, self.n_blk, 16), dtype=torch.uint8, device=rows[0].device)
+        for r in range(4):
+            v = rows[r].reshape(nb, 4, self.n_blk)
+            for c in range(4):
+                out[:, :, r + 4 * c] = v[:, c, :]
+        return out
+
     def encrypt_bytes_rows(self, rows: Sequence[np.ndarray], level: int | None = None):
         return [[self.e.encrypt(1.0 - 2.0 * ((row.astype(np.int64) >> j) & 1), self.pk, level=level)
                  for j in range(8)] for row in rows]

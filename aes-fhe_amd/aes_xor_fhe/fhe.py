@@ -29,8 +29,9 @@ from ._abi import Lib, Params, c_ct_p, c_key_p, c_pt_p, load_product
 SECURITY_BUDGET = {11: 54, 12: 109, 13: 218, 14: 438, 15: 881, 16: 1772, 17: 3544}
 
 # seed None: a fresh 256-bit ChaCha20 engine key from the OS entropy pool (os.urandom) per
-# engine, so that no two default engines derive the same keys; an explicit 64-bit seed reproduces
-# every key and encryption (tests, and multi-rank key sharing -- see `nonce_start`).
+# engine, so that no two default engines derive the same keys; an explicit seed (an integer below
+# 2^256 or 32 bytes) reproduces every key and encryption: a small integer for tests, a 256-bit
+# value shared by the ranks that must hold the same keys (parallel.shared_seed, `nonce_start`).
 # scale 44 with K = 8: log QP = 50 + 30 * 44 + 8 * 50 = 1770 <= 1772 (128-bit at N = 2^16).  The
 # general-mode Engine.bootstrap the reference's services call (xor_service.py:120-129) needs it:
 # measured at N = 2^16, L = 30 (tools/boot_general_diag.py): max slot error 4.7e-3 at scale 44,
@@ -57,10 +58,21 @@ def _params_for(log_n=None, max_level=None, special_primes=None, scale_bits=None
             p[k] = v
     p["threads"] = threads
     p["device"] = device
-    p["seed_ext"] = (0, 0, 0)
-    if p["seed"] is None:
-        p["seed"] = _urandom64()
-        p["seed_ext"] = (_urandom64(), _urandom64(), _urandom64())
+    s = p["seed"]
+    if s is None:  # a fresh 256-bit key
+        s = int.from_bytes(os.urandom(32), "little")
+    elif isinstance(s, (bytes, bytearray)):
+        if len(s) != 32:
+            raise ValueError("a bytes seed must be 32 bytes (256 bits)")
+        s = int.from_bytes(bytes(s), "little")
+    s = int(s)
+    if not 0 <= s < 1 << 256:
+        raise ValueError("seed must be an integer in [0, 2^256) or 32 bytes")
+    m = (1 << 64) - 1
+    # the ChaCha20 engine key: seed = bits 0..63, seed_ext = bits 64..255 (a 64-bit seed keeps the
+    # zero extension: reproducible tests; multi-rank key sharing passes a 256-bit shared seed,
+    # parallel.shared_seed)
+    p["seed"], p["seed_ext"] = s & m, ((s >> 64) & m, (s >> 128) & m, (s >> 192) & m)
     return p
 
 
@@ -175,6 +187,45 @@ class Ciphertext(_Handle):
         return f"Ciphertext(level={self.level}, batch={self.batch}, npoly={self.npoly})"
 
 
+class _LinearCiphertext(Ciphertext):
+    """A deferred linear combination: sum_i c_i * ct_i (each term one level below its input, as
+    `multiply(ct, constant)` defines it) + sum of ciphertexts + a constant.
+
+    ``Engine.multiply(ct, constant)`` returns one term; ``Engine.add`` of such objects (with each
+    other, with ciphertexts or with constants) returns the merged sum; any other use of the
+    handle (``_h``: a C call, decrypt, export, a product, a rotation ...) materialises it once
+    as ONE fused ``aesfhe_lincomb`` (one rescale of the sum) plus the ciphertext addends and
+    the constant.  ``level``, ``batch``, ``npoly`` and ``is_zero`` are those of the eager result,
+    so callers that read them (the reference's ``level < 8`` bootstrap rule, xor_service.py:
+    274-277) see the same values.  The reference's LUT evaluators (sbox/sbox_service.py:116-138,
+    gf_service.py:46-64, xor_service.py:271-286) issue one multiply and one add per coefficient;
+    this turns each such chain into the single fused launch sequence of `lincomb` instead of a
+    rescale + add per term.  The residues equal `Engine.lincomb` of the same terms (rescale of the
+    sum instead of the sum of rescales) on either backend, so the oracle stays the checker."""
+
+    __slots__ = ("_terms", "_addends", "_const", "_mat")
+
+    def __init__(self, engine: "Engine", terms, addends, const, level, batch):
+        self._lib, self._free = engine._lib, None
+        self.engine = engine
+        self._terms, self._addends, self._const, self._mat = terms, addends, complex(const), None
+        self.level, self.batch, self.npoly = level, batch, 2
+        self.is_zero = not terms and not addends and self._const == 0
+
+    @property
+    def _h(self):
+        if self._mat is None:
+            self._mat = self.engine._materialize(self)
+        return self._mat._h
+
+    def __del__(self):  # the materialised ciphertext frees itself
+        pass
+
+    def __repr__(self):
+        return (f"Ciphertext(level={self.level}, batch={self.batch}, npoly=2, deferred "
+                f"{len(self._terms)} terms + {len(self._addends)} addends)")
+
+
 class Plaintext:
     """Host-side slot vector; device encodings are materialised per (level, scale) on use.
     A constant vector (every slot equal) is multiplied as the polynomial a + b X^{N/2}."""
@@ -215,6 +266,10 @@ class Engine:
     ``special_primes``, ``scale_bits``, ``base_bits``, ``special_bits``, ``seed``) select explicit parameters; ``_lib`` injects
     another implementation of the ABI (tests use it for the CPU oracle).
 
+    ``fuse_linear`` (default True): ``multiply(ct, constant)`` and the ``add`` calls that consume
+    its result are deferred and materialised as one fused linear combination
+    (``_LinearCiphertext``); False evaluates every call eagerly (a rescale per product).
+
     Randomness: without ``seed`` the engine seed, every secret key created without a seed and
     the first encryption nonce are drawn from os.urandom.  With an explicit ``seed`` everything
     is reproducible and nonces count from ``nonce_start`` (default 0); engines that share a seed
@@ -228,8 +283,8 @@ class Engine:
                  special_prime_count: int | None = None, log_n: int | None = None,
                  special_primes: int | None = None, scale_bits: int | None = None,
                  base_bits: int | None = None, special_bits: int | None = None,
-                 seed: int | None = None, nonce_start: int | None = None,
-                 _lib: Lib | None = None):
+                 seed: int | bytes | None = None, nonce_start: int | None = None,
+                 fuse_linear: bool = True, _lib: Lib | None = None):
         ints = [a for a in args if isinstance(a, (int, np.integer)) and not isinstance(a, bool)]
         strs = [a for a in args if isinstance(a, str)]
         if strs:
@@ -277,6 +332,7 @@ class Engine:
         self._lib.engine_scales(self._h, scales)
         self.scales = [float(x) for x in scales]
         self._random_keys = seed is None
+        self._fuse_linear = bool(fuse_linear)
         if nonce_start is None:
             nonce_start = _urandom64() >> 1 if seed is None else 0
         self._nonce = int(nonce_start)
@@ -458,6 +514,10 @@ class Engine:
         return Plaintext(self, self._vec(x))
 
     def add(self, a, b) -> Ciphertext:
+        if isinstance(a, _LinearCiphertext) or isinstance(b, _LinearCiphertext):
+            r = self._linear_add(a, b)
+            if r is not None:
+                return r
         if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
             return self._call_ct(self._lib.add, a._h, b._h)
         if not isinstance(a, Ciphertext):
@@ -493,9 +553,50 @@ class Engine:
         pt = self._as_plain(b)
         if pt.is_const:
             c = pt.const
+            if self._fuse_linear and a.npoly == 2 and a.level >= 1:
+                terms = [(a, c)] if c != 0 else []
+                return _LinearCiphertext(self, terms, [], 0, a.level - 1, a.batch)
             return self._call_ct(self._lib.mul_const, a._h, c.real, c.imag)
         scale = self._lib.engine_mul_scale(self._h, a.level)
         return self._call_ct(self._lib.mul_pt, a._h, pt.device(a.level, scale))
+
+    # -- deferred linear combinations (_LinearCiphertext) -------------------------------------
+    def _linear_add(self, a, b):
+        """a + b with at least one deferred operand: the merged deferred sum, or None when b is
+        not linear in the sense above (a non-constant plaintext, a 3-polynomial ciphertext)."""
+        L, o = (a, b) if isinstance(a, _LinearCiphertext) else (b, a)
+        if isinstance(o, Ciphertext):
+            if o.npoly != 2:
+                return None
+            if L.batch != o.batch and 1 not in (L.batch, o.batch):
+                raise RuntimeError(f"batch mismatch {L.batch} vs {o.batch}")
+            if isinstance(o, _LinearCiphertext):
+                terms, adds, const = L._terms + o._terms, L._addends + o._addends, L._const + o._const
+            else:
+                terms, adds, const = L._terms, L._addends + [o], L._const
+            return _LinearCiphertext(self, terms, adds, const, min(L.level, o.level), max(L.batch, o.batch))
+        pt = self._as_plain(o)
+        if not pt.is_const:
+            return None
+        return _LinearCiphertext(self, L._terms, L._addends, L._const + pt.const, L.level, L.batch)
+
+    def _materialize(self, L: "_LinearCiphertext") -> Ciphertext:
+        """One aesfhe_lincomb of the terms (one rescale of the sum), then the ciphertext addends
+        (level-aligned adds) and the constant, at the deferred object's level."""
+        x = None
+        if L._terms:
+            x = self.lincomb([c for c, _ in L._terms], [k for _, k in L._terms])
+        for c in L._addends:
+            x = c if x is None else self._call_ct(self._lib.add, x._h, c._h)
+        if x is None:
+            x = self.zeros(L.batch, L.level)
+        if x.batch < L.batch:  # every part was a broadcast (B = 1) operand
+            x = self.concat([x] * L.batch)
+        if L._const != 0:
+            x = self._call_ct(self._lib.add_const, x._h, L._const.real, L._const.imag)
+        if x.level > L.level:
+            x = self.level_down(x, L.level)
+        return x
 
     def multiply_fma(self, a: Ciphertext, b: Ciphertext, relinearization_key: RelinearizationKey,
                      alpha: int = 1, c: Ciphertext | None = None, gamma: float = 0.0,
@@ -680,6 +781,64 @@ class Engine:
         b, p, l1, _ = a.shape
         return self._call_ct(self._lib.ct_import, _as_ptr(a, C.c_uint64), b, p, l1 - 1)
 
+    # -- device-resident client path (aesfhe_*_device) -------------------
+    @property
+    def client_device(self):
+        """torch device of client-path buffers: the engine's GPU (HIP engine) or the CPU (the
+        oracle, whose "device" memory is host memory)."""
+        import torch
+        return torch.device("cuda", self.device_id) if self.on_device else torch.device("cpu")
+
+    def _torch_sync(self):
+        import torch
+        if self.on_device:
+            torch.cuda.current_stream(self.client_device).synchronize()
+
+    def encrypt_device(self, values, key, level: int | None = None) -> Ciphertext:
+        """Encrypt a (B, <= slot_count) torch tensor of slot values (real or complex) that lives
+        on `client_device`: device encode (aesfhe_encode_device, bit-identical to the host codec)
+        and encryption (aesfhe_encrypt_device), no host copy.  Same nonce sequence as encrypt."""
+        import torch
+        level = self.max_level if level is None else int(level)
+        dev = self.client_device
+        t = values if isinstance(values, torch.Tensor) else torch.as_tensor(np.asarray(values))
+        t = t.to(dev)
+        if t.ndim == 1:
+            t = t[None]
+        if t.ndim != 2 or t.shape[1] > self.slot_count:
+            raise ValueError(f"values must be (<= {self.slot_count},) or (B, <= {self.slot_count})")
+        B, ns = t.shape
+        if t.is_complex():
+            re, im = t.real.to(torch.float64).contiguous(), t.imag.to(torch.float64).contiguous()
+        else:
+            re, im = t.to(torch.float64).contiguous(), None
+        co = torch.empty((B, 1 << self.log_coeff_count), dtype=torch.int64, device=dev)
+        self._torch_sync()  # the slot tensors are written on torch's stream
+        self._check(self._lib.encode_device(self._h, re.data_ptr(), im.data_ptr() if im is not None else None,
+                                            B, ns, ns, self.scales[level], co.data_ptr()))
+        nonce = self._nonce
+        self._nonce += 1
+        out = C.c_void_p()
+        self._check(self._lib.encrypt_device(self._h, key._h, co.data_ptr(), B, level, nonce, C.byref(out)))
+        self.synchronize()  # co is read on the engine's stream; torch may recycle it on return
+        return self._ct(out.value)
+
+    def decrypt_device(self, ct: Ciphertext, sk: SecretKey):
+        """Decrypt + decode into a (B, slot_count) complex128 torch tensor on `client_device`
+        (aesfhe_decrypt_device + aesfhe_decode_device: no host copy)."""
+        import torch
+        dev = self.client_device
+        n = self.slot_count
+        co = torch.empty((ct.batch, 2 * n), dtype=torch.int64, device=dev)
+        re = torch.empty((ct.batch, n), dtype=torch.float64, device=dev)
+        im = torch.empty((ct.batch, n), dtype=torch.float64, device=dev)
+        self._torch_sync()
+        self._check(self._lib.decrypt_device(self._h, sk._h, ct._h, co.data_ptr()))
+        self._check(self._lib.decode_device(self._h, co.data_ptr(), ct.batch, self.scales[ct.level],
+                                            re.data_ptr(), im.data_ptr()))
+        self.synchronize()
+        return torch.complex(re, im)
+
     # -- device-resident transfer (parallel.py: RCCL scatter / gather) ------------------------
     @property
     def on_device(self) -> bool:
@@ -698,6 +857,15 @@ class Engine:
         return self._call_ct(self._lib.ct_import_device, C.c_void_p(ptr), int(batch), int(npoly), int(level))
 
     # -- serialisation --------------------------------------------------
+    def key_fingerprint(self) -> int:
+        """63-bit digest of the engine key (256-bit seed) and prime chain: equal on two engines
+        iff they derive the same keys from the same key seeds (parallel.py checks it across
+        ranks before moving ciphertexts between them)."""
+        import hashlib
+        p = self._params
+        h = hashlib.sha256(repr((p["seed"], tuple(p["seed_ext"]), tuple(self.primes))).encode()).digest()
+        return int.from_bytes(h[:8], "little") >> 1
+
     def _fingerprint(self) -> dict:
         return {"log_n": self.log_coeff_count, "max_level": self.max_level,
                 "special_primes": self.special_prime_count, "primes": self.primes}
@@ -758,9 +926,10 @@ class Engine:
     def pool_stats(self) -> dict:
         """Device pool counters (aesfhe_engine_pool_stats): bytes held / live, hipMalloc calls,
         trims, reuses of a larger cached block."""
-        a = (C.c_int64 * 5)()
+        a = (C.c_int64 * 7)()
         self._check(self._lib.engine_pool_stats(self._h, a))
-        return dict(zip(("held", "live", "mallocs", "trims", "reuse_larger"), [int(x) for x in a]))
+        return dict(zip(("held", "live", "mallocs", "trims", "reuse_larger", "peak_live", "fragmentation"),
+                        [int(x) for x in a]))
 
     def pool_trim(self):
         """Release the cached device blocks (aesfhe_engine_pool_trim), e.g. between workloads."""

@@ -12,8 +12,12 @@ memory.  With the CPU oracle engine (tests, "gloo") the same code runs on host t
 HIP engine under gloo (several ranks rehearsing on one GPU, which RCCL refuses) the residues
 are staged through host tensors.
 
-Keys are never moved: every rank derives the same keys from the shared engine seed; each rank
-encrypts with its own nonce range (`rank_nonce_start`) so no two ranks reuse randomness.
+Keys are never moved: every rank derives the same keys from one 256-bit engine seed that rank 0
+draws and broadcasts (`shared_seed`); each rank encrypts with its own nonce range
+(`rank_nonce_start`) so no two ranks reuse randomness.  Before the first transfer over a process
+group the ranks compare `Engine.key_fingerprint()`: engines with different keys (e.g. default
+engines, each with its own random key) raise instead of computing on ciphertexts they cannot
+decrypt.
 """
 from __future__ import annotations
 
@@ -31,6 +35,41 @@ def shard_range(total: int, world: int, rank: int):
 def rank_nonce_start(rank: int) -> int:
     """First encryption nonce of `rank` for engines sharing one seed: disjoint 2^48 ranges."""
     return (int(rank) + 1) << 48
+
+
+def shared_seed(group=None, src: int = 0) -> int:
+    """A 256-bit engine seed drawn from os.urandom on rank `src` and broadcast to every rank (the
+    same on all of them), or a fresh local one without torch.distributed."""
+    import os
+    seed = int.from_bytes(os.urandom(32), "little")
+    try:
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            return seed
+    except ImportError:
+        return seed
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    words = torch.tensor([(seed >> (63 * i)) & ((1 << 63) - 1) for i in range(5)], dtype=torch.int64, device=dev)
+    dist.broadcast(words, src, group=group)
+    return sum(int(w) << (63 * i) for i, w in enumerate(words.cpu().tolist())) & ((1 << 256) - 1)
+
+
+def _check_keys(engine, group, dev):
+    """Raise unless every rank's engine derives the same keys (once per engine and group)."""
+    import torch
+    import torch.distributed as dist
+    done = engine.__dict__.setdefault("_fp_groups", set())
+    gid = id(group)
+    if gid in done:
+        return
+    mine = torch.tensor([engine.key_fingerprint()], dtype=torch.int64, device=dev)
+    allf = [torch.empty_like(mine) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(allf, mine, group=group)
+    if len({int(t.item()) for t in allf}) != 1:
+        raise RuntimeError("ranks hold engines with different keys (engine seed / prime chain): "
+                           "create every rank's Engine with one shared seed (parallel.shared_seed)")
+    done.add(gid)
 
 
 def _torch_device(engine, group=None):
@@ -81,6 +120,7 @@ def scatter_ciphertext(engine, ct, src: int = 0, group=None):
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     dev = _torch_device(engine, group)
+    _check_keys(engine, group, dev)
     meta = torch.zeros(3, dtype=torch.int64, device=dev)
     if rank == src:
         meta = torch.tensor([ct.batch, ct.npoly, ct.level], dtype=torch.int64, device=dev)
@@ -109,11 +149,13 @@ def scatter_ciphertext(engine, ct, src: int = 0, group=None):
 
 def gather_ciphertext(engine, ct, dst: int = 0, group=None):
     """Concatenate every rank's batched ciphertext (same npoly / level on all ranks, batch may
-    differ; a rank may pass None for an empty share) on rank `dst`, in rank order."""
+    differ; a rank may pass None for an empty share) on rank `dst`, in rank order.  None on
+    every rank if every share is empty."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     dev = _torch_device(engine, group)
+    _check_keys(engine, group, dev)
     mine = torch.tensor([ct.batch if ct is not None else 0,
                          ct.npoly if ct is not None else -1,
                          ct.level if ct is not None else -1], dtype=torch.int64, device=dev)
@@ -121,6 +163,8 @@ def gather_ciphertext(engine, ct, dst: int = 0, group=None):
     dist.all_gather(metas, mine, group=group)
     metas = [m.cpu().tolist() for m in metas]
     shapes = {(p, l) for b, p, l in metas if b > 0}
+    if not shapes:  # every share empty: nothing to gather
+        return None
     if len(shapes) != 1:
         raise ValueError(f"gather_ciphertext: ranks disagree on (npoly, level): {sorted(shapes)}")
     npoly, level = shapes.pop()

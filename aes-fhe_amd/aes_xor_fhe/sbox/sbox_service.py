@@ -60,12 +60,35 @@ class SBoxService:
         return self.sub_bytes(enc_arr)
 
     def sub_bytes_fused(self, enc_arr: Any) -> Any:
+        """Same hi / lo polynomials, evaluated with half the basis.  The input slots are 256-th
+        roots of unity (zeta_256^x), where x^(256-i) = conj(x^i); so with the powers x^1..x^128,
+        P(x) = c_0 + sum_{i<=128} c_i x^i + conj(sum_{i<128} conj(c_{256-i}) x^i): 127 basis
+        products instead of 254, the four sums in one lincomb_many pass, one conjugation per
+        polynomial.  One level fewer than sub_bytes (x^128 needs 7 levels, x^255 eight).  Without
+        a conjugation key in the context it falls back to one lincomb over the full basis."""
         e = self.engine
-        powers = self._build_power_basis(enc_arr)
+        cjk = getattr(self.ctx, "conjugation_key", None)
+        hi, lo = self.coeffs_hi, self.coeffs_lo
+        if cjk is None or len(hi) != 256 or len(lo) != 256:
+            powers = self._build_power_basis(enc_arr)
+            outs = []
+            for c in (hi, lo):
+                ks = [k for k in range(1, len(c)) if abs(c[k]) >= 1e-12]
+                o = e.lincomb([powers[k - 1] for k in ks], [c[k] for k in ks])
+                if abs(c[0]) >= 1e-12:
+                    o = e.add(o, complex(c[0]))
+                outs.append(o)
+            return e.multiply(outs[0], outs[1], self.rlk)
+        powers = e.make_power_basis(enc_arr, 128, self.rlk)
+        rows = []
+        for c in (hi, lo):
+            c = np.asarray(c, dtype=np.complex128)
+            rows.append(c[1:129])
+            rows.append(np.concatenate([np.conj(c[255:128:-1]), [0.0]]))
+        s = e.lincomb_many(powers, np.stack(rows))
         outs = []
-        for c in (self.coeffs_hi, self.coeffs_lo):
-            ks = [k for k in range(1, len(c)) if abs(c[k]) >= 1e-12]
-            o = e.lincomb([powers[k - 1] for k in ks], [c[k] for k in ks])
+        for t, c in enumerate((hi, lo)):
+            o = e.add(s[2 * t], e.conjugate(s[2 * t + 1], cjk))
             if abs(c[0]) >= 1e-12:
                 o = e.add(o, complex(c[0]))
             outs.append(o)

@@ -1,0 +1,176 @@
+// arena.h -- chunked best-fit arena for the engine's device memory (host logic only).
+//
+// Device memory is taken from the injected allocator in large chunks (Arena::chunk_bytes; a
+// larger request gets a chunk of its own) and carved by best fit with 256-B granularity; a freed
+// block merges with its free neighbours of the same chunk.  Every size shares every chunk, so the
+// memory held tracks the peak live set plus fragmentation instead of the sum of per-size-class
+// peaks (the size-class pool this replaced held 250 GB for 64 GB live in the bench round and
+// thrashed -- hipFree / hipMalloc + device syncs inside the timed region -- on the N = 2^17
+// ten-round run).  The engine enqueues all work on one stream, so a block freed by the host is
+// reused only by later stream-ordered work.  trim() returns the chunks that hold no live block.
+//
+// The allocator is injected (engine.hip: hipMalloc / hipFree / hipDeviceSynchronize;
+// tests/native/arena_asan.cpp: malloc / free under AddressSanitizer), so this header has no HIP
+// dependency and is unit-tested on the CPU.
+#pragma once
+#include <algorithm>
+#include <cstddef>
+#include <cstdint>
+#include <iterator>
+#include <map>
+#include <unordered_map>
+
+namespace aesfhe {
+
+struct ArenaAllocator {
+    void* (*alloc)(size_t bytes, void* ctx);  // nullptr on failure
+    void (*release)(void* p, void* ctx);
+    void (*sync)(void* ctx);                   // before chunks are returned
+    void* ctx;
+};
+
+struct Arena {
+    static constexpr size_t kAlign = 256;
+    ArenaAllocator A{};
+    size_t chunk_bytes = (size_t)1 << 33;
+    std::map<char*, size_t> chunks_;                  // base -> size
+    std::map<char*, size_t> free_addr_;               // free block -> size (address order)
+    std::multimap<size_t, char*> free_size_;          // size -> free block (best fit)
+    std::unordered_map<void*, size_t> live_;          // live block -> size
+    size_t held = 0, live = 0, peak_live = 0;
+    int64_t mallocs = 0, trims = 0, reuse_larger = 0;  // reuse_larger: blocks split off a larger free one
+
+    static size_t round_up(size_t bytes) { return std::max(kAlign, (bytes + kAlign - 1) & ~(kAlign - 1)); }
+
+    void add_free(char* p, size_t n) {
+        free_addr_[p] = n;
+        free_size_.insert({n, p});
+    }
+    void del_free(char* p, size_t n) {
+        free_addr_.erase(p);
+        auto r = free_size_.equal_range(n);
+        for (auto it = r.first; it != r.second; ++it)
+            if (it->second == p) {
+                free_size_.erase(it);
+                return;
+            }
+    }
+    char* chunk_of(char* p) const {
+        auto it = chunks_.upper_bound(p);
+        return it == chunks_.begin() ? nullptr : std::prev(it)->first;
+    }
+    bool new_chunk(size_t need) {
+        size_t want = std::max(chunk_bytes, need);
+        void* p = A.alloc(want, A.ctx);
+        if (!p && want > need) {  // nearly full: release empty chunks, then the exact need
+            trim();
+            want = need;
+            p = A.alloc(want, A.ctx);
+        }
+        if (!p) return false;
+        mallocs++;
+        held += want;
+        chunks_[(char*)p] = want;
+        add_free((char*)p, want);
+        return true;
+    }
+    // a block of at least `bytes` (256-B aligned within its chunk), or nullptr if the allocator fails
+    void* get(size_t bytes) {
+        const size_t n = round_up(bytes);
+        auto it = free_size_.lower_bound(n);
+        if (it == free_size_.end()) {
+            if (!new_chunk(n)) return nullptr;
+            it = free_size_.lower_bound(n);
+        }
+        char* p = it->second;
+        const size_t have = it->first;
+        free_size_.erase(it);
+        free_addr_.erase(p);
+        if (have > n) {
+            add_free(p + n, have - n);
+            reuse_larger++;
+        }
+        live_[p] = n;
+        live += n;
+        peak_live = std::max(peak_live, live);
+        return p;
+    }
+    // return a live block (unknown pointers, e.g. nullptr, are ignored)
+    void put(void* vp) {
+        if (!vp) return;
+        auto lt = live_.find(vp);
+        if (lt == live_.end()) return;
+        char* p = (char*)vp;
+        size_t n = lt->second;
+        live_.erase(lt);
+        live -= n;
+        char* ch = chunk_of(p);
+        // merge with the free block after p, then with the one before (same chunk only)
+        auto nx = free_addr_.find(p + n);
+        if (nx != free_addr_.end() && chunk_of(nx->first) == ch) {
+            const size_t m = nx->second;
+            del_free(p + n, m);
+            n += m;
+        }
+        auto pv = free_addr_.lower_bound(p);
+        if (pv != free_addr_.begin()) {
+            --pv;
+            if (pv->first + pv->second == p && chunk_of(pv->first) == ch) {
+                char* q = pv->first;
+                const size_t m = pv->second;
+                del_free(q, m);
+                p = q;
+                n += m;
+            }
+        }
+        add_free(p, n);
+    }
+    // return every chunk without a live block to the allocator (one sync first)
+    void trim() {
+        A.sync(A.ctx);
+        trims++;
+        for (auto it = chunks_.begin(); it != chunks_.end();) {
+            auto f = free_addr_.find(it->first);
+            if (f != free_addr_.end() && f->second == it->second) {
+                del_free(it->first, it->second);
+                A.release(it->first, A.ctx);
+                held -= it->second;
+                it = chunks_.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    }
+    // turn the live block p (exactly parts * part bytes, part a multiple of kAlign) into `parts`
+    // live blocks of `part` bytes each, freed independently (zero-copy split of a batched result);
+    // false if p is not such a block
+    bool split(void* p, int parts, size_t part) {
+        auto lt = live_.find(p);
+        if (lt == live_.end() || parts < 1 || part % kAlign || lt->second != (size_t)parts * part) return false;
+        live_.erase(lt);
+        for (int t = 0; t < parts; t++) live_[(char*)p + (size_t)t * part] = part;
+        return true;
+    }
+    // bytes held in chunks that also hold live blocks, minus the live bytes: what the arena keeps
+    // that neither serves a live block nor could be returned by trim()
+    size_t fragmentation() const {
+        size_t f = 0;
+        for (auto& kv : chunks_) {
+            auto it = free_addr_.find(kv.first);
+            if (it != free_addr_.end() && it->second == kv.second) continue;  // empty chunk
+            f += kv.second;
+        }
+        return f - std::min(f, live);
+    }
+    void release_all() {  // teardown: no live block remains in use
+        A.sync(A.ctx);
+        for (auto& kv : chunks_) A.release(kv.first, A.ctx);
+        chunks_.clear();
+        free_addr_.clear();
+        free_size_.clear();
+        live_.clear();
+        held = live = 0;
+    }
+};
+
+}  // namespace aesfhe

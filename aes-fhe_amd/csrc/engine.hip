@@ -2,8 +2,8 @@
 //
 // Replaces the closed desilofhe.Engine the reference calls (engine_context.py:6,32-85;
 // xor_service.py:36-129).  One HIP stream per engine; every operation is enqueued
-// asynchronously and host reads (decrypt / export) synchronise.  Device memory is recycled
-// through a size-bucketed pool, so steady-state operations never call hipMalloc.
+// asynchronously and host reads (decrypt / export) synchronise.  Device memory comes from a
+// chunked best-fit arena (arena.h), so steady-state operations never call hipMalloc.
 // Specification of every integer step: DESIGN.md section 3 (restated by oracle/ckks_oracle.c).
 #include <hip/hip_runtime.h>
 
@@ -24,6 +24,8 @@
 #include "kernels_ops.h"
 #include "ntt256f.h"
 #include "ks_fused.h"
+#include "arena.h"
+#include "codec_dev.h"
 
 using namespace aesfhe;
 
@@ -78,143 +80,31 @@ extern "C" const char* aesfhe_backend_name(void) { return "hip-gfx950"; }
 
 // -----------------------------------------------------------------------------------------------
 // engine state
-struct Pool {
-    // Chunked best-fit arena.  Device memory is taken from HIP in large chunks (default 16384
-    // limbs, i.e. 8 GiB at N = 2^16; a larger request gets a chunk of its own) and carved by
-    // best fit with 256-B granularity; a freed block merges with its free neighbours of the same
-    // chunk.  Every size shares every chunk, so the memory held tracks the peak live set plus
-    // fragmentation instead of the sum of per-size-class peaks (the size-class pool this replaces
-    // held 250 GB for 64 GB live in the bench round and thrashed -- hipFree / hipMalloc + device
-    // syncs inside the timed region -- on the N = 2^17 ten-round run).  All work is enqueued on
-    // the engine's one stream, so a block freed by the host is reused only by later stream-ordered
-    // work (as before).  trim() returns the chunks that hold no live block.
-    static constexpr size_t kAlign = 256;
-    size_t chunk_bytes = (size_t)1 << 33;
-    std::map<char*, size_t> chunks_;                  // base -> size
-    std::map<char*, size_t> free_addr_;               // free block -> size (address order)
-    std::multimap<size_t, char*> free_size_;          // size -> free block (best fit)
-    std::unordered_map<void*, size_t> live_;          // live block -> size
-    size_t held = 0, live = 0;
-    int64_t mallocs = 0, trims = 0, reuse_larger = 0;  // reuse_larger: blocks split off a larger free one
-    size_t cap = 0;  // unused (kept for the stats ABI); chunk allocation failures are handled below
-    void add_free(char* p, size_t n) {
-        free_addr_[p] = n;
-        free_size_.insert({n, p});
-    }
-    void del_free(char* p, size_t n) {
-        free_addr_.erase(p);
-        auto r = free_size_.equal_range(n);
-        for (auto it = r.first; it != r.second; ++it)
-            if (it->second == p) {
-                free_size_.erase(it);
-                return;
+// Device memory: the chunked best-fit arena of arena.h over hipMalloc / hipFree (its host logic
+// is unit-tested on the CPU under AddressSanitizer, tests/native/arena_asan.cpp).
+struct Pool : Arena {
+    Pool() {
+        A.alloc = [](size_t n, void*) -> void* {
+            void* p = nullptr;
+            if (hipMalloc(&p, n) != hipSuccess) {
+                (void)hipGetLastError();
+                return nullptr;
             }
-    }
-    char* chunk_of(char* p) {
-        auto it = chunks_.upper_bound(p);
-        return it == chunks_.begin() ? nullptr : std::prev(it)->first;
-    }
-    bool new_chunk(size_t need) {
-        size_t want = std::max(chunk_bytes, need);
-        void* p = nullptr;
-        hipError_t e = hipMalloc(&p, want);
-        if (e != hipSuccess && want > need) {  // nearly full: release empty chunks, then the exact need
-            (void)hipGetLastError();
-            trim();
-            want = need;
-            e = hipMalloc(&p, want);
-        }
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-        }
-        mallocs++;
-        held += want;
-        chunks_[(char*)p] = want;
-        add_free((char*)p, want);
-        return true;
+            return p;
+        };
+        A.release = [](void* p, void*) { hipFree(p); };
+        A.sync = [](void*) { hipDeviceSynchronize(); };
+        A.ctx = nullptr;
     }
     void* get(size_t bytes) {
-        const size_t n = std::max(kAlign, (bytes + kAlign - 1) & ~(kAlign - 1));
-        auto it = free_size_.lower_bound(n);
-        if (it == free_size_.end()) {
-            if (!new_chunk(n)) throw_err(AESFHE_ENOMEM, "device allocation of %zu bytes failed (%zu held, %zu live)", n, held, live);
-            it = free_size_.lower_bound(n);
-        }
-        char* p = it->second;
-        const size_t have = it->first;
-        free_size_.erase(it);
-        free_addr_.erase(p);
-        if (have > n) {
-            add_free(p + n, have - n);
-            reuse_larger++;
-        }
-        live_[p] = n;
-        live += n;
+        void* p = Arena::get(bytes);
+        if (!p) throw_err(AESFHE_ENOMEM, "device allocation of %zu bytes failed (%zu held, %zu live)", round_up(bytes), held, live);
         return p;
     }
-    void put(void* vp, size_t) {
-        if (!vp) return;
-        auto lt = live_.find(vp);
-        if (lt == live_.end()) return;
-        char* p = (char*)vp;
-        size_t n = lt->second;
-        live_.erase(lt);
-        live -= n;
-        char* ch = chunk_of(p);
-        // merge with the free block after p, then with the one before (same chunk only)
-        auto nx = free_addr_.find(p + n);
-        if (nx != free_addr_.end() && chunk_of(nx->first) == ch) {
-            const size_t m = nx->second;
-            del_free(p + n, m);
-            n += m;
-        }
-        auto pv = free_addr_.lower_bound(p);
-        if (pv != free_addr_.begin()) {
-            --pv;
-            if (pv->first + pv->second == p && chunk_of(pv->first) == ch) {
-                char* q = pv->first;
-                const size_t m = pv->second;
-                del_free(q, m);
-                p = q;
-                n += m;
-            }
-        }
-        add_free(p, n);
-    }
-    // return every chunk without a live block to HIP (one device sync)
-    void trim() {
-        hipDeviceSynchronize();
-        trims++;
-        for (auto it = chunks_.begin(); it != chunks_.end();) {
-            auto f = free_addr_.find(it->first);
-            if (f != free_addr_.end() && f->second == it->second) {
-                del_free(it->first, it->second);
-                hipFree(it->first);
-                held -= it->second;
-                it = chunks_.erase(it);
-            } else {
-                ++it;
-            }
-        }
-    }
-    // turn the live block p (exactly parts * part bytes, part a multiple of kAlign) into `parts`
-    // live blocks of `part` bytes each, freed independently (zero-copy split of a batched result)
+    void put(void* p, size_t) { Arena::put(p); }
     void split(void* p, int parts, size_t part) {
-        auto lt = live_.find(p);
-        if (lt == live_.end() || part % kAlign || lt->second != (size_t)parts * part)
+        if (!Arena::split(p, parts, part))
             throw_err(AESFHE_EARG, "pool split of a block that is not %d x %zu bytes", parts, part);
-        live_.erase(lt);
-        for (int t = 0; t < parts; t++) live_[(char*)p + (size_t)t * part] = part;
-    }
-    void release_all() {  // engine teardown: no live block remains
-        hipDeviceSynchronize();
-        for (auto& kv : chunks_) hipFree(kv.first);
-        chunks_.clear();
-        free_addr_.clear();
-        free_size_.clear();
-        live_.clear();
-        held = live = 0;
     }
 };
 
@@ -256,6 +146,11 @@ struct aesfhe_engine {
     char* ring_d = nullptr;
     char* ring_h = nullptr;
     size_t ring_size = 8u << 20, ring_off = 0;
+    // device codec (codec_dev.h): twiddles / rotation table built on first use, overflow flags
+    double *ckre = nullptr, *ckim = nullptr;
+    long* crot = nullptr;
+    int* cflags = nullptr;
+    size_t cflags_n = 0;
     // aesfhe_poly2 constant tables, keyed by (level, shape, coefficients)
     std::map<std::string, TwD*> poly2_tabs;
     // profiling
@@ -828,8 +723,13 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
     HIPC(hipSetDevice(e->device));
     HIPC(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     build_tables(e.get());
-    // arena chunks of 16384 limbs (8 GiB at N = 2^16), at least 256 MiB
+    // arena chunks of 16384 limbs (8 GiB at N = 2^16), at least 256 MiB; AESFHE_ARENA_CHUNK_MB
+    // overrides it (several engines sharing one GPU, small batches)
     e->pool.chunk_bytes = std::max((size_t)1 << 28, ((size_t)16384 * 8) << e->logN);
+    if (const char* cm = getenv("AESFHE_ARENA_CHUNK_MB")) {
+        const long mb = atol(cm);
+        if (mb > 0) e->pool.chunk_bytes = (size_t)mb << 20;
+    }
     HIPC(hipMalloc(&e->ring_d, e->ring_size));
     HIPC(hipHostMalloc((void**)&e->ring_h, e->ring_size, hipHostMallocDefault));
     *out = e.release();
@@ -868,6 +768,8 @@ static void engine_teardown(aesfhe_engine* e) {
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto& kv : e->poly2_tabs) hipFree(kv.second);
+    for (void* p : {(void*)e->ckre, (void*)e->ckim, (void*)e->crot, (void*)e->cflags})
+        if (p) hipFree(p);
     if (e->ring_h) hipHostFree(e->ring_h);
     hipStreamDestroy(e->stream);
     delete e;
@@ -943,6 +845,8 @@ extern "C" int aesfhe_engine_pool_stats(const aesfhe_engine* e, int64_t* out) {
     out[2] = e->pool.mallocs;
     out[3] = e->pool.trims;
     out[4] = e->pool.reuse_larger;
+    out[5] = (int64_t)e->pool.peak_live;
+    out[6] = (int64_t)e->pool.fragmentation();
     return AESFHE_OK;
 }
 
@@ -1345,17 +1249,23 @@ extern "C" void aesfhe_pt_free(aesfhe_pt* p) {
 
 // -----------------------------------------------------------------------------------------------
 // encryption / decryption
-extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int64_t* co, int32_t B,
-                              int32_t level, uint64_t nonce, aesfhe_ct** out) {
-    API_BEGIN
+// encryption of B coefficient vectors (int64, B x N) held on the host (aesfhe_encrypt) or on the
+// device (aesfhe_encrypt_device)
+static aesfhe_ct* encrypt_coeffs(aesfhe_engine* e, const aesfhe_key* key, const int64_t* co, int B, int level,
+                                 uint64_t nonce, bool host) {
     if (!key || (key->kind != 0 && key->kind != 1)) throw_err(AESFHE_EARG, "encryption key must be pk or sk");
     if (level < 0 || level > e->L || B < 1) throw_err(AESFHE_EARG, "bad level/batch");
     const int N = e->N, nl = level + 1;
     const long step = (long)nl * N;
     aesfhe_ct* c = ct_new(e, B, 2, level);
     Tmp vem(e, (size_t)B * 4 * step);
-    Tmp dco(e, (size_t)B * N);
-    HIPC(hipMemcpyAsync(dco.p, co, (size_t)B * N * 8, hipMemcpyHostToDevice, e->stream));
+    std::unique_ptr<Tmp> hco;
+    const u64* dcop = (const u64*)co;
+    if (host) {
+        hco.reset(new Tmp(e, (size_t)B * N));
+        HIPC(hipMemcpyAsync(hco->p, co, (size_t)B * N * 8, hipMemcpyHostToDevice, e->stream));
+        dcop = hco->p;
+    }
     const u64 base = derive(derive(e->seed, 0xE0CULL), nonce);
     std::vector<u64> k0s(B);
     for (int b = 0; b < B; b++) {
@@ -1368,7 +1278,7 @@ extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int
         hipLaunchKernelGGL(k_sample_small, dim3((N / 8 + 255) / 256), dim3(256), 0, e->stream, se0, e->ck, k1, 1, e->q, e->logN, e->Lp1, nl);
         if (key->kind == 1)
             hipLaunchKernelGGL(k_sample_small, dim3((N / 8 + 255) / 256), dim3(256), 0, e->stream, se1, e->ck, k2, 1, e->q, e->logN, e->Lp1, nl);
-        hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, nl, 1), dim3(256), 0, e->stream, (const i64*)(dco.p + (size_t)b * N), vb + 3 * step, nl, e->q, e->logN);
+        hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, nl, 1), dim3(256), 0, e->stream, (const i64*)(dcop + (size_t)b * N), vb + 3 * step, nl, e->q, e->logN);
     }
     // NTT everything: B * 4 groups of nl limbs (pid = limb index)
     Span all = span_s(vem.p, step, nl, nl, 0, e->Lp1);
@@ -1382,8 +1292,14 @@ extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int
         hipLaunchKernelGGL(k_enc_sk, dim3((N / 8 + 255) / 256, nl, B), dim3(256), 0, e->stream, (const u64*)vem.p, (const u64*)key->d, c->d, nl, e->q, e->qinv, e->ck, (const u64*)dk, e->logN);
     }
     HIPC(hipGetLastError());
-    HIPC(hipStreamSynchronize(e->stream));  // host coefficient buffer may be reused by caller
-    *out = c;
+    if (host) HIPC(hipStreamSynchronize(e->stream));  // host coefficient buffer may be reused by caller
+    return c;
+}
+
+extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int64_t* co, int32_t B,
+                              int32_t level, uint64_t nonce, aesfhe_ct** out) {
+    API_BEGIN
+    *out = encrypt_coeffs(e, key, co, B, level, nonce, true);
     API_END
 }
 
@@ -1391,20 +1307,14 @@ extern "C" int aesfhe_encrypt(aesfhe_engine* e, const aesfhe_key* key, const int
 // ciphertext has it; the two residues are CRT-combined and centred mod q0 q1 (a level-0
 // ciphertext: mod q0), so the plaintext capacity is q0 q1 / (2 Delta) instead of q0 / (2 Delta)
 // (= 32 at a 44-bit scale).  Coefficients beyond +-(2^63 - 1) saturate.
+static void decrypt_limbs(aesfhe_engine* e, const aesfhe_key* sk, const aesfhe_ct* c, u64* t, int nl);
 extern "C" int aesfhe_decrypt(aesfhe_engine* e, const aesfhe_key* sk, const aesfhe_ct* c, int64_t* out) {
     API_BEGIN
     if (!sk || sk->kind != 0) throw_err(AESFHE_EARG, "decryption needs the secret key");
     const int N = e->N;
     const int nl = c->level >= 1 ? 2 : 1;
     Tmp t(e, (size_t)nl * c->B * N);
-    View v = view_of(c);
-    for (int i = 0; i < nl; i++) {
-        u64* ti = t.p + (size_t)i * c->B * N;
-        hipLaunchKernelGGL(k_dec_limb0, dim3(N / 256, 1, c->B), dim3(256), 0, e->stream, v.d + (size_t)i * N, v.bs, v.ps, c->np,
-                           (const u64*)sk->d + (size_t)i * N, ti, e->chain.q[i], 1.0 / (double)e->chain.q[i], e->logN);
-        Span s = span_s(ti, N, 1, 1, i, e->Lp1);
-        ntt(e, s, s, c->B, true);
-    }
+    decrypt_limbs(e, sk, c, t.p, nl);
     std::vector<u64> h((size_t)nl * c->B * N);
     HIPC(hipMemcpyAsync(h.data(), t.p, h.size() * 8, hipMemcpyDeviceToHost, e->stream));
     HIPC(hipStreamSynchronize(e->stream));
@@ -1427,6 +1337,105 @@ extern "C" int aesfhe_decrypt(aesfhe_engine* e, const aesfhe_key* sk, const aesf
             }
         }
     }
+    API_END
+}
+
+// -----------------------------------------------------------------------------------------------
+// device-resident client path: the codec of aesfhe_encode / aesfhe_decode and
+// the encryption / decryption on device buffers, stream-ordered on the engine's stream.
+static CodecTabs codec_tabs(aesfhe_engine* e) {
+    const int n = e->N / 2;
+    const long M = 2L * e->N;
+    if (!e->ckre) {
+        Codec c(e->logN);  // host twiddles (libm cos / sin): the device tables are the same doubles
+        HIPC(hipMalloc(&e->ckre, (M + 1) * sizeof(double)));
+        HIPC(hipMalloc(&e->ckim, (M + 1) * sizeof(double)));
+        HIPC(hipMalloc(&e->crot, n * sizeof(long)));
+        HIPC(hipMemcpy(e->ckre, c.kre.data(), (M + 1) * sizeof(double), hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(e->ckim, c.kim.data(), (M + 1) * sizeof(double), hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(e->crot, c.rot.data(), n * sizeof(long), hipMemcpyHostToDevice));
+    }
+    return CodecTabs{e->ckre, e->ckim, e->crot, M, n, e->logN - 1};
+}
+
+static unsigned blocks_for(long count) { return (unsigned)((count + 255) / 256); }
+
+extern "C" int aesfhe_encode_device(aesfhe_engine* e, const double* re, const double* im, int32_t B, int64_t n_slots,
+                                    int64_t stride, double scale, int64_t* co) {
+    API_BEGIN
+    const CodecTabs T = codec_tabs(e);
+    const int n = T.n;
+    if (B < 1 || n_slots < 0 || n_slots > n || stride < n_slots || !co) throw_err(AESFHE_EARG, "bad encode shape");
+    Tmp a(e, (size_t)B * 2 * n), b(e, (size_t)B * 2 * n);
+    double *ar = (double*)a.p, *ai = ar + (size_t)B * n, *br = (double*)b.p, *bi = br + (size_t)B * n;
+    const long tot = (long)B * n, bfly = (long)B * (n / 2);
+    hipLaunchKernelGGL(k_sfft_load, dim3(blocks_for(tot)), dim3(256), 0, e->stream, re, im, (long)stride, (long)n_slots, ar, ai, n, B);
+    for (int len = n; len >= 2; len >>= 1)  // len = 1 butterflies are identities (lenh = 0)
+        hipLaunchKernelGGL(k_sfft_inv_stage, dim3(blocks_for(bfly)), dim3(256), 0, e->stream, ar, ai, T, len, B);
+    hipLaunchKernelGGL(k_sfft_bitrev, dim3(blocks_for(tot)), dim3(256), 0, e->stream, (const double*)ar, (const double*)ai, br, bi, n, T.logn, B);
+    const unsigned nb = blocks_for(tot);
+    if (e->cflags_n < nb) {
+        if (e->cflags) HIPC(hipFree(e->cflags));
+        HIPC(hipMalloc(&e->cflags, nb * sizeof(int)));
+        e->cflags_n = nb;
+    }
+    hipLaunchKernelGGL(k_sfft_round, dim3(nb), dim3(256), 0, e->stream, (const double*)br, (const double*)bi, n, B, scale, co, e->cflags);
+    HIPC(hipGetLastError());
+    std::vector<int> fl(nb);
+    HIPC(hipMemcpyAsync(fl.data(), e->cflags, nb * sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    HIPC(hipStreamSynchronize(e->stream));
+    for (int f : fl)
+        if (f) throw_err(AESFHE_EARG, "encoded coefficient overflows int64 (scale too large?)");
+    API_END
+}
+
+extern "C" int aesfhe_decode_device(aesfhe_engine* e, const int64_t* co, int32_t B, double scale, double* re, double* im) {
+    API_BEGIN
+    const CodecTabs T = codec_tabs(e);
+    const int n = T.n;
+    if (B < 1 || !co || !re || !im) throw_err(AESFHE_EARG, "bad decode arguments");
+    const long tot = (long)B * n, bfly = (long)B * (n / 2);
+    hipLaunchKernelGGL(k_sfft_unround, dim3(blocks_for(tot)), dim3(256), 0, e->stream, co, n, T.logn, B, scale, re, im);
+    for (int len = 2; len <= n; len <<= 1)
+        hipLaunchKernelGGL(k_sfft_fwd_stage, dim3(blocks_for(bfly)), dim3(256), 0, e->stream, re, im, T, len, B);
+    HIPC(hipGetLastError());
+    API_END
+}
+
+extern "C" int aesfhe_encrypt_device(aesfhe_engine* e, const aesfhe_key* key, const int64_t* co, int32_t B,
+                                     int32_t level, uint64_t nonce, aesfhe_ct** out) {
+    API_BEGIN
+    if (!co) throw_err(AESFHE_EARG, "null coefficient buffer");
+    *out = encrypt_coeffs(e, key, co, B, level, nonce, false);
+    API_END
+}
+
+// residues of limb 0 (and 1) of c + c1 s (+ c2 s^2), coefficient domain: t[i * B * N ...]
+static void decrypt_limbs(aesfhe_engine* e, const aesfhe_key* sk, const aesfhe_ct* c, u64* t, int nl) {
+    const int N = e->N;
+    View v = view_of(c);
+    for (int i = 0; i < nl; i++) {
+        u64* ti = t + (size_t)i * c->B * N;
+        hipLaunchKernelGGL(k_dec_limb0, dim3(N / 256, 1, c->B), dim3(256), 0, e->stream, v.d + (size_t)i * N, v.bs, v.ps, c->np,
+                           (const u64*)sk->d + (size_t)i * N, ti, e->chain.q[i], 1.0 / (double)e->chain.q[i], e->logN);
+        Span s = span_s(ti, N, 1, 1, i, e->Lp1);
+        ntt(e, s, s, c->B, true);
+    }
+}
+
+extern "C" int aesfhe_decrypt_device(aesfhe_engine* e, const aesfhe_key* sk, const aesfhe_ct* c, int64_t* co) {
+    API_BEGIN
+    if (!sk || sk->kind != 0) throw_err(AESFHE_EARG, "decryption needs the secret key");
+    if (!co) throw_err(AESFHE_EARG, "null coefficient buffer");
+    const int N = e->N, nl = c->level >= 1 ? 2 : 1;
+    Tmp t(e, (size_t)nl * c->B * N);
+    decrypt_limbs(e, sk, c, t.p, nl);
+    const long cnt = (long)c->B * N;
+    const u64 q0 = e->chain.q[0], q1 = nl == 2 ? e->chain.q[1] : 1;
+    hipLaunchKernelGGL(k_dec_crt, dim3(blocks_for(cnt)), dim3(256), 0, e->stream, (const uint64_t*)t.p,
+                       nl == 2 ? (const uint64_t*)t.p + cnt : (const uint64_t*)nullptr, cnt, q0, q1,
+                       nl == 2 ? h_invmod(q0 % q1, q1) : 0, co);
+    HIPC(hipGetLastError());
     API_END
 }
 

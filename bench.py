@@ -51,7 +51,7 @@ sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
 
 PEAK_HBM_GBS = 8000.0
 METRIC = "AES-128 blocks/sec (homomorphic full round) at N=2^16, L=30; 1/2/4/8 MI355X"
-SEED = 0x5EED5EED  # shared by every rank: identical keys without key traffic
+SEED = 0x5EED5EED  # the CPU baseline's engine (reproducible); the GPU ranks share a 256-bit seed
 
 PMC_FILE = ROOT / "profiles" / "r02" / "pmc" / "ntt_traffic.json"
 PMC_NOTE = ("HBM bytes per NTT launch = algorithmic bytes x the HBM/algorithmic ratio measured by "
@@ -142,9 +142,10 @@ class RoundDriver:
 
 def setup_engine(args, device, rank):
     from aes_xor_fhe.fhe import Engine
-    from aes_xor_fhe.parallel import rank_nonce_start
+    from aes_xor_fhe.parallel import rank_nonce_start, shared_seed
+    # one 256-bit engine key drawn on rank 0 and broadcast: every rank derives the same keys
     eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes,
-                 scale_bits=args.scale_bits, device_id=device, seed=SEED,
+                 scale_bits=args.scale_bits, device_id=device, seed=shared_seed(),
                  nonce_start=rank_nonce_start(rank))
     sk = eng.create_secret_key(1)
     pk = eng.create_public_key(sk)
@@ -236,7 +237,7 @@ def config_legs(args, eng, drv):
     # config 2: SubBytes of one ciphertext (32768 bytes = 2048 blocks), reference op order
     if "2" not in legs:
         return config3_leg(args, eng, drv, out) if "3" in legs else out
-    ctx = SimpleNamespace(engine=eng, relinearization_key=rlk)
+    ctx = SimpleNamespace(engine=eng, relinearization_key=rlk, conjugation_key=cjk)
     sb = SBoxService(ctx)
     x = np.random.default_rng(1).integers(0, 256, eng.slot_count)
     ct = eng.encrypt(zeta_encode(x, modulus=256), pk)
@@ -439,6 +440,8 @@ def main():
 
     log(f"rank {rank}/{world}: engine N=2^{args.log_n} L={args.max_level} K={args.special_primes}")
     eng, R = setup_engine(args, device, rank)
+    if eng._lib.backend != "hip-gfx950":
+        raise RuntimeError(f"bench needs the HIP engine, got backend {eng._lib.backend!r}")
     log("keys ready")
     if torch.cuda.is_available():
         torch.cuda.set_device(device)
@@ -547,6 +550,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
+            "backend": eng._lib.backend,
             "data": "synthetic random AES states + random round key, encrypted",
             "config": {
                 "workload": ("one full AES-128 middle round (ShiftRows+SubBytes+MixColumns+"

@@ -17,6 +17,9 @@
  *   aesfhe_encode/_decode       engine.encode(vec) (host codec)     xor_service.py:65-66,
  *                                                                    sbox/sbox_service.py:85-88
  *   aesfhe_encrypt/_decrypt     engine.encrypt(data, pk) / decrypt  engine_context.py:81-85
+ *   aesfhe_encode_device, ...   utils.zeta_encode + encrypt and     utils.py:40-59,
+ *     _decode/_encrypt/_decrypt decrypt + zeta_decode on device      engine_context.py:81-85
+ *                               buffers (the client path)
  *   aesfhe_add / _sub / _add_pt engine.add(a, b)                    xor_service.py:75-76
  *   aesfhe_mul                  engine.multiply(ct, ct, rlk)        xor_service.py:68-71
  *   aesfhe_mul_pt               engine.multiply(ct, pt)             xor_service.py:73,285
@@ -109,9 +112,10 @@ int aesfhe_engine_profile_read(aesfhe_engine *eng, const char *family, int64_t *
                                double *total_ms, double *bytes);
 /* device bytes currently held by the engine (keys + pool); 0 in the oracle */
 int64_t aesfhe_engine_device_bytes(const aesfhe_engine *eng);
-/* device pool counters: out[0] bytes held, [1] bytes live, [2] hipMalloc calls, [3] trims
- * (cache releases after a failed hipMalloc), [4] reuses of a larger cached block; zeros in the
- * oracle */
+/* device arena counters (out holds 7 values): out[0] bytes held, [1] bytes live, [2] hipMalloc
+ * calls, [3] trims, [4] blocks split off a larger free block, [5] peak bytes live since the engine
+ * was created, [6] fragmentation = bytes of chunks that hold a live block minus the live bytes
+ * (held but neither in use nor returnable by a trim); zeros in the oracle */
 int aesfhe_engine_pool_stats(const aesfhe_engine *eng, int64_t *out);
 /* release every cached (not live) device block (synchronises the engine's stream): between
  * workload phases whose buffer sizes differ, so the next phase does not evict in its timed path */
@@ -174,6 +178,26 @@ int aesfhe_encrypt(aesfhe_engine *eng, const aesfhe_key *key, const int64_t *coe
  * ciphertext: modulo q_0), saturated to +-(2^63 - 1). */
 int aesfhe_decrypt(aesfhe_engine *eng, const aesfhe_key *sk, const aesfhe_ct *ct,
                    int64_t *coeffs_out);
+/* ---- device-resident client path ----------------------------------
+ * The codec and the encryption on buffers in the engine's device memory (the oracle: host
+ * memory), stream-ordered on the engine's stream, for a client path with no host round trip
+ * (reference: utils.zeta_encode/zeta_decode, utils.py:40-59, + EngineContext.encrypt/decrypt,
+ * engine_context.py:81-85).  Results are bit-identical to aesfhe_encode / aesfhe_decode /
+ * aesfhe_encrypt / aesfhe_decrypt on the same values. */
+/* B slot vectors (re, im: row stride `stride` doubles, n_slots <= N/2 values each, zero padded;
+ * im may be NULL) -> B x N int64 coefficients at `scale`.  Synchronises (overflow check). */
+int aesfhe_encode_device(aesfhe_engine *eng, const double *re, const double *im, int32_t batch,
+                         int64_t n_slots, int64_t stride, double scale, int64_t *coeffs_out);
+/* B x N int64 coefficients -> B x N/2 slots (re_out, im_out: B x N/2 doubles each) */
+int aesfhe_decode_device(aesfhe_engine *eng, const int64_t *coeffs, int32_t batch, double scale,
+                         double *re_out, double *im_out);
+/* aesfhe_encrypt with the coefficients in device memory (no host copy, no synchronisation) */
+int aesfhe_encrypt_device(aesfhe_engine *eng, const aesfhe_key *key, const int64_t *coeffs,
+                          int32_t batch, int32_t level, uint64_t nonce, aesfhe_ct **out);
+/* aesfhe_decrypt into device memory (batch x N centred int64 coefficients; no synchronisation) */
+int aesfhe_decrypt_device(aesfhe_engine *eng, const aesfhe_key *sk, const aesfhe_ct *ct,
+                          int64_t *coeffs_out);
+
 /* info[0]=batch info[1]=npoly info[2]=level info[3]=is_zero */
 int aesfhe_ct_info(const aesfhe_ct *ct, int32_t info[4]);
 /* NTT-domain residues, layout [batch][poly][limb 0..level][N] */

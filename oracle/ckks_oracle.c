@@ -190,17 +190,19 @@ static void chacha20_block(const uint32_t k[8], u64 label, u64 ctr, uint32_t out
     }
     for (int i = 0; i < 16; i++) out[i] = w[i] + x[i];
 }
+/* one cached block per thread, keyed by the key's words (not its address: a freed engine's key
+ * storage can be reused by a new engine with another key) */
 static __thread struct {
-    const uint32_t* k;
+    uint32_t k[8];
     u64 label, ctr;
     int valid;
     uint32_t w[16];
 } cc_cache;
 static u64 rnd(const uint32_t k[8], u64 label, u64 idx) {
     const u64 ctr = idx >> 3;
-    if (!cc_cache.valid || cc_cache.k != k || cc_cache.label != label || cc_cache.ctr != ctr) {
+    if (!cc_cache.valid || cc_cache.label != label || cc_cache.ctr != ctr || memcmp(cc_cache.k, k, sizeof cc_cache.k)) {
         chacha20_block(k, label, ctr, cc_cache.w);
-        cc_cache.k = k;
+        memcpy(cc_cache.k, k, sizeof cc_cache.k);
         cc_cache.label = label;
         cc_cache.ctr = ctr;
         cc_cache.valid = 1;
@@ -558,7 +560,7 @@ int aesfhe_engine_pool_trim(aesfhe_engine *e) { return e ? 0 : fail(AESFHE_EARG,
 int aesfhe_engine_pool_stats(const aesfhe_engine *e, int64_t *out) {
     (void)e;
     if (!out) return AESFHE_EARG;
-    for (int i = 0; i < 5; i++) out[i] = 0;
+    for (int i = 0; i < 7; i++) out[i] = 0;
     return 0;
 }
 
@@ -703,6 +705,28 @@ int aesfhe_decode(int32_t logN, const int64_t *co, double scale, double *re, dou
     }
     fft_special(&c, re, im);
     codec_free(&c);
+    return 0;
+}
+
+/* The client-path entry points (include/aesfhe.h "device-resident client path"): the oracle's
+ * "device" is host memory, so they are the host codec / encryption over B rows. */
+int aesfhe_encode_device(aesfhe_engine *e, const double *re, const double *im, int32_t B, int64_t n_slots,
+                         int64_t stride, double scale, int64_t *co) {
+    if (B < 1 || n_slots < 0 || stride < n_slots || !co) return fail(AESFHE_EARG, "bad encode shape");
+    for (int b = 0; b < B; b++) {
+        int rc = aesfhe_encode(e->logN, re ? re + (size_t)b * stride : NULL, im ? im + (size_t)b * stride : NULL,
+                               n_slots, scale, co + (size_t)b * e->N);
+        if (rc) return rc;
+    }
+    return 0;
+}
+int aesfhe_decode_device(aesfhe_engine *e, const int64_t *co, int32_t B, double scale, double *re, double *im) {
+    if (B < 1 || !co || !re || !im) return fail(AESFHE_EARG, "bad decode arguments");
+    const size_t n = (size_t)e->N / 2;
+    for (int b = 0; b < B; b++) {
+        int rc = aesfhe_decode(e->logN, co + (size_t)b * e->N, scale, re + b * n, im + b * n);
+        if (rc) return rc;
+    }
     return 0;
 }
 
@@ -1057,6 +1081,16 @@ int aesfhe_decrypt(aesfhe_engine *e, const aesfhe_key *sk, const aesfhe_ct *c, i
     free(t0);
     free(t1);
     return 0;
+}
+
+int aesfhe_encrypt_device(aesfhe_engine *e, const aesfhe_key *key, const int64_t *co, int32_t B,
+                          int32_t level, uint64_t nonce, aesfhe_ct **out) {
+    if (!co) return fail(AESFHE_EARG, "null coefficient buffer");
+    return aesfhe_encrypt(e, key, co, B, level, nonce, out);
+}
+int aesfhe_decrypt_device(aesfhe_engine *e, const aesfhe_key *sk, const aesfhe_ct *c, int64_t *out) {
+    if (!out) return fail(AESFHE_EARG, "null coefficient buffer");
+    return aesfhe_decrypt(e, sk, c, out);
 }
 
 int aesfhe_ct_export(aesfhe_engine *e, const aesfhe_ct *c, uint64_t *out) {

@@ -37,8 +37,10 @@ def oracle_lib():
 
 @pytest.fixture(scope="session")
 def product_lib():
-    from aes_xor_fhe._abi import load_product
-    return load_product()
+    from aes_xor_fhe._abi import PRODUCT_BACKEND, load_product
+    lib = load_product()
+    assert lib.backend == PRODUCT_BACKEND, lib.backend
+    return lib
 
 
 @pytest.fixture(scope="session")

@@ -95,3 +95,17 @@ def test_product_path_fails_loudly_without_extension(monkeypatch, tmp_path):
     monkeypatch.setenv("AESFHE_LIB", str(tmp_path / "missing.so"))
     with pytest.raises(RuntimeError, match="HIP extension not found"):
         abi.load_product()
+
+
+def test_load_product_refuses_another_backend():
+    """AESFHE_LIB may select another build of the product, never another backend: pointing it at
+    the CPU oracle must fail loudly instead of letting the GPU tests / bench run the checker."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ORACLE_SO, PKG, _build_oracle
+    _build_oracle()
+    env = dict(os.environ, AESFHE_LIB=str(ORACLE_SO), PYTHONPATH=str(PKG))
+    r = subprocess.run([sys.executable, "-c", "from aes_xor_fhe._abi import load_product; load_product()"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0 and "not the product" in r.stderr, r.stderr[-2000:]

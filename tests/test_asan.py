@@ -39,3 +39,14 @@ def test_oracle_chacha_kat(tmp_path):
                     str(ROOT / "tests" / "native" / "oracle_chacha_kat.c"), "-lm"], check=True)
     r = subprocess.run([str(exe)], env=ENV, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "oracle chacha ok" in r.stdout, (r.returncode, r.stderr[-2000:])
+
+
+def test_device_arena_asan(tmp_path):
+    """The engine's device arena (aes-fhe_amd/csrc/arena.h: best fit, neighbour merge, zero-copy
+    split, trim, peak_live / fragmentation counters) over malloc under ASan + UBSan, against a
+    shadow model (tests/native/arena_asan.cpp)."""
+    exe = tmp_path / "arena_asan"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                    "-o", str(exe), str(ROOT / "tests" / "native" / "arena_asan.cpp")], check=True)
+    r = subprocess.run([str(exe)], env=ENV, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "arena_asan ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])

@@ -99,6 +99,44 @@ def _worker_rows(rank, world, port, so, result_q):
         dist.destroy_process_group()
 
 
+def _worker_keys(rank, world, port, so, result_q):
+    """shared_seed is one 256-bit value on every rank; engines built from it pass the key check;
+    engines with their own seeds make scatter raise on every rank; an all-empty gather is None."""
+    sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        from aes_xor_fhe._abi import Lib
+        from aes_xor_fhe.fhe import Engine
+        from aes_xor_fhe.parallel import gather_ciphertext, scatter_ciphertext, shared_seed
+        lib = Lib(so)
+        s = shared_seed()
+        seeds = [torch.zeros(5, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(seeds, torch.tensor([(s >> (63 * i)) & ((1 << 63) - 1) for i in range(5)]))
+        same = all(torch.equal(seeds[0], t) for t in seeds) and s >= 1 << 64
+        kw = dict(log_n=10, max_level=3, special_primes=2)
+        e = Engine(_lib=lib, seed=s, **kw)
+        sk = e.create_secret_key(1)
+        ct = e.encrypt(np.ones((2, 8)), sk) if rank == 0 else None
+        got = scatter_ciphertext(e, ct)
+        ok = same and got is not None and got.batch == 1
+        ok = ok and gather_ciphertext(e, None) is None
+        bad = Engine(_lib=lib, seed=1000 + rank, **kw)
+        try:
+            scatter_ciphertext(bad, bad.encrypt(np.ones((2, 8)), bad.create_secret_key(1)) if rank == 0 else None)
+            ok = False
+        except RuntimeError as ex:
+            ok = ok and "different keys" in str(ex)
+        oks = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(oks, torch.tensor([int(ok)]))
+        if rank == 0:
+            result_q.put(all(int(t) == 1 for t in oks))
+    finally:
+        dist.destroy_process_group()
+
+
 def _spawn(target, so, world=2, timeout=900):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -117,6 +155,11 @@ def test_shard_range():
     from aes_xor_fhe.parallel import shard_range
     parts = [shard_range(10, 4, r) for r in range(4)]
     assert parts == [(0, 3), (3, 6), (6, 8), (8, 10)]
+
+
+def test_two_rank_shared_seed_and_key_check(oracle_lib):
+    from conftest import ORACLE_SO
+    assert _spawn(_worker_keys, str(ORACLE_SO)) is True
 
 
 def test_two_rank_scatter_round_gather(oracle_lib):

@@ -1,0 +1,90 @@
+"""Deferred linear combinations in the facade (fhe._LinearCiphertext, Engine(fuse_linear=True)):
+`multiply(ct, constant)` and the adds that consume it are materialised as one fused lincomb.
+
+Checked on the CPU oracle: the same levels / is_zero flags / batch errors as the eager
+evaluation (fuse_linear=False), decoded values equal to it, residues equal to an explicit
+Engine.lincomb of the same terms, and the reference-order S-box LUT (sbox/sbox_service.py:116-138)
+decoding to FIPS-197 with the reference's op trace either way."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from aes_xor_fhe import aes_tables as T
+from aes_xor_fhe.fhe import Engine, _LinearCiphertext
+
+from _tracing import make_wrap
+
+KW = dict(log_n=10, max_level=8, special_primes=3, seed=5)
+TRACES = json.loads((Path(__file__).resolve().parent / "golden" / "traces.json").read_text())
+
+
+def _engines(oracle_lib):
+    out = []
+    for fuse in (True, False):
+        e = Engine(_lib=oracle_lib, fuse_linear=fuse, **KW)
+        sk = e.create_secret_key(3)
+        out.append((e, sk, e.create_public_key(sk)))
+    return out
+
+
+def test_levels_flags_and_values_match_eager(oracle_lib):
+    (f, skf, pkf), (g, skg, pkg) = _engines(oracle_lib)
+    rng = np.random.default_rng(0)
+    z = rng.uniform(-1, 1, (2, f.slot_count)) + 1j * rng.uniform(-1, 1, (2, f.slot_count))
+    res = []
+    for e, pk in ((f, pkf), (g, pkg)):
+        a = e.encrypt(z, pk, level=7)
+        b = e.encrypt(z[:1], pk, level=5)  # broadcast operand, lower level
+        t0 = e.multiply(a, 0.0)
+        t1 = e.add(t0, e.multiply(a, 0.5 - 0.25j))
+        t2 = e.add(t1, e.multiply(b, 2.0))           # term one level lower (5 -> 4)
+        t3 = e.add(e.encode(np.full(e.slot_count, 0.125 + 1j)), t2)  # constant plaintext
+        t4 = e.add(t3, b)                             # a ciphertext addend at level 5
+        t5 = e.add(t4, 0.75)
+        res.append([t0, t1, t2, t3, t4, t5])
+    for lf, le in zip(*res):
+        assert (lf.level, lf.batch, lf.npoly, lf.is_zero) == (le.level, le.batch, le.npoly, le.is_zero)
+    assert isinstance(res[0][5], _LinearCiphertext) and not isinstance(res[1][5], _LinearCiphertext)
+    want = 0.5 * z - 0.25j * z + 2.0 * z[:1] + (0.125 + 1j) + z[:1] + 0.75
+    for e, sk, r in ((f, skf, res[0][5]), (g, skg, res[1][5])):
+        np.testing.assert_allclose(e.decrypt(r, sk), want, atol=1e-4)
+    assert res[0][0].is_zero and res[0][0].level == 6
+    np.testing.assert_allclose(f.decrypt(res[0][0], skf), 0, atol=1e-6)
+
+
+def test_materialised_residues_equal_lincomb(oracle_lib):
+    (f, skf, pkf), _ = _engines(oracle_lib)
+    rng = np.random.default_rng(1)
+    cts = [f.encrypt(rng.uniform(-1, 1, f.slot_count), pkf, level=lv) for lv in (7, 6, 6, 4)]
+    co = [0.5, -1.25j, 3.0 + 0.5j, 0.0625]
+    acc = f.multiply(cts[0], co[0])
+    for c, k in zip(cts[1:], co[1:]):
+        acc = f.add(acc, f.multiply(c, k))
+    assert isinstance(acc, _LinearCiphertext) and acc.level == 3
+    np.testing.assert_array_equal(f.export_residues(acc), f.export_residues(f.lincomb(cts, co)))
+
+
+def test_batch_mismatch_raises_like_eager(oracle_lib):
+    (f, _, pkf), (g, _, pkg) = _engines(oracle_lib)
+    for e, pk in ((f, pkf), (g, pkg)):
+        a = e.encrypt(np.ones((2, 4)), pk)
+        b = e.encrypt(np.ones((3, 4)), pk)
+        with pytest.raises(RuntimeError, match="batch mismatch"):
+            e.add(e.multiply(a, 2.0), e.multiply(b, 2.0))
+
+
+@pytest.mark.parametrize("fuse", [True, False], ids=["deferred", "eager"])
+def test_sbox_reference_order_either_way(oracle_lib, fuse):
+    from aes_xor_fhe.sbox.sbox_service import SBoxService
+    from aes_xor_fhe.utils import zeta_decode, zeta_encode
+    w = make_wrap(oracle_lib, tracing=True, fuse_linear=fuse)
+    sb = SBoxService(w.ctx)
+    x = np.random.default_rng(2).integers(0, 256, w.engine.slot_count)
+    enc = w.engine.encrypt(zeta_encode(x, modulus=256), w.public_key)
+    w.engine.trace.clear()
+    out = sb.sub_bytes_array(enc)
+    trace = dict(w.engine.trace)
+    assert trace == TRACES["sub_bytes_array"]
+    assert np.array_equal(zeta_decode(w.engine.decrypt(out, w.secret_key), modulus=256), T.SBOX[x])
