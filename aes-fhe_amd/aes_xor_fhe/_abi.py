@@ -54,6 +54,7 @@ SIGNATURES = [
     ("aesfhe_engine_profile", C.c_int, [c_eng_p, C.c_int32]),
     ("aesfhe_engine_profile_read", C.c_int,
      [c_eng_p, C.c_char_p, _P(C.c_int64), _P(C.c_double), _P(C.c_double)]),
+    ("aesfhe_engine_profile_kernels", C.c_int, [c_eng_p, C.c_char_p, C.c_int64, _P(C.c_int64)]),
     ("aesfhe_engine_device_bytes", C.c_int64, [c_eng_p]),
     ("aesfhe_engine_pool_stats", C.c_int, [c_eng_p, C.POINTER(C.c_int64)]),
     ("aesfhe_engine_pool_trim", C.c_int, [c_eng_p]),

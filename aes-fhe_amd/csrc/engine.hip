@@ -112,6 +112,12 @@ struct ProfRec {
     int fam;
     hipEvent_t a, b;
     double bytes;
+    const char* label;  // kernel class (static string) or nullptr
+};
+
+struct KernStat {  // per kernel class (aesfhe_engine_profile_kernels)
+    int64_t n = 0;
+    double ms = 0, bytes = 0;
 };
 
 struct aesfhe_engine {
@@ -160,6 +166,7 @@ struct aesfhe_engine {
     double prof_ms[4] = {0, 0, 0, 0};
     double prof_bytes[4] = {0, 0, 0, 0};
     int64_t prof_n[4] = {0, 0, 0, 0};
+    std::map<std::string, KernStat> prof_k;
 
     Tabs tabs() const {
         Tabs t;
@@ -217,8 +224,9 @@ struct ProfScope {
     hipEvent_t a = nullptr, b = nullptr;
     hipStream_t s;
     bool on;
-    ProfScope(aesfhe_engine* e_, int f, double by, hipStream_t s_ = nullptr)
-        : e(e_), fam(f), bytes(by), s(s_ ? s_ : e_->stream), on((e_->prof >> f) & 1) {
+    const char* label;
+    ProfScope(aesfhe_engine* e_, int f, double by, const char* lab = nullptr, hipStream_t s_ = nullptr)
+        : e(e_), fam(f), bytes(by), s(s_ ? s_ : e_->stream), on((e_->prof >> f) & 1), label(lab) {
         if (!on) return;
         a = take();
         b = take();
@@ -237,7 +245,7 @@ struct ProfScope {
     ~ProfScope() {
         if (!on) return;
         hipEventRecord(b, s);
-        e->recs.push_back({fam, a, b, bytes});
+        e->recs.push_back({fam, a, b, bytes, label});
     }
 };
 
@@ -250,6 +258,12 @@ static void prof_flush(aesfhe_engine* e) {
         e->prof_ms[r.fam] += ms;
         e->prof_bytes[r.fam] += r.bytes;
         e->prof_n[r.fam] += 1;
+        if (r.label) {
+            KernStat& k = e->prof_k[r.label];
+            k.n++;
+            k.ms += ms;
+            k.bytes += r.bytes;
+        }
         e->spare.push_back(r.a);
         e->spare.push_back(r.b);
     }
@@ -376,11 +390,11 @@ static void ntt_fwd_t(aesfhe_engine* e, Span src, Span dst, int total) {
     Tabs T = e->tabs();
     const double by = 8.0 * e->N * (double)total;
     {
-        ProfScope ps(e, FAM_NTT, by);
+        ProfScope ps(e, FAM_NTT, by, "ntt_generic");
         hipLaunchKernelGGL(k_ntt_fwd_cols<R1>, dim3(kC2 / CW, total), dim3(256), 0, e->stream, src, dst, T);
     }
     {
-        ProfScope ps(e, FAM_NTT, by);
+        ProfScope ps(e, FAM_NTT, by, "ntt_generic");
         hipLaunchKernelGGL(k_ntt_fwd_rows<R1>, dim3(R1 / RW, total), dim3(256), 0, e->stream, dst, T);
     }
 }
@@ -391,11 +405,11 @@ static void ntt_inv_t(aesfhe_engine* e, Span src, Span dst, int total) {
     Tabs T = e->tabs();
     const double by = 8.0 * e->N * (double)total;
     {
-        ProfScope ps(e, FAM_NTT, by);
+        ProfScope ps(e, FAM_NTT, by, "ntt_generic");
         hipLaunchKernelGGL(k_ntt_inv_rows<R1>, dim3(R1 / RW, total), dim3(256), 0, e->stream, src, dst, T);
     }
     {
-        ProfScope ps(e, FAM_NTT, by);
+        ProfScope ps(e, FAM_NTT, by, "ntt_generic");
         hipLaunchKernelGGL(k_ntt_inv_cols<R1>, dim3(kC2 / CW, total), dim3(256), 0, e->stream, dst, T);
     }
 }
@@ -409,11 +423,11 @@ static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse
     // write-once 16 B per coefficient (the two-pass split itself is charged as overhead)
     const double by = 8.0 * e->N * (double)total;
     {
-        ProfScope ps(e, FAM_NTT, by);
+        ProfScope ps(e, FAM_NTT, by, inverse ? "ntt_inv_rows" : "ntt_fwd_cols");
         if (!inverse) hipLaunchKernelGGL(k_nttf_fwd_cols<R>, dim3(16, total), dim3(256), 0, e->stream, src, dst, T);
         else hipLaunchKernelGGL((k_nttf_inv_rows<R, false>), dim3(R / 16, total), dim3(256), 0, e->stream, src, dst, T, Span{}, (const u64*)nullptr);
     }
-    ProfScope ps(e, FAM_NTT, by);
+    ProfScope ps(e, FAM_NTT, by, inverse ? "ntt_inv_cols" : "ntt_fwd_rows");
     if (!inverse) hipLaunchKernelGGL((k_nttf_fwd_rows_t<false, R>), dim3(R / 16, total), dim3(256), 0, e->stream, dst, T, RowFin{});
     else hipLaunchKernelGGL(k_nttf_inv_cols<R>, dim3(16, total), dim3(256), 0, e->stream, dst, T);
 }
@@ -428,7 +442,7 @@ static void intt_prod(aesfhe_engine* e, Span a, Span b, Span dst, int total, con
     Tabs T = e->tabs();
     const double by = 8.0 * e->N * (double)total;
     {
-        ProfScope ps(e, FAM_NTT, 2.0 * by);  // two operands read
+        ProfScope ps(e, FAM_NTT, 2.0 * by, "ntt_inv_rows_prod");  // two operands read
         if (e->logN == 16) {
             if (fac) hipLaunchKernelGGL((k_nttf_inv_rows<256, true, true>), dim3(16, total), dim3(256), 0, e->stream, a, dst, T, b, fac);
             else hipLaunchKernelGGL((k_nttf_inv_rows<256, true, false>), dim3(16, total), dim3(256), 0, e->stream, a, dst, T, b, fac);
@@ -437,7 +451,7 @@ static void intt_prod(aesfhe_engine* e, Span a, Span b, Span dst, int total, con
             else hipLaunchKernelGGL((k_nttf_inv_rows<512, true, false>), dim3(32, total), dim3(256), 0, e->stream, a, dst, T, b, fac);
         }
     }
-    ProfScope ps(e, FAM_NTT, by);
+    ProfScope ps(e, FAM_NTT, by, "ntt_inv_cols");
     if (e->logN == 16) hipLaunchKernelGGL(k_nttf_inv_cols<256>, dim3(16, total), dim3(256), 0, e->stream, dst, T);
     else hipLaunchKernelGGL(k_nttf_inv_cols<512>, dim3(16, total), dim3(256), 0, e->stream, dst, T);
     HIPC(hipGetLastError());
@@ -805,6 +819,7 @@ extern "C" int aesfhe_engine_profile(aesfhe_engine* e, int32_t en) {
     e->prof = en == -1 ? 7 : (en & 7);
     if (e->prof) {
         for (int i = 0; i < 4; i++) e->prof_ms[i] = e->prof_bytes[i] = 0, e->prof_n[i] = 0;
+        e->prof_k.clear();
         // pre-create events so that none is created inside a measured region
         while (e->spare.size() < 65536) {
             hipEvent_t x;
@@ -827,6 +842,25 @@ extern "C" int aesfhe_engine_profile_read(aesfhe_engine* e, const char* fam, int
         *n = e->prof_n[f];
         *ms = e->prof_ms[f];
         if (bytes) *bytes = e->prof_bytes[f];
+    }
+    API_END
+}
+extern "C" int aesfhe_engine_profile_kernels(aesfhe_engine* e, char* buf, int64_t cap, int64_t* need) {
+    API_BEGIN
+    prof_flush(e);
+    std::string js = "{";
+    char tmp[256];
+    for (auto& kv : e->prof_k) {
+        snprintf(tmp, sizeof tmp, "%s\"%s\": [%lld, %.6f, %.1f]", js.size() > 1 ? ", " : "", kv.first.c_str(),
+                 (long long)kv.second.n, kv.second.ms, kv.second.bytes);
+        js += tmp;
+    }
+    js += "}";
+    if (need) *need = (int64_t)js.size() + 1;
+    if (buf && cap > 0) {
+        const size_t m = std::min((size_t)cap - 1, js.size());
+        memcpy(buf, js.data(), m);
+        buf[m] = 0;
     }
     API_END
 }
@@ -1485,7 +1519,7 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1, 
         // D = q_l, optional level-down constant): t never reaches HBM in NTT form
         const int total = P * l;
         {
-            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols_spread");
             const SpreadSrc ss{(const u64*)x.p, (long)N, e->chain.q[l], ctop, ctopf};
             auto kern = N == 65536 ? (sc ? k_nttf_fwd_cols_spread<256, 2> : k_nttf_fwd_cols_spread<256, 1>)
                                    : (sc ? k_nttf_fwd_cols_spread<512, 2> : k_nttf_fwd_cols_spread<512, 1>);
@@ -1493,7 +1527,7 @@ static aesfhe_ct* rescale_view(aesfhe_engine* e, const View& in, int64_t C = 1, 
         }
         RowFin f{(const u64*)in.d, in.bs, in.ps, Opnd2{nullptr, 0, 0, 0}, o->d, 2L * l * N, (long)l * N,
                  e->rs_invf + (size_t)l * e->Lp1, l, sc ? (const double*)dff_c : nullptr};
-        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total * 3.0);  // half an NTT + input read + output write
+        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total * 3.0, "ntt_fwd_rows_fin");  // half an NTT + input read + output write
         if (N == 65536) hipLaunchKernelGGL((k_nttf_fwd_rows_t<true, 256>), dim3(16, total), dim3(256), 0, e->stream, st, e->tabs(), f);
         else hipLaunchKernelGGL((k_nttf_fwd_rows_t<true, 512>), dim3(32, total), dim3(256), 0, e->stream, st, e->tabs(), f);
         HIPC(hipGetLastError());
@@ -1561,7 +1595,7 @@ static void mul_const_into(aesfhe_engine* e, const View& in, int64_t A, int64_t 
     const_factors(e, A, Bc, nl, f, ff);
     u64* df = upload_small(e, f.data(), f.size());
     double* dff = upload_small(e, ff.data(), ff.size());
-    ProfScope ps(e, FAM_EW, 0);
+    ProfScope ps(e, FAM_EW, 8.0 * e->N * nl * (double)o->B * in.np * (acc ? 3 : 2), "mul_const");
     hipLaunchKernelGGL(k_mul_const, ew_grid(e, nl, o->B * in.np), dim3(256), 0, e->stream, opnd(in, o->B), out_of(o), in.np, (const u64*)df, (const double*)dff, e->q, acc, e->logN);
     HIPC(hipGetLastError());
 }
@@ -1649,7 +1683,7 @@ static int addsub(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* b, int 
     align_to(e, b, l, Bv);
     int B = std::max(a->B, b->B), np = std::max(a->np, b->np);
     aesfhe_ct* r = ct_new(e, B, np, l);
-    ProfScope ps(e, FAM_EW, 0);
+    ProfScope ps(e, FAM_EW, 24.0 * e->N * (l + 1) * (double)B * np, "add");
     hipLaunchKernelGGL(k_addsub, ew_grid(e, l + 1, B * np), dim3(256), 0, e->stream, opnd(A.v, B), opnd(Bv.v, B), out_of(r), np, e->q, sub, e->logN);
     HIPC(hipGetLastError());
     r->is_zero = a->is_zero && b->is_zero;
@@ -1805,7 +1839,7 @@ extern "C" int aesfhe_dot_pt(aesfhe_engine* e, const aesfhe_ct* const* cts, cons
         auto dpp = upload_small(e, pp.data(), pp.size());
         auto dsb = upload_small(e, sb.data(), sb.size());
         {
-            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (pc.size() + 1));
+            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (pc.size() + 1), "dot_pt");
             hipLaunchKernelGGL(k_dot_pt, ew_grid(e, nl, B * np), dim3(256), 0, e->stream, (const u64* const*)dpc, (const long*)dsb, (long)nl * e->N, (const u64* const*)dpp, (int)pc.size(), out_of(acc), np, e->q, e->qinv, e->logN);
         }
         HIPC(hipGetLastError());
@@ -1883,7 +1917,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
             const SpreadSrc ss{(const u64*)dc.p + (long)lo * N, lN, 0, 0, 0.0};
             auto kern = N == 65536 ? k_nttf_fwd_cols_spread<256, 3> : k_nttf_fwd_cols_spread<512, 3>;
             auto cols = [&](Span sp, int total) {
-                ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+                ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols_spread");
                 hipLaunchKernelGGL(kern, dim3(16, total), dim3(256), 0, e->stream, ss, sp, e->tabs());
             };
             if (lo > 0) cols(span_s(exj, neN, lo, lo, 0, e->Lp1), B * lo);
@@ -1893,7 +1927,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         }
         // 2. ModUp base conversion of digit j to every other limb, then NTT those limbs
         {
-            ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne);
+            ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne, "modup");
             if (alpha < 1 || alpha > 16) throw_err(AESFHE_EUNSUPPORTED, "ModUp digit width outside 1..16");
             AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, bconv_groups(N, B, ne), B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
                               (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
@@ -1902,7 +1936,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         HIPC(hipGetLastError());
         auto fwd = [&](Span sp, int total) {
             if (!cols_only) return ntt(e, sp, sp, total, false);
-            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
             ntt_fwd_cols(e, sp, total);
         };
         if (lo > 0) fwd(span_s(exj, neN, lo, lo, 0, e->Lp1), B * lo);
@@ -1938,14 +1972,14 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
         const int nown = std::min(l + 1, beta * K);
         const double opw = pb ? (4.0 + (pc && pc->ptr ? 2.0 : 0.0)) * (l + 1)
                               : (double)nown + (pmod && addend.ptr ? (double)addend.np * (l + 1) : 0.0);
-        ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown + opw) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))));
+        ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown + opw) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))), "ks_rows_inner");
         const int R = N / 256, blocks = 8 * B * (ne * (R / 8) / 8);
         const Opnd none{nullptr, 0, 0, 0};
         auto kern = pb ? (R == 256 ? k_nttf_rows_ks<1, 256, true> : k_nttf_rows_ks<1, 512, true>)
                        : (R == 256 ? k_nttf_rows_ks<1, 256, false> : k_nttf_rows_ks<1, 512, false>);
         hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum, pb ? *pb : none, fac, pc ? *pc : none);
     } else {
-        ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B * (accum ? 2 : 1)));
+        ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B * (accum ? 2 : 1)), "ks_inner");
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
         hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, addend, pm, e->logN, (int)accum);
     }
@@ -1974,7 +2008,7 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
     const double* dinvf = r ? e->mdr_dinvf + cell * e->Lp1 : e->md_pinvf;
     Tmp conv(e, (size_t)B * 2 * kN);
     {
-        ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1));
+        ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1), "moddown");
         if (K + r < 1 || K + r > 16) throw_err(AESFHE_EUNSUPPORTED, "ModDown source width outside 1..16");
         AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, bconv_groups(N, B * 2, lk + 1), B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN,
                            invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv,
@@ -1987,20 +2021,20 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
         Tabs T = e->tabs();
         const int total = B * 2 * (lk + 1);
         {
-            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total);
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
             ntt_fwd_cols(e, sc, total);
         }
         RowFin f{(const u64*)acc, 2 * neN, neN, Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}, o->d,
                  2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf, lk + 1};
         // the row pass (credited half an NTT) plus the finish: acc read, output written (+ addend)
-        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total * (3.0 + (fin_add.ptr ? 1.0 : 0.0)));
+        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total * (3.0 + (fin_add.ptr ? 1.0 : 0.0)), "ntt_fwd_rows_fin");
         if (N == 65536) hipLaunchKernelGGL((k_nttf_fwd_rows_t<true, 256>), dim3(16, total), dim3(256), 0, e->stream, sc, T, f);
         else hipLaunchKernelGGL((k_nttf_fwd_rows_t<true, 512>), dim3(32, total), dim3(256), 0, e->stream, sc, T, f);
         HIPC(hipGetLastError());
         return;
     }
     ntt(e, sc, sc, B * 2 * (lk + 1), false);
-    ProfScope psf(e, FAM_KS, 8.0 * N * (double)B * 2 * (lk + 1) * 4);
+    ProfScope psf(e, FAM_KS, 8.0 * N * (double)B * 2 * (lk + 1) * 4, "moddown_finish");
     hipLaunchKernelGGL(k_moddown_finish, dim3(N / 256, lk + 1, B * 2), dim3(256), 0, e->stream, (const u64*)acc, 2 * neN, neN, (const u64*)conv.p, 2 * kN, kN, fin_add, out_of(o), e->q, dinv, dinvf, e->logN);
     HIPC(hipGetLastError());
 }
@@ -2078,7 +2112,7 @@ static aesfhe_ct* relin_rescale(aesfhe_engine* e, const aesfhe_ct* c, const aesf
 static aesfhe_ct* tensor_ct(aesfhe_engine* e, const View& a, const View& b, int B) {
     const int l = a.level;
     aesfhe_ct* t = ct_new(e, B, 3, l);
-    ProfScope ps(e, FAM_EW, 0);
+    ProfScope ps(e, FAM_EW, 56.0 * e->N * (l + 1) * (double)B, "tensor");
     hipLaunchKernelGGL(k_tensor, ew_grid(e, l + 1, B), dim3(256), 0, e->stream, opnd(a, B), opnd(b, B), out_of(t), e->q, e->qinv, 0, e->logN);
     HIPC(hipGetLastError());
     return t;
@@ -2193,7 +2227,7 @@ extern "C" int aesfhe_mul_fma(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe
     }
     aesfhe_ct* t = ct_new(e, B, 3, l);
     {
-        ProfScope ps(e, FAM_EW, 0);
+        ProfScope ps(e, FAM_EW, 72.0 * e->N * (l + 1) * (double)B, "tensor_fma");
         hipLaunchKernelGGL(k_tensor_fma, ew_grid(e, l + 1, B), dim3(256), 0, e->stream, prod ? opnd(A.v, B) : none, prod ? opnd(Bv.v, B) : none,
                            hasc ? opnd(trunc_view(c, l), B) : none, out_of(t), (const u64*)dfac, e->q, e->qinv, e->logN);
     }
@@ -2333,7 +2367,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             const int beta = ks_beta(e, l);
             auto dk = upload_small(e, kd.data(), kd.size());
             auto dko = upload_small(e, ko.data(), ko.size());
-            ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + kd.size() * (2.0 * beta + 2.0 * B)));
+            ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + kd.size() * (2.0 * beta + 2.0 * B)), "ks_inner_multi");
             auto inner = beta <= 4 ? k_ks_inner_multi<4, 4> : beta <= 8 ? k_ks_inner_multi<8, 2> : k_ks_inner_multi<12, 1>;
             hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, c1, cv.bs, (const u64*)ext->p, neN, (long)B * neN, (const u64* const*)dk, (int)kd.size(), 2L * e->np * N, (long)e->np * N, (u64* const*)dko, 2 * neN, neN, B, beta, e->K, l, e->q, e->qinv, e->Lp1, c0, (const double*)e->pmodf, e->logN);
             HIPC(hipGetLastError());
@@ -2373,7 +2407,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             auto dpt = upload_small(e, pt.data(), pt.size());
             auto dso = upload_small(e, so.data(), so.size());
             {
-                ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (nb + gn) + terms));
+                ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (nb + gn) + terms), "dot_pt_ext_multi");
                 // two (b, c) polynomials per workgroup (four measured the same: 153.7 vs 153.3 ms per
                 // B = 16 bit bootstrap, 162.7 with one)
                 hipLaunchKernelGGL((k_dot_pt_ext_multi<kGM, 2>), dim3((ne * (N / 256) + 7) / 8 * 8 * B), dim3(256), 0, e->stream, (const u64* const*)dep, (const u64*)dgal, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, e->q, e->qinv, e->Lp1, e->logN, B * 2);
@@ -2599,7 +2633,7 @@ extern "C" int aesfhe_lincomb(aesfhe_engine* e, const aesfhe_ct* const* cts, int
         auto df = upload_small(e, f.data(), f.size());
         auto dff = upload_small(e, ff.data(), ff.size());
         {
-            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (m + 1));
+            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (m + 1), "lincomb");
             hipLaunchKernelGGL(k_lincomb, ew_grid(e, nl, B * np), dim3(256), 0, e->stream, (const u64* const*)dp, (const long*)db, (const int*)dn, m, (const long*)dps, (const u64*)df, (const double*)dff, out_of(acc), np, nl, e->q, e->qinv, e->logN);
         }
         HIPC(hipGetLastError());
@@ -2683,7 +2717,7 @@ extern "C" int aesfhe_lincomb_many(aesfhe_engine* e, const aesfhe_ct* const* cts
         auto dF = upload_small(e, F.data(), F.size());
         auto dFF = upload_small(e, FF.data(), FF.size());
         {
-            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (nc + ml));
+            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * np * (nc + ml), "lincomb_many");
             hipLaunchKernelGGL(k_lincomb_many, ew_grid(e, nl, B * np), dim3(256), 0, e->stream, (const u64* const*)dp, (const long*)db, (const int*)dn, nc, (const long*)dps, (const u64*)dF, (const double*)dFF, ml, acc.p, orow, obs, np, nl, e->q, e->qinv, e->logN);
         }
         HIPC(hipGetLastError());
@@ -2735,7 +2769,7 @@ extern "C" int aesfhe_dot(aesfhe_engine* e, const aesfhe_ct* const* a, const aes
         auto dsa = upload_small(e, sa.data(), sa.size());
         auto dsb = upload_small(e, sb.data(), sb.size());
         {
-            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * (4.0 * m + 3));
+            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * (4.0 * m + 3), "dot");
             hipLaunchKernelGGL(k_dot, ew_grid(e, nl, B), dim3(256), 0, e->stream, (const u64* const*)dpa, (const long*)dsa, (const u64* const*)dpb, (const long*)dsb, m, (long)nl * e->N, out_of(acc), e->q, e->qinv, e->logN);
         }
         HIPC(hipGetLastError());
@@ -2858,7 +2892,7 @@ extern "C" int aesfhe_poly2(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_
         const long obs = 3L * nl * N;
         aesfhe_ct* d3 = ct_new(e, Bt, 3, l);
         {
-            ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml));
+            ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml), "poly2");
             for (int t0 = 0; t0 < ml; t0 += kPoly2Out)
                 hipLaunchKernelGGL(k_poly2, ew_grid(e, nl, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny, tab, ml, t0, std::min(kPoly2Out, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, e->logN);
         }
@@ -3010,7 +3044,7 @@ extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, in
         const long obs = 3L * nl * N;
         aesfhe_ct* d3 = ct_new(e, ml * B, 3, l);
         {
-            ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml));
+            ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml), "poly2_int");
             constexpr int mo = 4;  // outputs per launch (8: 219 VGPRs, 2 waves, measured slower)
             for (int t0 = 0; t0 < ml; t0 += mo)
                 for (int la = 0; la < nl;) {  // runs of limbs of one kernel class

@@ -53,10 +53,12 @@ PEAK_HBM_GBS = 8000.0
 METRIC = "AES-128 blocks/sec (homomorphic full round) at N=2^16, L=30; 1/2/4/8 MI355X"
 SEED = 0x5EED5EED  # the CPU baseline's engine (reproducible); the GPU ranks share a 256-bit seed
 
-PMC_FILE = ROOT / "profiles" / "r02" / "pmc" / "ntt_traffic.json"
-PMC_NOTE = ("HBM bytes per NTT launch = algorithmic bytes x the HBM/algorithmic ratio measured by "
-            "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 calibration) + WRITE_SIZE on the same NTT kernels "
-            "at the same parameters (profiles/r02/pmc/ntt_traffic.json)")
+PEAK_FP64_TFLOPS = 78.6  # MI355X vector FP64 (AMD spec: 256 CUs x 128 FLOP/clk x 2.4 GHz)
+PMC_FILE = ROOT / "profiles" / "r03" / "pmc" / "round_traffic.json"
+PMC_NOTE = ("HBM bytes per NTT-family launch measured with rocprofv3 --pmc FETCH_SIZE (x2, the gfx950 "
+            "correction of MI355X_MICROARCH.md) and --pmc WRITE_SIZE, separate passes, over exactly one "
+            "bench round step (tools/pmc_traffic.py -> profiles/r03/pmc/round_traffic.json, stamped "
+            "with the git HEAD it measured)")
 
 
 _T0 = time.perf_counter()
@@ -67,13 +69,45 @@ def log(msg):
     print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
-def traffic_per_launch(alg_bytes):
-    """HBM bytes per NTT launch from the committed PMC measurement (None if absent)."""
+def pmc_record():
+    """The committed PMC measurement of one round step (None if absent)."""
     try:
-        ratio = json.loads(PMC_FILE.read_text())["traffic_over_alg"]
-    except (OSError, ValueError, KeyError):
+        return json.loads(PMC_FILE.read_text())
+    except (OSError, ValueError):
         return None
-    return round(alg_bytes * ratio)
+
+
+def kernel_table(eng, pmc, steps):
+    """Per kernel class of the profiled steps (aesfhe_engine_profile_kernels, HIP events on the
+    engine stream): launches, average duration, algorithmic GB/s and its fraction of the HBM
+    peak; with the PMC record, the measured HBM bytes per launch (-> GB/s, fraction) and, where
+    counted, the fp64 FLOP rate against the FP64 vector peak."""
+    import ctypes as C
+    need = C.c_int64()
+    eng._check(eng._lib.engine_profile_kernels(eng._h, None, 0, C.byref(need)))
+    buf = C.create_string_buffer(need.value)
+    eng._check(eng._lib.engine_profile_kernels(eng._h, buf, need.value, C.byref(need)))
+    raw = json.loads(buf.value.decode())
+    total = sum(ms for _, ms, _ in raw.values()) or 1.0
+    pk = (pmc or {}).get("per_kernel", {})
+    out = {}
+    for k, (n, ms, by) in sorted(raw.items(), key=lambda kv: -kv[1][1]):
+        avg_s = ms * 1e-3 / n
+        rec = {"launches_per_step": round(n / steps, 1), "avg_us": round(avg_s * 1e6, 2),
+               "share_of_kernel_time": round(ms / total, 4)}
+        if by > 0:
+            gbs = by / n / avg_s / 1e9
+            rec.update(alg_bytes_per_launch=round(by / n), alg_gbs=round(gbs, 1), frac=round(gbs / PEAK_HBM_GBS, 4))
+        p = pk.get(k)
+        if p:
+            hbm = p["hbm_bytes_per_launch"]
+            rec.update(hbm_bytes_per_launch=round(hbm), hbm_gbs=round(hbm / avg_s / 1e9, 1),
+                       hbm_frac=round(hbm / avg_s / 1e9 / PEAK_HBM_GBS, 4))
+            if p.get("f64_flops_per_launch"):
+                tf = p["f64_flops_per_launch"] / avg_s / 1e12
+                rec.update(f64_tflops=round(tf, 2), fp64_frac=round(tf / PEAK_FP64_TFLOPS, 4))
+        out[k] = rec
+    return out
 
 
 def parse():
@@ -103,6 +137,13 @@ def parse():
                     help="bit-ciphertext pairs per bootstrap call (0: 32 / aes10-batch)")
     ap.add_argument("--aes10-batch", type=int, default=16,
                     help="ciphertext sets for the full 10-round AES-128 measurement (0: skip)")
+    ap.add_argument("--client-batch", type=int, default=8,
+                    help="ciphertext sets of the device client-path leg (0: skip)")
+    ap.add_argument("--pmc-marks", action="store_true",
+                    help="bracket the timed steps with marker kernels (tools/pmc_traffic.py selects "
+                         "the PMC records between them)")
+    ap.add_argument("--no-harness", action="store_true",
+                    help="skip the reference-harness leg (full_round on 32768 bytes, xor_cipher)")
     return ap.parse_args()
 
 
@@ -214,11 +255,23 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
             "timed_mallocs": timed_mallocs}
 
 
+def _materialize(out):
+    """Touch every ciphertext handle of a result (a deferred linear combination is evaluated on
+    first use, fhe._LinearCiphertext), so the timed region contains all of its work."""
+    from aes_xor_fhe.fhe import Ciphertext
+    if isinstance(out, Ciphertext):
+        out._h
+    elif isinstance(out, (list, tuple)):
+        for o in out:
+            _materialize(o)
+
+
 def _timed(eng, fn, reps=1):
     eng.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
         out = fn()
+        _materialize(out)
     eng.synchronize()
     return out, (time.perf_counter() - t0) / reps
 
@@ -281,6 +334,99 @@ def config3_leg(args, eng, drv, out):
     return out
 
 
+def reference_harness_leg(args, lib=None, threads=0):
+    """The reference's own timing harness (new.py:231-262, test_all_process.py:21-48):
+    AESFHERound.full_round -- AddRoundKey in the nibble domain: split, Zeta-16 encode, encrypt
+    four ciphertexts, two XORService.xor_cipher calls, decrypt, recombine -- on 32768 random bytes
+    (state and key from default_rng(1), as new.py:246-250), through EngineWrapper(XORConfig()):
+    the signature-1 engine, N = 2^16, L = 30 (K = 8, scale 44).  Plus one xor_cipher of two
+    32768-slot nibble ciphertexts (BASELINE.md section 2 models it at 5.2 ms per ciphertext at
+    8 TB/s).  GPU (lib None): timed after a warm-up call; CPU oracle (lib given): one timed call.
+    Both verified (state ^ key; the decrypted XOR)."""
+    from aes_xor_fhe.new import AESFHERound
+    from aes_xor_fhe.parallel import shared_seed
+    from aes_xor_fhe.xor_service import EngineWrapper, XORConfig, XORService, ZetaEncoder
+    kw = dict(seed=SEED if lib is not None else shared_seed())
+    if lib is not None:
+        kw["_lib"] = lib
+    w = EngineWrapper(XORConfig(thread_count=threads, engine_kwargs=kw))
+    eng = w.engine
+    svc = XORService(w)
+    ark = AESFHERound(w, svc)
+    rng = np.random.default_rng(1)
+    state = rng.integers(0, 256, 32768, dtype=np.uint8)
+    key = rng.integers(0, 256, 32768, dtype=np.uint8)
+    if lib is None:  # GPU: warm-up call (plaintext caches, pool)
+        ark.full_round(state, key)
+    # each xor_cipher call inside full_round timed on its own (materialised + synchronised)
+    xor_times, xor_levels = [], []
+    inner = svc.xor_cipher
+
+    def timed_xor(ea, eb):
+        eng.synchronize()
+        t = time.perf_counter()
+        out = inner(ea, eb)
+        _materialize(out)
+        eng.synchronize()
+        xor_times.append(time.perf_counter() - t)
+        xor_levels.append((ea.level, out.level))
+        return out
+    svc.xor_cipher = timed_xor
+    t0 = time.perf_counter()
+    res = ark.full_round(state, key)
+    t_round = time.perf_counter() - t0
+    svc.xor_cipher = inner
+    ok_round = bool(np.array_equal(res, state ^ key))
+    t_xor = sum(xor_times) / len(xor_times)
+    return {"full_round_32768_bytes": {"ms": round(t_round * 1e3, 2), "value": round(2048 / t_round, 1),
+                                       "unit": "blocks/s (32768 bytes = 2048 AES blocks, AddRoundKey)",
+                                       "verified": ok_round},
+            "xor_cipher": {"ms": round(t_xor * 1e3, 2), "calls": len(xor_times), "verified": ok_round,
+                           "note": "mean of the two xor_cipher calls inside full_round (hi and lo nibbles), "
+                                   "verified through full_round's output",
+                           "level_in": xor_levels[0][0], "level_out": xor_levels[0][1]},
+            "engine": {"log_n": eng.log_coeff_count, "max_level": eng.max_level,
+                       "special_primes": eng.special_prime_count, "threads": threads or None}}
+
+
+def client_path_leg(args, eng, drv, key):
+    """End-to-end client path on the device (reference utils.py:40-59 +
+    engine_context.py:81-85): host bytes -> H2D -> on-GPU packing / +-1 bit slicing / encode /
+    encrypt -> one AES round -> on-GPU decrypt / decode / unpack -> D2H, verified against
+    FIPS-197; blocks/s over the whole path, with the phases."""
+    import torch
+    from aes_xor_fhe import aes_tables as T
+    R = drv.R
+    nb = args.client_batch
+    rk = np.random.default_rng(25073102).integers(0, 256, 16, dtype=np.uint8)
+    blocks = np.random.default_rng(4242).integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
+    dev = eng.client_device
+
+    def run():
+        t0 = time.perf_counter()
+        st = R.encrypt_blocks_device(torch.from_numpy(blocks).to(dev))
+        eng.synchronize()
+        t1 = time.perf_counter()
+        out = R.round(st, key)
+        _materialize([c for row in out for c in row])
+        eng.synchronize()
+        t2 = time.perf_counter()
+        got = R.decrypt_blocks_device(out).cpu().numpy()
+        t3 = time.perf_counter()
+        return got, (t0, t1, t2, t3)
+
+    run()  # warm-up (codec tables, pool)
+    got, (t0, t1, t2, t3) = run()
+    ok = bool(np.array_equal(got, T.aes_round(blocks, rk))) if args.check else None
+    return {"value": round(nb * R.n_blk / (t3 - t0), 1), "unit": "blocks/s", "sets": nb,
+            "blocks": nb * R.n_blk, "ms": round((t3 - t0) * 1e3, 1),
+            "in_ms": round((t1 - t0) * 1e3, 1), "round_ms": round((t2 - t1) * 1e3, 1),
+            "out_ms": round((t3 - t2) * 1e3, 1), "verified": ok,
+            "path": "bytes H2D -> pack/bit-slice (torch on device) -> aesfhe_encode_device -> "
+                    "aesfhe_encrypt_device -> round -> aesfhe_decrypt_device -> aesfhe_decode_device "
+                    "-> unpack -> D2H"}
+
+
 def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
     """One set per rank encrypted on rank 0, scattered to the ranks (device tensors, RCCL),
     one round per rank, gathered and verified on rank 0.  Times: scatter and gather of the
@@ -335,10 +481,22 @@ def _cpu_model():
     return None
 
 
+def host_cores():
+    """CPUs this process may use: the affinity set, capped by OMP_NUM_THREADS when the
+    environment sets it (the GPU box's CPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
+
+
 def cpu_baseline(args):
     """The oracle (CPU restatement of the same engine) timing one full middle round of one set
-    at the GPU workload's parameters -- measured, not extrapolated; OMP over limbs with this
-    process's OMP_NUM_THREADS (16 on the GPU box)."""
+    at the GPU workload's parameters -- measured, not extrapolated -- at every host core and at 8
+    threads, plus the reference's own harness (full_round on 32768 bytes, one xor_cipher) at
+    every host core."""
     import subprocess
     so = ROOT / "oracle" / "_build" / "liboracle_ckks.so"
     if not so.exists():
@@ -347,7 +505,12 @@ def cpu_baseline(args):
     from aes_xor_fhe._abi import Lib
     from aes_xor_fhe.fhe import Engine
     lib = Lib(so)
-    threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
+    # every host core this process may use (the oracle's OpenMP loops run
+    # over limbs and batch elements, the count passed explicitly as the engine's thread count),
+    # and 8 threads: the reference's desilofhe default (xor_service.py:25-26).  The GPU box
+    # grants a share of its CPUs (OMP_NUM_THREADS, 16 per GPU) while os.cpu_count() reports the
+    # whole machine (256): more threads than the share only oversubscribe it.
+    threads = host_cores()
 
     def round_time(nthr):
         eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes,
@@ -369,14 +532,18 @@ def cpu_baseline(args):
     n_blk, t, ok = round_time(threads)
     rec = {"value": round(n_blk / t, 2), "unit": "blocks/s", "cores": threads, "kind": "port",
            "measured": True, "verified": ok, "os_cpu_count": os.cpu_count(), "cpu_model": _cpu_model(),
+           "cores_note": "all CPUs this process may use (affinity set capped by OMP_NUM_THREADS, the box's share)",
            "sample": (f"oracle (oracle/ckks_oracle.c, gcc -O2, OpenMP over limbs, {threads} threads) "
                       f"timing one full middle AES-128 round ({args.layout} layout) of one set = "
                       f"{n_blk} blocks at N=2^{args.log_n}, L={args.max_level}, K={args.special_primes}: "
                       f"{t:.1f} s, FIPS-verified")}
+    log("cpu baseline: oracle round at 8 threads (the reference's thread_count default)")
+    _, t8, ok8 = round_time(8)
+    rec["threads_8"] = {"value": round(n_blk / t8, 2), "s": round(t8, 1), "verified": ok8, "cores": 8}
+    if not args.no_harness and args.log_n == 16:
+        log(f"cpu baseline: reference harness (full_round, xor_cipher) on the oracle at {threads} threads")
+        rec["reference_harness"] = reference_harness_leg(args, lib=lib, threads=threads)
     if args.cpu_extended:
-        log("cpu baseline: oracle round at 8 threads (the reference's thread_count default)")
-        _, t8, ok8 = round_time(8)
-        rec["threads_8"] = {"value": round(n_blk / t8, 2), "s": round(t8, 1), "verified": ok8}
         log("cpu baseline: configs 2 and 3 on the oracle")
         rec["configs"] = cpu_config_legs(args, lib, threads)
     return rec
@@ -478,12 +645,20 @@ def main():
         log("warm-up step")
 
     import ctypes as C
+
+    def mark():  # a torch fill kernel: the PMC tool's step delimiter
+        if args.pmc_marks and torch.cuda.is_available():
+            torch.cuda.synchronize()
+            torch.full((1,), 7.0, device=torch.device("cuda", device))
+            torch.cuda.synchronize()
     barrier()
+    mark()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = step()
     barrier()
     elapsed = allmax(time.perf_counter() - t0)
+    mark()
     log(f"timed: {args.steps} steps, {elapsed / args.steps * 1e3:.1f} ms/step")
     round_pool = eng.pool_stats()
     ok = None
@@ -496,8 +671,9 @@ def main():
     n_ntt, ms_ntt, by_ntt = C.c_int64(), C.c_double(), C.c_double()
     n_ks, ms_ks, by_ks = C.c_int64(), C.c_double(), C.c_double()
     prof_ms = 0.0
+    kernels = None
     if args.profile_steps > 0:
-        eng._check(eng._lib.engine_profile(eng._h, 1 | 2))
+        eng._check(eng._lib.engine_profile(eng._h, -1))
         eng.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.profile_steps):
@@ -506,6 +682,7 @@ def main():
         prof_ms = (time.perf_counter() - t0) * 1e3 / args.profile_steps
         eng._check(eng._lib.engine_profile_read(eng._h, b"ntt", C.byref(n_ntt), C.byref(ms_ntt), C.byref(by_ntt)))
         eng._check(eng._lib.engine_profile_read(eng._h, b"keyswitch", C.byref(n_ks), C.byref(ms_ks), C.byref(by_ks)))
+        kernels = kernel_table(eng, pmc_record(), args.profile_steps)
         eng._check(eng._lib.engine_profile(eng._h, 0))
 
     # the round's buffers and cached blocks (other sizes) would otherwise crowd the device in
@@ -527,6 +704,16 @@ def main():
         configs = config_legs(args, eng, R)
         gc.collect()
         eng.pool_trim()
+        if not args.no_harness:
+            configs["reference_harness"] = reference_harness_leg(args)
+            gc.collect()
+            log("reference harness leg done")
+    client = None
+    if world == 1 and args.client_batch > 0 and args.layout == "rows":
+        client = client_path_leg(args, eng, R, key)
+        gc.collect()
+        eng.pool_trim()
+        log("client path leg done")
     aes10 = None
     log("config legs done" if configs else "no config legs")
     if args.aes10_batch > 0 and args.layout == "rows":
@@ -538,6 +725,12 @@ def main():
         steps_prof = max(args.profile_steps, 1)
         avg_launch_ms = ms_ntt.value / max(n_ntt.value, 1)
         achieved = by_ntt.value / (ms_ntt.value * 1e-3) / 1e9 if ms_ntt.value else 0.0
+        alg_per_launch = by_ntt.value / max(n_ntt.value, 1)
+        pmc = pmc_record()
+        fam = (pmc or {}).get("ntt_family") or {}
+        same_shape = bool(fam) and pmc.get("workload") == {"log_n": args.log_n, "max_level": args.max_level,
+                                                           "special_primes": args.special_primes,
+                                                           "batch": args.batch, "layout": args.layout}
         rec = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -569,8 +762,10 @@ def main():
                 "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "frac_per_pass_rw": round(2 * achieved / PEAK_HBM_GBS, 4),  # each pass's own read+write
-                "traffic": traffic_per_launch(by_ntt.value / max(n_ntt.value, 1)),
-                "traffic_source": PMC_NOTE,
+                "traffic": round(fam["hbm_bytes_per_launch"]) if same_shape else None,
+                "traffic_over_alg": round(fam["hbm_bytes_per_launch"] / alg_per_launch, 3) if same_shape and alg_per_launch else None,
+                "traffic_source": PMC_NOTE if same_shape else "no PMC record of this workload",
+                "traffic_head": (pmc or {}).get("head") if same_shape else None,
                 "measured_over": f"{args.profile_steps} profiled round steps after the timed region",
                 "launches": n_ntt.value, "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "alg_bytes_per_launch": round(by_ntt.value / max(n_ntt.value, 1)),
@@ -578,10 +773,12 @@ def main():
                 "keyswitch_kernels_gbs": round(by_ks.value / (ms_ks.value * 1e-3) / 1e9, 1) if ms_ks.value else None,
                 "keyswitch_share_of_step": round(ms_ks.value / steps_prof / max(prof_ms, 1e-9), 3),
                 "profiled_ms_per_step": round(prof_ms, 1),
+                "kernels": kernels,
             },
             "cpu_baseline": None,
             "aes128_10_rounds": aes10,
             "configs": configs,
+            "client_path": client,
             "scatter_gather": sg,
         }
         if not args.no_cpu_baseline and world == 1:

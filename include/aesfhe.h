@@ -110,6 +110,12 @@ int aesfhe_engine_sync(aesfhe_engine *eng);
 int aesfhe_engine_profile(aesfhe_engine *eng, int32_t enable);
 int aesfhe_engine_profile_read(aesfhe_engine *eng, const char *family, int64_t *launches,
                                double *total_ms, double *bytes);
+/* Per kernel class of the recorded families since profiling was enabled, as JSON text
+ * {"class": [launches, total_ms, algorithmic_bytes], ...} (classes: ntt_fwd_cols, ntt_fwd_rows,
+ * ntt_fwd_rows_fin, ntt_fwd_cols_spread, ntt_inv_rows, ntt_inv_rows_prod, ntt_inv_cols, modup,
+ * ks_rows_inner, moddown, poly2_int, lincomb, ...).  Writes at most cap bytes (NUL-terminated)
+ * into buf (may be NULL) and the size needed into *need.  "{}" in the oracle. */
+int aesfhe_engine_profile_kernels(aesfhe_engine *eng, char *buf, int64_t cap, int64_t *need);
 /* device bytes currently held by the engine (keys + pool); 0 in the oracle */
 int64_t aesfhe_engine_device_bytes(const aesfhe_engine *eng);
 /* device arena counters (out holds 7 values): out[0] bytes held, [1] bytes live, [2] hipMalloc
