@@ -209,12 +209,43 @@ def main():
     out, traces["shift_rows"] = counts(lambda: sr.shift_rows(ct))
     g["shiftrows_in"] = state
     g["shiftrows_out"] = np.real(ew.decrypt(out))[:16]
+    # InvShiftRows (shiftrows_service.py:53-69) on the same state
+    out, traces["inverse_shift_rows"] = counts(lambda: sr.inverse_shift_rows(ct))
+    g["inv_shiftrows_out"] = np.real(ew.decrypt(out))[:16]
 
     # MixRow merged ShiftRows+MixColumns (shift_mix_zeta.py:14-69): op trace only
     mr = smz.MixRow(svc, ew)
     st4 = np.arange(16).reshape(4, 4) % 16
     out, traces["mixrow_merged_shift_mix"] = counts(lambda: mr.merged_shift_mix_fhe(st4))
     g["mixrow_abs_max"] = np.array([np.abs(ew.decrypt(out)).max()])
+
+    # MixRow inverse (shift_mix_zeta.py:71-122): op trace and the values its final decrypt
+    # decodes.  Its last line reshapes the whole slot vector into 4 x 4 (shift_mix_zeta.py:121)
+    # and raises for any slot count above 16; the trace holds every engine call before that, the
+    # 16 decoded values are taken from that final decrypt.
+    from aes_xor_fhe.utils import zeta_decode as zd16
+    inv_in = np.arange(16, dtype=np.float64) % 16
+    ct_inv = ew.encrypt(zeta_encode(inv_in))
+    last = {}
+    orig_decrypt = Engine.decrypt
+
+    def spy(self, ct, key):
+        v = orig_decrypt(self, ct, key)
+        last["v"] = v
+        return v
+    Engine.decrypt = spy
+    Engine.trace = []
+    try:
+        mr.merged_inv_mixshift_fhe_from_ct(ct_inv)
+        raised = ""
+    except ValueError as ex:
+        raised = str(ex)
+    finally:
+        Engine.decrypt = orig_decrypt
+    traces["mixrow_merged_inv_mixshift"] = dict(Counter(Engine.trace))
+    g["mixrow_inv_in"] = inv_in
+    g["mixrow_inv_out"] = np.round(zd16(last["v"])).astype(np.int64)[:16].reshape(4, 4)
+    g["mixrow_inv_reference_raises"] = np.array([bool(raised)])
 
     # GF(2^8) x2 / x3 (gf_service.py:55-78).  The coefficient files it loads are absent from the
     # reference tree; they are produced by the reference's own generator

@@ -151,3 +151,39 @@ def test_transformer_with_bootstrap(twrap):           # mixcolumns_service.py:21
     out = AESFHETransformer(w, svc, gf).merged_shift_mix(np.arange(16, dtype=np.uint8))
     _same_trace(w.engine.trace, TRACES["transformer_merged_shift_mix"])
     assert out.npoly == 2 and 0 <= out.level <= 30
+    assert bool(np.all(np.isfinite(w.decrypt(out)))) == bool(GOLD["transformer_out_finite"][0])
+
+
+def test_mixrow_inverse_with_bootstrap(twrap):         # shift_mix_zeta.py:71-122
+    """The inverse merged shift-mix on the GPU with the real Engine.bootstrap: the reference's op
+    trace (bootstraps >= the golden's, as above) and the exact-arithmetic result (all zero,
+    golden) within the general-mode bootstrap's error before decoding."""
+    from aes_xor_fhe.shift_mix_zeta import MixRow
+    from aes_xor_fhe.utils import zeta_encode
+    w = twrap
+    svc = XORService(w)
+    svc.coeff_cache.get_plaintext_coeffs(w)
+    ct = w.encrypt(zeta_encode(GOLD["mixrow_inv_in"], modulus=16))
+    seen = []
+    dec = w.decrypt
+    w.decrypt = lambda c: seen.append(dec(c)) or seen[-1]
+    try:
+        w.engine.trace.clear()
+        out = MixRow(svc, w).merged_inv_mixshift_fhe_from_ct(ct)
+    finally:
+        del w.decrypt
+    _same_trace(w.engine.trace, TRACES["mixrow_merged_inv_mixshift"])
+    assert out.shape == (4, 4)
+    err = np.abs(seen[-1]).max()
+    print("MixRow inverse max |slot| (exact: 0):", err)
+    assert err < 0.05 and not GOLD["mixrow_inv_out"].any()
+
+
+def test_inverse_shift_rows_gpu(wrap):                # shiftrows_service.py:53-69
+    from aes_xor_fhe.shiftrows_service import AESFHEShiftRows
+    sr = AESFHEShiftRows(wrap)
+    n = wrap.engine.slot_count
+    state = np.resize(np.arange(16), n).astype(np.float64) + 16 * (np.arange(n) // 16)
+    exp = T.inv_shift_rows(state.reshape(-1, 16).astype(np.int64)).ravel()
+    out = np.real(wrap.decrypt(sr.inverse_shift_rows(wrap.encrypt(state)))).round().astype(int)
+    assert np.array_equal(out, exp)

@@ -201,6 +201,67 @@ def test_mixrow_trace_matches_reference(oracle_lib):
     assert got == TRACES["mixrow_merged_shift_mix"]
 
 
+def test_inverse_shift_rows_trace_and_reference_agreement(oracle_lib):
+    """InvShiftRows (shiftrows_service.py:53-69), repaired: the reference masks each row once
+    and rotates it (4 products, 3 rotations: golden trace), which is wrong for the slots whose
+    row shift wraps around the 4-slot row; the restatement masks the wrapping part apart (7
+    products, 6 rotations).  The reference's output (golden) equals the repaired inverse on
+    the slots that do not wrap."""
+    from aes_xor_fhe.shiftrows_service import AESFHEShiftRows
+    w = make_wrap(oracle_lib, L=6, tracing=True)
+    sr = AESFHEShiftRows(w)
+    ct = w.encrypt(np.arange(16, dtype=np.float64))
+    w.engine.trace.clear()
+    out = sr.inverse_shift_rows(ct)
+    assert TRACES["inverse_shift_rows"] == {"mul_ct_pt": 4, "rotate": 3, "add_ct_ct": 3}
+    assert {k: v for k, v in w.engine.trace.items() if v} == {"mul_ct_pt": 7, "rotate": 6, "add_ct_ct": 6}
+    got = np.real(w.decrypt(out))[:16].round().astype(int)
+    exp = T.inv_shift_rows(np.arange(16, dtype=np.int64)[None])[0]
+    assert np.array_equal(got, exp)
+    ref = GOLD["inv_shiftrows_out"].round().astype(int)
+    pos = np.arange(16)
+    nowrap = (pos // 4 - pos % 4) >= 0   # row r (= pos // 4 in the reference's 4-slot rows)
+    agree = ref == exp
+    assert agree[nowrap].all() and not agree.all()
+
+
+def test_mixrow_inverse_trace_matches_reference(oracle_lib):
+    """MixRow.merged_inv_mixshift_fhe_from_ct (shift_mix_zeta.py:71-122) with a client-aided
+    refresh (test only): the reference's op trace (golden, every call before the reference's
+    final 4 x 4 reshape, which raises on a full slot vector) and its decoded values (exact
+    arithmetic: all zero) -- here the slots before decoding stay within noise of 0."""
+    from aes_xor_fhe.shift_mix_zeta import MixRow
+    w = make_wrap(oracle_lib, L=30, K=8, tracing=True)
+    e = w.engine
+
+    def refresh(ct):
+        e.trace["bootstrap"] += 1
+        v = e.decrypt(ct, w.secret_key)
+        e.trace["decrypt"] -= 1
+        e.trace["encrypt"] -= 1
+        return e.encrypt(v, w.public_key)
+    w.bootstrap = refresh
+    svc = XORService(w)
+    svc.coeff_cache.get_plaintext_coeffs(w)
+    mr = MixRow(svc, w)
+    ct = w.encrypt(zeta_encode_16(GOLD["mixrow_inv_in"]))
+    seen = []
+    dec = w.decrypt
+    w.decrypt = lambda c: seen.append(dec(c)) or seen[-1]
+    e.trace.clear()
+    out = mr.merged_inv_mixshift_fhe_from_ct(ct)
+    got = {k: v for k, v in e.trace.items() if v}
+    assert got == TRACES["mixrow_merged_inv_mixshift"]
+    assert out.shape == GOLD["mixrow_inv_out"].shape == (4, 4)
+    assert np.abs(seen[-1]).max() < 0.05 and not GOLD["mixrow_inv_out"].any()
+    assert bool(GOLD["mixrow_inv_reference_raises"][0])
+
+
+def zeta_encode_16(v):
+    from aes_xor_fhe.utils import zeta_encode
+    return zeta_encode(np.asarray(v), modulus=16)
+
+
 def test_gf_coefficients_match_reference_generator():
     """coeffs_gen's GF x2 / x3 LUT coefficients against the vectors the reference's own
     generator writes (generator/generate_gf2_gf3_coeffs.py:47-70, run by make_golden.py)."""
