@@ -255,6 +255,7 @@ class AESRowRound:
                 if progress:
                     progress(f"refresh {refreshes} before round {rnd}")
                 if timings is not None:
+                    self.e.materialize(S)
                     self.e.synchronize()
                     timings["bootstrap"] = timings.get("bootstrap", 0.0) + time.perf_counter() - t0
             t0 = time.perf_counter()
@@ -264,6 +265,7 @@ class AESRowRound:
             if progress:
                 progress(f"round {rnd} from level {lvl}")
             if timings is not None:
+                self.e.materialize(S)  # deferred products belong to this round's time
                 self.e.synchronize()
                 dt = time.perf_counter() - t0
                 timings["rounds"] = timings.get("rounds", 0.0) + dt
@@ -274,18 +276,19 @@ class AESRowRound:
         """SubBytes -> ShiftRows -> MixColumns -> AddRoundKey on the row-sliced +-1 bit state."""
         import time
 
-        def mark(name, t0):
+        def mark(name, t0, obj=None):
             if timings is None:
                 return t0
+            self.e.materialize(obj)  # deferred products belong to this stage
             self.e.synchronize()
             t1 = time.perf_counter()
             timings[name] = timings.get(name, 0.0) + (t1 - t0)
             return t1
         t = mark("start", 0.0) if timings is not None else 0.0
         A = self.sub_bytes(bits)  # SubBytes first: ShiftRows commutes with it and is cheaper
-        t = mark("sub_bytes", t)  # on the SubBytes output (level l-4: fewer limbs per rotation)
+        t = mark("sub_bytes", t, A)  # on the SubBytes output (level l-4: fewer limbs per rotation)
         A = self.shift_rows(A)
-        t = mark("shift_rows", t)
+        t = mark("shift_rows", t, A)
         out = self.mix_columns_add_round_key(A, key)
-        mark("mix_columns_add_round_key", t)
+        mark("mix_columns_add_round_key", t, out)
         return out

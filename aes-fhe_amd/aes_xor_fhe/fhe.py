@@ -187,6 +187,43 @@ class Ciphertext(_Handle):
         return f"Ciphertext(level={self.level}, batch={self.batch}, npoly={self.npoly})"
 
 
+class _ProductCiphertext(Ciphertext):
+    """A deferred relinearised product a * b (``Engine.multiply(a, b, rlk)``): level, batch and
+    is_zero are the eager result's; the first use of the handle evaluates it as the eager
+    ``aesfhe_mul`` would (same residues).  Only `multiply(product, constant)` looks inside:
+    such terms, summed by ``add`` (``_LinearCiphertext``), are materialised together as ONE
+    fused bivariate evaluation (``aesfhe_poly2``: one relinearisation and two rescales for all
+    of them), the reference's per-coefficient loop of xor_service.py:271-286 in one launch
+    sequence."""
+
+    __slots__ = ("_a", "_b", "_rlk", "_mat")
+
+    def __init__(self, engine: "Engine", a: Ciphertext, b: Ciphertext, rlk):
+        self._lib, self._free = engine._lib, None
+        self.engine = engine
+        self._a, self._b, self._rlk, self._mat = a, b, rlk, None
+        self.level, self.batch, self.npoly = min(a.level, b.level) - 1, max(a.batch, b.batch), 2
+        self.is_zero = a.is_zero or b.is_zero
+
+    @property
+    def _h(self):
+        if self._mat is None:
+            e = self.engine
+            self._mat = e._call_ct(e._lib.mul, self._a._h, self._b._h, self._rlk._h)
+            self._a = self._b = None  # release the operands
+        return self._mat._h
+
+    @property
+    def pending(self) -> bool:
+        return self._mat is None
+
+    def __del__(self):  # the materialised ciphertext frees itself
+        pass
+
+    def __repr__(self):
+        return f"Ciphertext(level={self.level}, batch={self.batch}, npoly=2, deferred product)"
+
+
 class _LinearCiphertext(Ciphertext):
     """A deferred linear combination: sum_i c_i * ct_i (each term one level below its input, as
     `multiply(ct, constant)` defines it) + sum of ciphertexts + a constant.
@@ -268,7 +305,9 @@ class Engine:
 
     ``fuse_linear`` (default True): ``multiply(ct, constant)`` and the ``add`` calls that consume
     its result are deferred and materialised as one fused linear combination
-    (``_LinearCiphertext``); False evaluates every call eagerly (a rescale per product).
+    (``_LinearCiphertext``), and ``multiply(a, b, rlk)`` is deferred to its first use
+    (``_ProductCiphertext``) so that products scaled by constants and summed become one fused
+    bivariate evaluation; False evaluates every call eagerly (a rescale per product).
 
     Randomness: without ``seed`` the engine seed, every secret key created without a seed and
     the first encryption nonce are drawn from os.urandom.  With an explicit ``seed`` everything
@@ -543,6 +582,10 @@ class Engine:
     def multiply(self, a, b, relinearization_key: RelinearizationKey | None = None) -> Ciphertext:
         if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
             if relinearization_key is not None:
+                if (self._fuse_linear and a.npoly == 2 and b.npoly == 2 and min(a.level, b.level) >= 1
+                        and (a.batch == b.batch or 1 in (a.batch, b.batch))
+                        and isinstance(relinearization_key, RelinearizationKey)):
+                    return _ProductCiphertext(self, a, b, relinearization_key)
                 return self._call_ct(self._lib.mul, a._h, b._h, relinearization_key._h)
             t = self._call_ct(self._lib.tensor, a._h, b._h)
             return self._call_ct(self._lib.rescale, t._h)
@@ -584,8 +627,19 @@ class Engine:
         """One aesfhe_lincomb of the terms (one rescale of the sum), then the ciphertext addends
         (level-aligned adds) and the constant, at the deferred object's level."""
         x = None
-        if L._terms:
-            x = self.lincomb([c for c, _ in L._terms], [k for _, k in L._terms])
+        plain, prods = [], {}
+        for c, k in L._terms:
+            if isinstance(c, _ProductCiphertext) and c.pending:
+                if not c.is_zero:
+                    prods.setdefault(id(c._rlk), []).append((c, k))
+            else:
+                plain.append((c, k))
+        for group in prods.values():
+            y = self._product_sum(group)
+            x = y if x is None else self._call_ct(self._lib.add, x._h, y._h)
+        if plain:
+            y = self.lincomb([c for c, _ in plain], [k for _, k in plain])
+            x = y if x is None else self._call_ct(self._lib.add, x._h, y._h)
         for c in L._addends:
             x = c if x is None else self._call_ct(self._lib.add, x._h, c._h)
         if x is None:
@@ -597,6 +651,23 @@ class Engine:
         if x.level > L.level:
             x = self.level_down(x, L.level)
         return x
+
+    def _product_sum(self, terms) -> Ciphertext:
+        """sum_t k_t a_t b_t over deferred products of one relinearisation key: one aesfhe_poly2
+        call (the distinct left operands as its x basis, the right ones as its y basis, at most
+        15 each), else the products one by one."""
+        xs, ys = {}, {}
+        for p, _ in terms:
+            xs.setdefault(id(p._a), p._a)
+            ys.setdefault(id(p._b), p._b)
+        if len(xs) > 15 or len(ys) > 15:
+            return self.lincomb([p for p, _ in terms], [k for _, k in terms])
+        xi = {k: i + 1 for i, k in enumerate(xs)}
+        yi = {k: j + 1 for j, k in enumerate(ys)}
+        C = np.zeros((1, len(xs) + 1, len(ys) + 1), dtype=np.complex128)
+        for p, k in terms:
+            C[0, xi[id(p._a)], yi[id(p._b)]] += k
+        return self.poly2(list(xs.values()), list(ys.values()), C, terms[0][0]._rlk)[0]
 
     def multiply_fma(self, a: Ciphertext, b: Ciphertext, relinearization_key: RelinearizationKey,
                      alpha: int = 1, c: Ciphertext | None = None, gamma: float = 0.0,
@@ -937,6 +1008,17 @@ class Engine:
 
     def synchronize(self):
         self._check(self._lib.engine_sync(self._h))
+
+    @staticmethod
+    def materialize(obj):
+        """Evaluate every deferred ciphertext (products, linear combinations) in a ciphertext
+        or a nested list / tuple of them now (enqueued on the engine's stream); returns obj."""
+        if isinstance(obj, Ciphertext):
+            obj._h
+        elif isinstance(obj, (list, tuple)):
+            for o in obj:
+                Engine.materialize(o)
+        return obj
 
 
 def _naf_steps(r: int, n: int) -> list:

@@ -234,6 +234,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     m0 = eng.pool_stats()["mallocs"]
     t0 = time.perf_counter()
     out, nref = R.encrypt_aes128(st, keys, bs, timings=tm, pairs_per_call=ppc, progress=log)
+    _materialize([c for row in out for c in row])
     barrier()
     el = allmax(time.perf_counter() - t0)
     timed_mallocs = eng.pool_stats()["mallocs"] - m0
@@ -256,14 +257,11 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
 
 
 def _materialize(out):
-    """Touch every ciphertext handle of a result (a deferred linear combination is evaluated on
-    first use, fhe._LinearCiphertext), so the timed region contains all of its work."""
-    from aes_xor_fhe.fhe import Ciphertext
-    if isinstance(out, Ciphertext):
-        out._h
-    elif isinstance(out, (list, tuple)):
-        for o in out:
-            _materialize(o)
+    """Evaluate every deferred ciphertext of a result (products and linear combinations are
+    evaluated on first use: fhe._ProductCiphertext / _LinearCiphertext), so the timed region
+    contains all of its work."""
+    from aes_xor_fhe.fhe import Engine
+    Engine.materialize(out)
 
 
 def _timed(eng, fn, reps=1):
@@ -449,6 +447,7 @@ def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
     t_sc = allmax(time.perf_counter() - t0)
     bytes_in = sum(c.batch * c.npoly * (c.level + 1) for c in mine) * 8 * (1 << eng.log_coeff_count)
     res = drv.cts(drv.round(drv.from_cts(mine), key))
+    _materialize(res)
     barrier()
     t0 = time.perf_counter()
     full = [gather_ciphertext(eng, c) for c in res]
@@ -524,6 +523,7 @@ def cpu_baseline(args):
         st, key = R.encrypt(blocks), R.key(rk)
         t0 = time.perf_counter()
         out = R.round(st, key)
+        _materialize(R.cts(out))
         t = time.perf_counter() - t0
         ok = bool((R.decrypt(out) == T.aes_round(blocks, rk)).all())
         return R.n_blk, t, ok
@@ -637,7 +637,9 @@ def main():
     log(f"{args.batch} sets encrypted")
 
     def step():
-        return R.round(st, key)
+        out = R.round(st, key)
+        _materialize(R.cts(out))  # deferred products / sums are part of the step
+        return out
 
     for _ in range(args.warmup):
         out = step()

@@ -30,6 +30,8 @@ def main():
     for r in range(a.reps):
         t0 = time.perf_counter()
         out = bench.config_legs(args, eng, drv)
+        if "h" in a.legs.split(","):
+            out["reference_harness"] = bench.reference_harness_leg(args)
         out["wall_s"] = round(time.perf_counter() - t0, 2)
         print(json.dumps(out), flush=True)
 
