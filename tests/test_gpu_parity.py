@@ -371,3 +371,25 @@ def test_power_basis_255_full_params_bit_exact(product_lib, oracle_lib, gpu_avai
     assert [c.level for c in res[0]] == [30 - int(np.ceil(np.log2(k))) for k in range(1, 256)]
     for p in (1, 2, 127, 128, 255):
         np.testing.assert_allclose(g.decrypt(res[0][p - 1], sks[0]), z ** p, atol=1e-3)
+
+
+def test_poly2_int_sbox_shape_bit_exact(product_lib, oracle_lib, gpu_available):
+    """aesfhe_poly2_int with the S-box's shape at N = 2^16: 15 x and 15 y basis ciphertexts
+    (ny = 16, the compile-time basis size), full and partial output blocks of 4, integer weights
+    in [-8, 8] / 64, mixed basis levels, the top limb q_0 on the folding kernel -- residue for
+    residue against the oracle."""
+    kw = dict(log_n=16, max_level=7, special_primes=3, seed=41)
+    g, o = _pair(product_lib, oracle_lib, **kw)
+    rng = np.random.default_rng(15)
+    zx = rng.uniform(-1, 1, (2, g.slot_count))
+    zy = rng.uniform(-1, 1, g.slot_count)
+    W = rng.integers(-8, 9, (10, 16, 16))
+    W[3] = 0
+    res = []
+    for eng in (g, o):
+        k = _keys(eng)
+        xb = eng.make_power_basis(eng.encrypt(zx, k["pk"], level=6), 15, k["rlk"])
+        yb = eng.make_power_basis(eng.encrypt(zy, k["pk"], level=6), 15, k["rlk"])
+        res.append(eng.poly2_int(xb, yb, W, 64, k["rlk"]))
+    for a, b in zip(*res):
+        _same(g, o, a, b)
