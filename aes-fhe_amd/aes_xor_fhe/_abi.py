@@ -120,6 +120,8 @@ SIGNATURES = [
     ("aesfhe_lincomb_many", C.c_int,
      [c_eng_p, _P(c_ct_p), C.c_int32, _P(C.c_double), _P(C.c_double), C.c_int32, _P(c_ct_p)]),
     ("aesfhe_dot", C.c_int, [c_eng_p, _P(c_ct_p), _P(c_ct_p), C.c_int32, c_key_p, _P(c_ct_p)]),
+    ("aesfhe_dot_fma", C.c_int, [c_eng_p, _P(c_ct_p), _P(c_ct_p), C.c_int32, _P(c_ct_p), _P(C.c_double),
+                                 C.c_int32, C.c_double, c_key_p, _P(c_ct_p)]),
     ("aesfhe_poly2", C.c_int,
      [c_eng_p, _P(c_ct_p), C.c_int32, _P(c_ct_p), C.c_int32, _P(C.c_double), _P(C.c_double),
       C.c_int32, c_key_p, _P(c_ct_p)]),

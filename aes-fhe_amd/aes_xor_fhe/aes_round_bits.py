@@ -26,7 +26,8 @@ Full AES-128 (`encrypt_aes128`, BASELINE configs 4-5): AddRoundKey(k0), rounds 1
 final round without MixColumns (depth 4 + 1), with bit-mode bootstrapping
 (bootstrap.Bootstrapper.bootstrap_bits: two bit ciphertexts per refresh, batched) whenever the
 next round would leave fewer levels than SlotToCoeff needs.  At L = 30: ARK0 -> 29, rounds 1-3
--> 8, then {refresh -> 17, two rounds -> 3} x 3 and {refresh, final round}: four refreshes.
+-> 8, {refresh -> 19, two rounds -> 5} x 2, refresh -> 19, rounds 8-9 and the final round -> 0:
+three refreshes (the bootstrap's output level L - 11).
 """
 from __future__ import annotations
 

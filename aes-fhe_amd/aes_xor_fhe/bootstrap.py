@@ -16,7 +16,10 @@ Pipeline for a ciphertext c at level 0 encrypting slots z (message m at the cano
 4. SlotToCoeff: (q_0 / (2 pi D_0)) B_log(n) ... B_1 applied to y_re + i y_im (the bit reversal
    cancels) returns the slots z at level L - depth.
 
-Depth = 1 + 2 * groups + ceil(log2(deg + 1)) + 1 + r (16 with the defaults at any N).
+Depth = 1 + 2 * groups + ceil(log2(deg + 1)) + 1 + r (16 with the defaults at any N).  The bit
+mode (bootstrap_bits, StC first) spends groups levels before ModRaise and, with bits_opt,
+groups + ceil(log2(deg + 1)) + r = 3 + 5 + 3 = 11 after it: c_in rides in the CtS diagonals and
+the Chebyshev sum is evaluated depth-optimally (chebyshev_opt).
 """
 from __future__ import annotations
 
@@ -105,7 +108,8 @@ def _bsgs_plan(offsets: List[int], n: int):
 class Bootstrapper:
     def __init__(self, engine: Engine, sk, rlk, cjk=None, *, hw: int = 32, K: float = 12.0,
                  r: int = 3, deg: int = 31, groups: int = 3, seed: int = 7,
-                 bits_deg: int = 31, bits_r: int = 3, lazy: bool = True, baby_scale: int = 2):
+                 bits_deg: int | None = None, bits_r: int = 3, lazy: bool = True, baby_scale: int = 2,
+                 bits_opt: bool = True):
         e = self.e = engine
         self.rlk = rlk
         self.cjk = cjk if cjk is not None else e.create_conjugation_key(sk)
@@ -113,6 +117,12 @@ class Bootstrapper:
         self.n = self.N // 2
         self.L = e.max_level
         self.r, self.deg, self.B = r, deg, K + 1.0
+        # bits_opt: the bit mode folds c_in into the CoeffToSlot diagonals and evaluates EvalMod's
+        # Chebyshev sum in depth ceil(log2(deg + 1)) (chebyshev_opt) -- two levels fewer (11
+        # instead of 13), which is what lets ten AES rounds run on three refreshes
+        self.bits_opt = bits_opt
+        if bits_deg is None:
+            bits_deg = 29 if bits_opt else 31
         self.bits_deg, self.bits_r = bits_deg, bits_r
         # lazy: linear maps through aesfhe_linear_bsgs (baby rotations kept in Q u P, one ModDown
         # per giant + one for all giant key switches); baby steps are then cheap, so the BSGS
@@ -129,8 +139,14 @@ class Bootstrapper:
         # CtS: (D_L / (2 q0 Bnd)) * prod of inverse stages; StC: (q0 / (2 pi D_0)) * forward stages
         cts = transform_groups(n, N, groups, inverse=True)
         stc = transform_groups(n, N, groups, inverse=False)
-        # c_in = D_L / (2 q0 Bnd) ~ 2^-15 folded into the diagonals would leave their plaintext
-        # integers ~25 bits.  It is applied as its own constant multiply instead (one level): the
+        # bit mode: c_in = D_L / (2 q0 Bnd) ~ 2^-15.7 spread over the CtS groups' diagonals
+        # (c_in^(1/groups) each, plaintext integers ~2^30): the rounding it adds to t / q0 is
+        # ~1e-7, and the bit mode's error enters squared
+        self.B_bits = K + 1.0
+        f_in = (D[self.L] / (2.0 * q0 * self.B_bits)) ** (1.0 / groups)
+        cts_bits = [{d: v * f_in for d, v in M.items()} for M in cts] if bits_opt else None
+        # General mode: c_in folded into one group's diagonals would leave their plaintext integers
+        # ~25 bits, and this mode's error is linear in it.  It is applied as its own constant multiply instead (one level): the
         # engine multiplies by exactly A / s (A = llround(c_in s)), and the bound is re-derived
         # from that value so that 2 pi Bnd x = 2 pi t / q0 holds exactly.
         s = e._lib.engine_mul_scale(e._h, self.L)
@@ -144,6 +160,7 @@ class Bootstrapper:
         stc_bits[-1] = {d: v * c_bits for d, v in stc_bits[-1].items()}
         self.cts, self.stc = [self._prepare(M) for M in cts], [self._prepare(M) for M in stc]
         self.stc_bits = [self._prepare(M) for M in stc_bits]
+        self.cts_bits = [self._prepare(M) for M in cts_bits] if bits_opt else self.cts
         # rotation keys: hoisted keys for the baby steps (one ModUp per group input), ordinary
         # keys for the giant steps
         babies, giants = set(), set()
@@ -159,15 +176,18 @@ class Bootstrapper:
         # for every bit of a value, so it adds coherently through the S-box's Walsh polynomial
         # and the MixColumns products: full AES-128 failed at N = 2^10 with it (random noise of
         # 2e-4 does not), hence the bits_deg / bits_r knobs default to the general fit.
-        self.cheb = self._cheb_fit(deg, r)
-        self.cheb_bits = self._cheb_fit(bits_deg, bits_r)
+        # With bits_opt the bit-mode fit is degree 29 (fit error after the double angles 3e-10).
+        self.cheb = self._cheb_fit(deg, r, self.B)
+        self.cheb_bits = self._cheb_fit(bits_deg, bits_r, self.B_bits if bits_opt else self.B)
         self.depth = 1 + 2 * groups + math.ceil(math.log2(deg + 1)) + 1 + r
-        self.bits_level = self.L - (1 + groups + math.ceil(math.log2(bits_deg + 1)) + 1 + bits_r)
+        cheb_depth = math.ceil(math.log2(bits_deg + 1)) + (0 if bits_opt else 1)
+        self.bits_level = self.L - ((0 if bits_opt else 1) + groups + cheb_depth + bits_r)
 
-    def _cheb_fit(self, deg: int, r: int) -> np.ndarray:
+    @staticmethod
+    def _cheb_fit(deg: int, r: int, bnd: float) -> np.ndarray:
         kk = np.arange(deg + 1)
         xs = np.cos(np.pi * (kk + 0.5) / (deg + 1))
-        f = np.cos(2 * np.pi * (self.B * xs - 0.25) / (1 << r))
+        f = np.cos(2 * np.pi * (bnd * xs - 0.25) / (1 << r))
         return np.polynomial.chebyshev.chebfit(xs, f, deg)
 
     def _prepare(self, M: Dict[int, np.ndarray]):
@@ -280,22 +300,130 @@ class Bootstrapper:
         T.clear()  # ev / tk form a closure cycle: release the T_k now, not at the next gc pass
         return e.add(out, c0)
 
+    def chebyshev_opt(self, x: Ciphertext, coeffs: np.ndarray) -> Ciphertext:
+        """sum_k c_k T_k(x) in depth ceil(log2(deg + 1)) -- one level less than `chebyshev`.
+
+        Canonical scales make every non-integer constant cost a level, so a leaf
+        c_0 + ... + c_7 T_7 cannot sit at depth 3.  Here the leaves stop at degree 3 and take
+        their constants where a level is free: c_3 T_3 = T_2 (2 c_3 T_1) - c_3 T_1 gives
+            c_0 + c_1 T_1 + c_2 T_2 + c_3 T_3 = c_0 + (c_1 - c_3) T_1 + c_2 T_2 + T_2 (2 c_3 T_1)
+        (T_2 and the depth-1 multiple of x multiply at depth 2 = ceil(log2 4)); above the leaves
+        the same recursive division as `chebyshev` by the giants T_4, T_8, T_16, ..
+        (T_2g = 2 T_g^2 - 1): p = q T_g + r with deg q < g lands at depth log2(g) + 1.
+
+        Every part is produced at the level where it is consumed (`ev(c, lv)`): a node's
+        products are (a, b) pairs with both operands at lv + 1, summed by ONE relinearisation
+        together with its remainder's pairs, its linear terms (x, T_2, T_g with constants, read
+        truncated with their scale folded into the constant) and its constant: one
+        aesfhe_dot_fma per materialised node.  The depth-1 multiples of x are lincombs that land
+        at the level they are used at; the giants are level-downed once per level needed.  Degree 29: 11 relinearisations
+        (4 of them the giants T_2 .. T_16), depth 5."""
+        e = self.e
+        l0 = x.level
+        T = {1: x}
+        down = {}
+        marks = {}
+        tiny = 1e-14
+
+        def giant(g, lv=None):
+            if g not in T:
+                h = giant(g // 2)
+                T[g] = e.multiply_fma(h, h, self.rlk, alpha=2, beta=-1.0)
+            t = T[g]
+            if lv is None or t.level == lv:
+                return t
+            if (g, lv) not in down:
+                down[(g, lv)] = e.level_down(t, lv)
+            return down[(g, lv)]
+
+        def lincomb_at(terms, lv):
+            """sum k * ct as one lincomb whose output is at level lv (a zero marker ciphertext
+            at lv + 1 sets the level when every input sits higher)."""
+            cts = [c for c, _ in terms]
+            ks = [complex(k) for _, k in terms]
+            if min(c.level for c in cts) - 1 > lv:
+                if lv + 1 not in marks:
+                    marks[lv + 1] = e.zeros(1, lv + 1)
+                cts.append(marks[lv + 1])
+                ks.append(0j)
+            return e.lincomb(cts, ks)
+
+        def lin_add(lin, g, k):
+            if abs(k) >= tiny:
+                lin[g] = lin.get(g, 0.0) + k
+
+        def materialize(pairs, lin, c0, lv):
+            terms = [(giant(g), k) for g, k in sorted(lin.items())]
+            if pairs:  # products, linear terms and constant: one aesfhe_dot_fma
+                return e.dot_fma([a for a, _ in pairs], [b for _, b in pairs], self.rlk, terms, c0)
+            if not terms:
+                raise ValueError("chebyshev_opt: constant node")
+            y = lincomb_at(terms, lv)
+            return e.add(y, c0) if c0 != 0 else y
+
+        def ev(c, lv):
+            """(pairs with operands at lv + 1, {giant g: coefficient} for a lincomb at lv, c_0)"""
+            d = len(c) - 1
+            while d > 0 and abs(c[d]) < tiny:
+                d -= 1
+            lin = {}
+            if d <= 3:
+                pairs = []
+                if d == 3:
+                    lam = lincomb_at([(x, 2.0 * c[3])], lv + 1)
+                    pairs.append((giant(2, lv + 1), lam))
+                    lin_add(lin, 1, float(c[1] - c[3]))
+                elif d >= 1:
+                    lin_add(lin, 1, float(c[1]))
+                if d >= 2:
+                    lin_add(lin, 2, float(c[2]))
+                return pairs, lin, float(c[0])
+            g = 1 << (d.bit_length() - 1)
+            q = np.zeros(d - g + 1)
+            r = np.array(c[:g], dtype=float)
+            q[0] = c[g]
+            for j in range(1, d - g + 1):
+                q[j] = 2.0 * c[g + j]
+                r[g - j] -= c[g + j]
+            pairs, lin, r0 = ev(r, lv)
+            if d == g:
+                lin_add(lin, g, float(q[0]))  # q is the constant c_g
+            else:
+                qt = materialize(*ev(q, lv + 1), lv + 1)
+                pairs = pairs + [(qt, giant(g, lv + 1))]
+            return pairs, lin, r0
+
+        deg = len(coeffs) - 1
+        out = materialize(*ev(list(coeffs), l0 - math.ceil(math.log2(deg + 1))), l0 - math.ceil(math.log2(deg + 1)))
+        T.clear()
+        down.clear()
+        marks.clear()
+        return out
+
     def evalmod(self, x: Ciphertext, bits: bool = False) -> Ciphertext:
         e = self.e
-        c = self.chebyshev(x, self.cheb_bits if bits else self.cheb)
+        if bits and self.bits_opt:
+            c = self.chebyshev_opt(x, self.cheb_bits)
+        else:
+            c = self.chebyshev(x, self.cheb_bits if bits else self.cheb)
         for _ in range(self.bits_r if bits else self.r):
             c = e.multiply_fma(c, c, self.rlk, alpha=2, beta=-1.0)  # cos 2t = 2 cos^2 t - 1
         return c  # sin(2 pi Bnd x)
 
-    def _raise_to_slots(self, c: Ciphertext):
+    def _raise_to_slots(self, c: Ciphertext, bits: bool = False):
         """Level-0 ciphertext (coefficients t mod q0) -> (x_re, x_im) with slots t / (q0 Bnd) of
-        the bit-reversed real / imaginary coefficient halves, at level L - 1 - groups."""
+        the bit-reversed real / imaginary coefficient halves, at level L - 1 - groups (bit mode
+        with bits_opt: L - groups, c_in folded into the CtS diagonals)."""
         e = self.e
         c = e.switch_key(c, self.to_sparse)
         c = e.mod_raise(c, self.L)
         c = e.switch_key(c, self.from_sparse)
-        c = e.multiply(c, self.c_in)
-        for plan in self.cts:
+        if bits and self.bits_opt:
+            plans = self.cts_bits
+        else:
+            c = e.multiply(c, self.c_in)
+            plans = self.cts
+        for plan in plans:
             c = self.linear(c, plan)
         cj = e.conjugate(c, self.cjk)
         return e.add(c, cj), e.multiply_i(e.subtract(c, cj), -1)
@@ -319,8 +447,8 @@ class Bootstrapper:
         half, b in the second); after ModRaise t/q0 = I +- 1/4 + eps, so EvalMod's
         sin(2 pi t / q0) = +-cos(2 pi eps) returns the bits in the slots directly -- the
         error of the input bits enters squared, and the signal is O(1) (no q0 / D_0 gain at the
-        end).  Inputs need level >= groups; outputs are at level L - 1 - 2 groups... - r
-        (``self.bits_level``).  Returns (a', b') (b' None when b is None)."""
+        end).  Inputs need level >= groups; outputs are at ``self.bits_level`` = L - 11 with the
+        defaults (L - 13 with bits_opt=False).  Returns (a', b') (b' None when b is None)."""
         e = self.e
         lv = len(self.stc_bits)
         x = a if b is None else e.add(e.level_down(a, min(a.level, b.level)),
@@ -331,7 +459,7 @@ class Bootstrapper:
             x = e.level_down(x, lv)
         for plan in self.stc_bits:
             x = self.linear(x, plan)
-        x_re, x_im = self._raise_to_slots(x)
+        x_re, x_im = self._raise_to_slots(x, bits=True)
         if b is None:
             return self.evalmod(x_re, bits=True), None
         nb = x_re.batch

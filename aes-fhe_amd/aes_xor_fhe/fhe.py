@@ -785,6 +785,19 @@ class Engine:
         bb = (c_ct_p * n)(*[c._h for c in b])
         return self._call_ct(self._lib.dot, aa, bb, n, relinearization_key._h)
 
+    def dot_fma(self, a: Sequence[Ciphertext], b: Sequence[Ciphertext], relinearization_key: RelinearizationKey,
+                addends: Sequence = (), beta: float = 0.0) -> Ciphertext:
+        """sum_i a_i b_i + sum_j gamma_j c_j + beta for addends [(c_j, gamma_j)] (real gamma, c_j at
+        least at the products' level, truncated) with one relinearisation + rescale
+        (aesfhe_dot_fma)."""
+        n, nc = len(a), len(addends)
+        aa = (c_ct_p * n)(*[c._h for c in a])
+        bb = (c_ct_p * n)(*[c._h for c in b])
+        cc = (c_ct_p * max(nc, 1))(*[c._h for c, _ in addends])
+        g = np.ascontiguousarray([float(k) for _, k in addends] or [0.0], dtype=np.float64)
+        return self._call_ct(self._lib.dot_fma, aa, bb, n, cc, _as_ptr(g, C.c_double), nc, float(beta),
+                             relinearization_key._h)
+
     def poly2(self, x_basis: Sequence[Ciphertext], y_basis: Sequence[Ciphertext], coeffs,
               relinearization_key: RelinearizationKey) -> list:
         """outs[t] = sum_{i,j} C[t, i, j] x^i y^j for C of shape (m, nx, ny), with

@@ -2779,6 +2779,97 @@ extern "C" int aesfhe_dot(aesfhe_engine* e, const aesfhe_ct* const* a, const aes
     API_END
 }
 
+// sum_i a_i b_i + sum_j gamma_j c_j + beta, one relinearisation + rescale (include/aesfhe.h
+// aesfhe_dot_fma): the k_dot tensor sum and the addends on d0 / d1 in one pass (k_dot_fma),
+// then relin_rescale.  Bit-identical to the oracle's term-by-term sum.
+extern "C" int aesfhe_dot_fma(aesfhe_engine* e, const aesfhe_ct* const* a, const aesfhe_ct* const* b, int32_t n,
+                              const aesfhe_ct* const* c, const double* gamma, int32_t nc, double beta,
+                              const aesfhe_key* rlk, aesfhe_ct** out) {
+    API_BEGIN
+    if (n < 1) throw_err(AESFHE_EARG, "empty dot product");
+    if (nc < 0) throw_err(AESFHE_EARG, "negative addend count");
+    if (!rlk || rlk->kind != 2) throw_err(AESFHE_EARG, "dot needs a relinearization key");
+    int l = a[0]->level, B = 1;
+    for (int i = 0; i < n; i++) {
+        if (a[i]->np != 2 || b[i]->np != 2) throw_err(AESFHE_EDEGREE, "dot inputs should have 2 polynomials");
+        l = std::min(l, std::min(a[i]->level, b[i]->level));
+        B = std::max(B, std::max(a[i]->B, b[i]->B));
+    }
+    for (int j = 0; j < nc; j++) {
+        if (c[j]->np != 2) throw_err(AESFHE_EDEGREE, "dot_fma addends should have 2 polynomials");
+        B = std::max(B, c[j]->B);
+    }
+    for (int j = 0; j < nc; j++)
+        if (c[j]->level < l) throw_err(AESFHE_ELEVEL, "dot_fma addend level %d below the product level %d", c[j]->level, l);
+    for (int i = 0; i < n; i++)
+        if ((a[i]->B != B && a[i]->B != 1) || (b[i]->B != B && b[i]->B != 1)) throw_err(AESFHE_EARG, "batch mismatch");
+    for (int j = 0; j < nc; j++)
+        if (c[j]->B != B && c[j]->B != 1) throw_err(AESFHE_EARG, "batch mismatch");
+    if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a dot product");
+    const int nl = l + 1;
+    std::vector<std::unique_ptr<Aligned>> al;
+    std::vector<const u64*> pa, pb;
+    std::vector<long> sa, sb;
+    for (int i = 0; i < n; i++) {
+        if (a[i]->is_zero || b[i]->is_zero) continue;
+        al.emplace_back(new Aligned());
+        align_to(e, a[i], l, *al.back());
+        const View va = al.back()->v;
+        al.emplace_back(new Aligned());
+        align_to(e, b[i], l, *al.back());
+        const View vb = al.back()->v;
+        pa.push_back(va.d);
+        pb.push_back(vb.d);
+        sa.push_back(va.B == 1 && B > 1 ? 0 : va.bs);
+        sb.push_back(vb.B == 1 && B > 1 ? 0 : vb.bs);
+    }
+    // addends: truncated views, C_j per limb
+    const double* D = e->chain.scale.data();
+    std::vector<const u64*> cp;
+    std::vector<long> cbs, cps;
+    std::vector<u64> cf;
+    for (int j = 0; j < nc; j++) {
+        const int64_t Cc = llround(gamma[j] * (D[l] * (D[l] / D[c[j]->level])));
+        if (c[j]->is_zero || Cc == 0) continue;
+        const View v = trunc_view(c[j], l);
+        cp.push_back(v.d);
+        cbs.push_back(v.B == 1 && B > 1 ? 0 : v.bs);
+        cps.push_back(v.ps);
+        for (int i = 0; i < nl; i++) cf.push_back(h_smod(Cc, e->chain.q[i]));
+    }
+    const int64_t Rb = llround(beta * D[l]), R = llround(D[l]);
+    std::vector<u64> km(nl);
+    for (int i = 0; i < nl; i++) {
+        const u64 q = e->chain.q[i];
+        km[i] = h_mulmod(h_smod(Rb, q), h_smod(R, q), q);
+    }
+    aesfhe_ct* acc = ct_new(e, B, 3, l);
+    try {
+        const int m = (int)pa.size(), mc = (int)cp.size();
+        const u64* const* dpa = m ? (const u64* const*)upload_small(e, pa.data(), pa.size()) : nullptr;
+        const u64* const* dpb = m ? (const u64* const*)upload_small(e, pb.data(), pb.size()) : nullptr;
+        const long* dsa = m ? upload_small(e, sa.data(), sa.size()) : nullptr;
+        const long* dsb = m ? upload_small(e, sb.data(), sb.size()) : nullptr;
+        const u64* const* dcp = mc ? (const u64* const*)upload_small(e, cp.data(), cp.size()) : nullptr;
+        const long* dcb = mc ? upload_small(e, cbs.data(), cbs.size()) : nullptr;
+        const long* dcs = mc ? upload_small(e, cps.data(), cps.size()) : nullptr;
+        const u64* dcf = mc ? upload_small(e, cf.data(), cf.size()) : nullptr;
+        const u64* dkm = upload_small(e, km.data(), km.size());
+        {
+            ProfScope ps_(e, FAM_EW, 8.0 * e->N * nl * (double)B * (4.0 * m + 2.0 * mc + 3), "dot");
+            hipLaunchKernelGGL(k_dot_fma, ew_grid(e, nl, B), dim3(256), 0, e->stream, dpa, dsa, dpb, dsb, m, (long)nl * e->N,
+                               dcp, dcb, dcs, mc, dcf, dkm, nl, out_of(acc), e->q, e->qinv, e->logN);
+        }
+        HIPC(hipGetLastError());
+        *out = relin_rescale(e, acc, rlk, 1);
+    } catch (...) {
+        aesfhe_ct_free(acc);
+        throw;
+    }
+    aesfhe_ct_free(acc);
+    API_END
+}
+
 // Bivariate polynomial with shared power bases (fused BSGS):
 //   out_t = sum_{i<nx, j<ny} C[t][i][j] x^i y^j,   xb = x^1..x^{nx-1}, yb = y^1..y^{ny-1}.
 // Constants carry the integer scale S1 = Delta_{l-2} q_l q_{l-1} / Delta_l^2 (x^0, y^0 terms

@@ -236,6 +236,49 @@ __global__ void k_dot(const u64* const* __restrict__ ap, const long* __restrict_
     base[2 * o.ps] = red_m(d2, q, qi);
 }
 
+// aesfhe_dot_fma's tensor: the k_dot sum of n pairs (n may be 0) plus the addends on d0 / d1,
+// d0 += sum_j c_j0 C_j + K, d1 += sum_j c_j1 C_j (C_j = cf[j * nl + l], K = km[l]; addend j read
+// at limb l of its own layout: batch stride cbs[j], 0 = broadcast, poly stride cps[j]), one pass.
+// grid (N/256, nl, B)
+__global__ void k_dot_fma(const u64* const* __restrict__ ap, const long* __restrict__ abs_,
+                          const u64* const* __restrict__ bp, const long* __restrict__ bbs, int n,
+                          long ps, const u64* const* __restrict__ cp, const long* __restrict__ cbs,
+                          const long* __restrict__ cps, int nc, const u64* __restrict__ cf,
+                          const u64* __restrict__ km, int nl, Out o, const u64* __restrict__ qs,
+                          const double* __restrict__ qinv, int logN) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y, bb = blockIdx.z;
+    const u64 q = qs[l];
+    const double qi = qinv[l];
+    const long off = ((long)l << logN) + k;
+    u64 d0 = 0, d1 = 0, d2 = 0;
+    for (int i = 0; i < n; i++) {
+        const u64* a = ap[i] + (long)bb * abs_[i] + off;
+        const u64* b = bp[i] + (long)bb * bbs[i] + off;
+        const u64 a0 = a[0], a1 = a[ps], b0 = b[0], b1 = b[ps];
+        d0 += mul_m(a0, b0, q, qi);
+        d1 += mul_m(a0, b1, q, qi) + mul_m(a1, b0, q, qi);
+        d2 += mul_m(a1, b1, q, qi);
+        if ((i & 15) == 15) {  // keep the lazy sums below 2^52 for red_m
+            d0 = red_m(d0, q, qi);
+            d1 = red_m(d1, q, qi);
+            d2 = red_m(d2, q, qi);
+        }
+    }
+    d0 = red_m(d0, q, qi);
+    d1 = red_m(d1, q, qi);
+    for (int j = 0; j < nc; j++) {
+        const u64* c = cp[j] + (long)bb * cbs[j] + off;
+        const u64 f = cf[(long)j * nl + l];
+        d0 = add_m(d0, mul_m(c[0], f, q, qi), q);
+        d1 = add_m(d1, mul_m(c[cps[j]], f, q, qi), q);
+    }
+    u64* base = o.ptr + (long)bb * o.bs + off;
+    base[0] = add_m(d0, km[l], q);
+    base[o.ps] = d1;
+    base[2 * o.ps] = red_m(d2, q, qi);
+}
+
 // ---------------------------------------------------------------------------------------------
 // rescale
 // t[P][i][k] = centered(x[P][k]) mod q_i for i < l ; grid (N/256, l, P)

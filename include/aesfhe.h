@@ -298,6 +298,16 @@ int aesfhe_lincomb_many(aesfhe_engine *eng, const aesfhe_ct *const *cts, int32_t
 /* sum_i a_i (*) b_i, one relinearisation + one rescale for the whole sum */
 int aesfhe_dot(aesfhe_engine *eng, const aesfhe_ct *const *a, const aesfhe_ct *const *b,
                int32_t n, const aesfhe_key *rlk, aesfhe_ct **out);
+/* out = sum_i a_i (*) b_i + sum_j gamma_j c_j + beta with ONE relinearisation + rescale: level
+ * l - 1 for l = min level of the a_i, b_i (level-downed to l like aesfhe_dot); every addend c_j
+ * (2 polynomials, level >= l) is truncated to l and enters the tensor's d0 / d1 times
+ * C_j = llround(gamma_j * (D_l * (D_l / D_cj))); beta is added to d0 as
+ * llround(beta * D_l) * llround(D_l) mod q (the aesfhe_mul_fma rules, n products and nc addends).
+ * A zero-coefficient (C_j = 0) or zero addend is skipped.  (Node sums of the depth-optimal
+ * Chebyshev evaluation in the bootstrapping; no reference counterpart.) */
+int aesfhe_dot_fma(aesfhe_engine *eng, const aesfhe_ct *const *a, const aesfhe_ct *const *b,
+                   int32_t n, const aesfhe_ct *const *c, const double *gamma, int32_t nc,
+                   double beta, const aesfhe_key *rlk, aesfhe_ct **out);
 /* m bivariate polynomials over shared power bases (the 2-D LUT evaluation of the reference's
  * nibble services, xor_service.py:245-286 / sbox_service.py:116-138, fused):
  *   outs[t] = sum_{i<nx, j<ny} C[t][i][j] x^i y^j,  C = re + i*im row-major [m][nx][ny],

@@ -2096,6 +2096,72 @@ int aesfhe_dot(aesfhe_engine *e, const aesfhe_ct *const *a, const aesfhe_ct *con
     return 0;
 }
 
+/* sum_i a_i (x) b_i + sum_j gamma_j c_j + beta, one relinearisation + rescale (include/aesfhe.h
+ * aesfhe_dot_fma): the aesfhe_dot tensor sum, then every addend truncated to l times
+ * C_j = llround(gamma_j * D_l * (D_l / D_cj)) on d0 / d1 and K = llround(beta D_l) llround(D_l)
+ * on d0 (the aesfhe_mul_fma constants). */
+int aesfhe_dot_fma(aesfhe_engine *e, const aesfhe_ct *const *a, const aesfhe_ct *const *b, int32_t n,
+                   const aesfhe_ct *const *c, const double *gamma, int32_t nc, double beta,
+                   const aesfhe_key *rlk, aesfhe_ct **out) {
+    if (n < 1) return fail(AESFHE_EARG, "empty dot product");
+    if (nc < 0) return fail(AESFHE_EARG, "negative addend count");
+    if (!rlk || rlk->kind != 2) return fail(AESFHE_EARG, "dot needs a relinearization key");
+    int l = a[0]->level, B = 1;
+    for (int i = 0; i < n; i++) {
+        if (a[i]->npoly != 2 || b[i]->npoly != 2) return fail(AESFHE_EDEGREE, "dot inputs should have 2 polynomials");
+        if (a[i]->level < l) l = a[i]->level;
+        if (b[i]->level < l) l = b[i]->level;
+        if (a[i]->B > B) B = a[i]->B;
+        if (b[i]->B > B) B = b[i]->B;
+    }
+    for (int j = 0; j < nc; j++) {
+        if (c[j]->npoly != 2) return fail(AESFHE_EDEGREE, "dot_fma addends should have 2 polynomials");
+        if (c[j]->B > B) B = c[j]->B;
+    }
+    for (int j = 0; j < nc; j++)
+        if (c[j]->level < l) return fail(AESFHE_ELEVEL, "dot_fma addend level %d below the product level %d", c[j]->level, l);
+    for (int i = 0; i < n; i++)
+        if ((a[i]->B != B && a[i]->B != 1) || (b[i]->B != B && b[i]->B != 1)) return fail(AESFHE_EARG, "batch mismatch");
+    for (int j = 0; j < nc; j++)
+        if (c[j]->B != B && c[j]->B != 1) return fail(AESFHE_EARG, "batch mismatch");
+    if (l < 1) return fail(AESFHE_ELEVEL, "no level left for a dot product");
+    const int N = e->N;
+    aesfhe_ct *acc = ct_new(e, B, 3, l);
+    for (int i = 0; i < n; i++) {
+        if (a[i]->is_zero || b[i]->is_zero) continue;
+        aesfhe_ct *x = level_down_raw(e, a[i], l), *y = level_down_raw(e, b[i], l);
+        tensor_acc(e, x, y, acc);
+        aesfhe_ct_free(x);
+        aesfhe_ct_free(y);
+    }
+    const i64 Rb = llround(beta * e->scales[l]), R = llround(e->scales[l]);
+    for (int j = 0; j < nc; j++) {
+        const i64 Cc = llround(gamma[j] * (e->scales[l] * (e->scales[l] / e->scales[c[j]->level])));
+        if (c[j]->is_zero || Cc == 0) continue;
+        for (int bb = 0; bb < B; bb++)
+            for (int i = 0; i <= l; i++) {
+                const u64 q = e->q[i], cm = smod(Cc, q);
+                u64 *d0 = limb(e, acc, bb, 0, i), *d1 = limb(e, acc, bb, 1, i);
+                const u64 *c0 = limb(e, c[j], c[j]->B == 1 ? 0 : bb, 0, i);
+                const u64 *c1 = limb(e, c[j], c[j]->B == 1 ? 0 : bb, 1, i);
+                for (int k = 0; k < N; k++) {
+                    d0[k] = add_mod(d0[k], mul_mod_slow(c0[k], cm, q), q);
+                    d1[k] = add_mod(d1[k], mul_mod_slow(c1[k], cm, q), q);
+                }
+            }
+    }
+    if (Rb != 0)
+        for (int bb = 0; bb < B; bb++)
+            for (int i = 0; i <= l; i++) {
+                const u64 q = e->q[i], km = mul_mod_slow(smod(Rb, q), smod(R, q), q);
+                u64 *d0 = limb(e, acc, bb, 0, i);
+                for (int k = 0; k < N; k++) d0[k] = add_mod(d0[k], km, q);
+            }
+    *out = relin_rescale_raw(e, acc, rlk, 1);
+    aesfhe_ct_free(acc);
+    return 0;
+}
+
 /* Bivariate polynomial over shared power bases (include/aesfhe.h aesfhe_poly2), evaluated
  * term by term: per output, inner sums a_i = F_i0 + sum_{j>=1} F_ij y^j (F = llround(c*S1*
  * rx_i*ry_j), times R = llround(D_l) for an x^0 or y^0 factor, R^2 for both), tensor

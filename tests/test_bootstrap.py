@@ -84,7 +84,7 @@ def test_bootstrap_bits_oracle(oracle_lib):
     noise = 0.03 * rng.standard_normal((2, n))
     ya, yb = bs.bootstrap_bits(e.encrypt(a + noise[0], pk, level=6),
                                e.encrypt(b + noise[1], pk, level=4))
-    assert ya.level == yb.level == bs.bits_level == e.max_level - 13
+    assert ya.level == yb.level == bs.bits_level == e.max_level - 11
     # the input error enters squared: 1 - cos(2 pi e / 4) <= 1.24 e^2
     for y, v, nz in ((ya, a, noise[0]), (yb, b, noise[1])):
         err = np.abs(e.decrypt(y, sk) - v)
@@ -130,7 +130,7 @@ def test_bootstrap_bits_full_params(product_lib, gpu_available):
     rng = np.random.default_rng(5)
     a, b = rng.choice([-1.0, 1.0], n), rng.choice([-1.0, 1.0], n)
     ya, yb = bs.bootstrap_bits(e.encrypt(a, pk, level=3), e.encrypt(b, pk, level=3))
-    assert ya.level == 17
+    assert ya.level == 19  # L - 11: c_in folded into CtS, depth-5 Chebyshev sum
     assert np.abs(e.decrypt(ya, sk) - a).max() < 1e-3
     assert np.abs(e.decrypt(yb, sk) - b).max() < 1e-3
 

@@ -224,6 +224,36 @@ def test_mul_fma_and_mixed_lincomb_bit_exact(product_lib, oracle_lib, gpu_availa
         _same(g, o, cg, co)
 
 
+@pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=8, special_primes=4, seed=5)],
+                         ids=["n4096", "n65536"])
+def test_dot_fma_bit_exact(product_lib, oracle_lib, gpu_available, kw):
+    """aesfhe_dot_fma (the depth-optimal Chebyshev node sum): products at mixed levels and
+    broadcast batches, addends above the product level (truncated), zero coefficients, beta; and
+    its slots against the plain expression."""
+    g, o = _pair(product_lib, oracle_lib, **kw)
+    res = []
+    rng = np.random.default_rng(11)
+    L = kw["max_level"]
+    z = [rng.uniform(-1, 1, (2, g.slot_count)) for _ in range(5)]
+    for eng in (g, o):
+        k = _keys(eng)
+        a0, b0 = eng.encrypt(z[0], k["pk"], level=L - 2), eng.encrypt(z[1][:1], k["pk"], level=L - 2)
+        a1, b1 = eng.encrypt(z[2], k["pk"], level=L - 1), eng.encrypt(z[3], k["pk"], level=L)
+        c0 = eng.encrypt(z[4], k["pk"], level=L)
+        outs = [eng.dot_fma([a0, a1], [b0, b1], k["rlk"], [(c0, 0.75), (a1, -1.5), (b1, 0.0)], -0.5),
+                eng.dot_fma([a0], [a0], k["rlk"], [(b0, 2.0)]),
+                eng.dot_fma([a1], [b1], k["rlk"], beta=1.25)]
+        res.append((outs, k))
+    for cg, co in zip(res[0][0], res[1][0]):
+        _same(g, o, cg, co)
+    sk = res[0][1]["sk"]
+    want = [z[0] * z[1][:1] + z[2] * z[3] + 0.75 * z[4] - 1.5 * z[2] - 0.5, z[0] * z[0] + 2.0 * z[1][:1],
+            z[2] * z[3] + 1.25]
+    for cg, w, lv in zip(res[0][0], want, (L - 3, L - 3, L - 2)):
+        assert cg.level == lv
+        np.testing.assert_allclose(g.decrypt(cg, sk).real, w, atol=1e-4)
+
+
 @pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=3, special_primes=2, seed=5),
                                 dict(log_n=16, max_level=12, special_primes=10, seed=5)],
                          ids=["n4096", "n65536", "n65536K10"])

@@ -28,12 +28,14 @@ def main():
     ap.add_argument("--phases", action="store_true", help="also time each bootstrap phase")
     ap.add_argument("--baby-scale", type=int, default=2, help="BSGS baby steps x this (lazy mode)")
     ap.add_argument("--eager", action="store_true", help="rotate_hoisted + dot_pt + galois linear maps")
+    ap.add_argument("--no-opt", action="store_true", help="bit mode without bits_opt (c_in multiply, depth-6 Chebyshev)")
     a = ap.parse_args()
     e = Engine(log_n=a.log_n, max_level=a.max_level, special_primes=a.special_primes, scale_bits=a.scale_bits, seed=3)
     sk = e.create_secret_key(1)
     pk = e.create_public_key(sk)
     t = time.time()
-    bs = Bootstrapper(e, sk, e.create_relinearization_key(sk), lazy=not a.eager, baby_scale=a.baby_scale)
+    bs = Bootstrapper(e, sk, e.create_relinearization_key(sk), lazy=not a.eager, baby_scale=a.baby_scale,
+                      bits_opt=not a.no_opt)
     e.synchronize()
     setup = time.time() - t
     n = e.slot_count
@@ -53,7 +55,7 @@ def main():
                       "special_primes": a.special_primes, "scale_bits": a.scale_bits, "setup_s": round(setup, 2),
                       "ms_per_call": round(1e3 * min(ts), 1), "cts_per_call": 2 * a.batch,
                       "ms_per_ct": round(1e3 * min(ts) / (2 * a.batch), 2),
-                      "out_level": ya.level, "max_err": float(err),
+                      "out_level": ya.level, "max_err": float(err), "bits_opt": bs.bits_opt,
                       "rotation_keys": len(bs.rot)}), flush=True)
     if a.phases:
         def timed(fn, *xs):
@@ -69,12 +71,13 @@ def main():
         c, ph["to_sparse"] = timed(e.switch_key, x, bs.to_sparse)
         c, ph["mod_raise"] = timed(e.mod_raise, c, bs.L)
         c, ph["from_sparse"] = timed(e.switch_key, c, bs.from_sparse)
-        c, ph["c_in"] = timed(e.multiply, c, bs.c_in)
-        for i, plan in enumerate(bs.cts):
+        if not bs.bits_opt:
+            c, ph["c_in"] = timed(lambda v: e.materialize(e.multiply(v, bs.c_in)), c)
+        for i, plan in enumerate(bs.cts_bits):
             c, ph[f"cts{i}"] = timed(bs.linear, c, plan)
         (xr, xi), ph["conj"] = timed(lambda v: (lambda cj: (e.add(v, cj), e.multiply_i(e.subtract(v, cj), -1)))(e.conjugate(v, bs.cjk)), c)
         xx, ph["concat"] = timed(lambda p, q: e.concat([p, q]), xr, xi)
-        ch, ph["chebyshev"] = timed(bs.chebyshev, xx, bs.cheb_bits)
+        ch, ph["chebyshev"] = timed(bs.chebyshev_opt if bs.bits_opt else bs.chebyshev, xx, bs.cheb_bits)
         y = ch
         for i in range(bs.bits_r):
             y, ph[f"double{i}"] = timed(lambda v: (lambda sq: e.add(e.add(sq, sq), -1.0))(e.multiply(v, v, bs.rlk)), y)
