@@ -228,16 +228,27 @@ class AESRowRound:
 
     # A round multiplies the slot error of its input by ~10-15 (the S-box's Walsh polynomial sums
     # ~10 products, MixColumns chains three), and bit-mode bootstrapping returns its input error
-    # squared: so the error at a refresh must stay ~1e-2.  Three rounds from a fresh encryption
-    # or refresh reach ~5e-3 at N = 2^16 / 2^17 (measured, tools/aes10_diag.py); a fourth (L = 35
-    # allows it by levels) reached 0.12 at N = 2^17 and the run diverged.
-    MAX_ROUNDS_PER_REFRESH = 3
+    # squared: so the error at a refresh must stay ~1e-2.  Measured at N = 2^16 (scale 40,
+    # tools/aes10_diag.py, max | |v| - 1 | over all slots): three rounds from a fresh encryption
+    # reach 1.8e-3, but a refresh leaves ~1.5e-4, after which two rounds reach 5-7e-3 and a third
+    # ~0.1 -- too much for the next refresh (a fourth from a fresh encryption, which L = 35 allows
+    # by levels, reached 0.12 at N = 2^17 and the run diverged).  The final round may still follow
+    # as a third one: its output is only decrypted (decision margin 1; measured <= 0.13).
+    MAX_ROUNDS_FRESH = 3
+    MAX_ROUNDS_AFTER_REFRESH = 2
+
+    def needs_refresh(self, level: int, final: bool, since: int, refreshed: bool, stc: int) -> bool:
+        """Refresh before the next round?  When its depth does not fit, when a middle round would
+        leave fewer than `stc` (SlotToCoeff) levels, or after MAX_ROUNDS_* middle rounds."""
+        need = self.FINAL_DEPTH if final else self.ROUND_DEPTH
+        limit = self.MAX_ROUNDS_AFTER_REFRESH if refreshed else self.MAX_ROUNDS_FRESH
+        return level < need or (not final and (level - need < stc or since >= limit))
 
     def encrypt_aes128(self, bits, keys, bs, timings: dict | None = None, pairs_per_call: int = 8,
                        progress=None):
         """AES-128 encryption of the bit state under the 11 encrypted round keys `keys`
         (FIPS-197 section 5.1), bootstrapping with `bs` (a bootstrap.Bootstrapper) as the level
-        budget requires, and at least every MAX_ROUNDS_PER_REFRESH rounds.  Returns the state
+        budget and the error budget (needs_refresh) require.  Returns the state
         and the number of refreshes.  progress: optional callable(str) told after each step."""
         import time
         stc = len(bs.stc_bits)
@@ -246,9 +257,8 @@ class AESRowRound:
         since = 0
         for rnd in range(1, 11):
             final = rnd == 10
-            need = self.FINAL_DEPTH if final else self.ROUND_DEPTH
             lvl = min(c.level for row in S for c in row)
-            if lvl < need or (not final and lvl - need < stc) or since >= self.MAX_ROUNDS_PER_REFRESH:
+            if self.needs_refresh(lvl, final, since, refreshes > 0, stc):
                 since = 0
                 t0 = time.perf_counter()
                 S = self.refresh(S, bs, pairs_per_call)

@@ -18,7 +18,7 @@ Pipeline for a ciphertext c at level 0 encrypting slots z (message m at the cano
 
 Depth = 1 + 2 * groups + ceil(log2(deg + 1)) + 1 + r (16 with the defaults at any N).  The bit
 mode (bootstrap_bits, StC first) spends groups levels before ModRaise and, with bits_opt,
-groups + ceil(log2(deg + 1)) + r = 3 + 5 + 3 = 11 after it: c_in rides in the CtS diagonals and
+groups + ceil(log2(deg + 1)) + r = 3 + 4 + 4 = 11 after it: c_in rides in the CtS diagonals and
 the Chebyshev sum is evaluated depth-optimally (chebyshev_opt).
 """
 from __future__ import annotations
@@ -108,7 +108,7 @@ def _bsgs_plan(offsets: List[int], n: int):
 class Bootstrapper:
     def __init__(self, engine: Engine, sk, rlk, cjk=None, *, hw: int = 32, K: float = 12.0,
                  r: int = 3, deg: int = 31, groups: int = 3, seed: int = 7,
-                 bits_deg: int | None = None, bits_r: int = 3, lazy: bool = True, baby_scale: int = 2,
+                 bits_deg: int | None = None, bits_r: int | None = None, lazy: bool = True, baby_scale: int = 2,
                  bits_opt: bool = True):
         e = self.e = engine
         self.rlk = rlk
@@ -122,7 +122,9 @@ class Bootstrapper:
         # instead of 13), which is what lets ten AES rounds run on three refreshes
         self.bits_opt = bits_opt
         if bits_deg is None:
-            bits_deg = 29 if bits_opt else 31
+            bits_deg = 15 if bits_opt else 31
+        if bits_r is None:
+            bits_r = 4 if bits_opt else 3
         self.bits_deg, self.bits_r = bits_deg, bits_r
         # lazy: linear maps through aesfhe_linear_bsgs (baby rotations kept in Q u P, one ModDown
         # per giant + one for all giant key switches); baby steps are then cheap, so the BSGS
@@ -176,12 +178,42 @@ class Bootstrapper:
         # for every bit of a value, so it adds coherently through the S-box's Walsh polynomial
         # and the MixColumns products: full AES-128 failed at N = 2^10 with it (random noise of
         # 2e-4 does not), hence the bits_deg / bits_r knobs default to the general fit.
-        # With bits_opt the bit-mode fit is degree 29 (fit error after the double angles 3e-10).
+        # With bits_opt the bit mode uses degree 15 and r = 4 (depth 4 + 4, 7 + 4
+        # relinearisations instead of 11 + 3 for degree 29 and r = 3), fitted where the bit mode
+        # evaluates it (_bits_fit): the plain Chebyshev interpolant's error, 5.4e-5 at
+        # t / q0 = +1/4 (I = 0, where all four double angles amplify it 4x), drops to ~2e-7.
         self.cheb = self._cheb_fit(deg, r, self.B)
-        self.cheb_bits = self._cheb_fit(bits_deg, bits_r, self.B_bits if bits_opt else self.B)
+        if bits_opt:
+            self.cheb_bits = self._bits_fit(bits_deg, bits_r, self.B_bits, K)
+        else:
+            self.cheb_bits = self._cheb_fit(bits_deg, bits_r, self.B)
         self.depth = 1 + 2 * groups + math.ceil(math.log2(deg + 1)) + 1 + r
         cheb_depth = math.ceil(math.log2(bits_deg + 1)) + (0 if bits_opt else 1)
         self.bits_level = self.L - ((0 if bits_opt else 1) + groups + cheb_depth + bits_r)
+
+    @staticmethod
+    def _bits_fit(deg: int, r: int, bnd: float, K: float, width: float = 1e-2,
+                  weight: float = 1e3) -> np.ndarray:
+        """Chebyshev coefficients of cos(2 pi (bnd x - 1/4) / 2^r) for the bit mode, by weighted
+        least squares: 400 Chebyshev nodes of [-1, 1] (weight 1) plus the points the bit mode
+        actually feeds it, x = (I +- 1/4 + d) / bnd for |I| <= K and |d| <= width (input bit errors
+        up to 4 width), weighted by `weight` times the error gain of the r double angles there
+        (prod |4 cos(2^k theta)|, 4^r at I = 0 and I = 2^(r-1), near 0 elsewhere)."""
+        def f(x):
+            return np.cos(2 * np.pi * (bnd * x - 0.25) / (1 << r))
+        grid = np.cos(np.pi * (np.arange(400) + 0.5) / 400)
+        dl = np.linspace(-width, width, 25)
+        I = np.arange(-int(K), int(K) + 1)
+        pts = np.concatenate([(i + s + dl) / bnd for i in I for s in (0.25, -0.25)])
+        gain = np.ones_like(pts)
+        c = f(pts)
+        for _ in range(r):
+            gain *= np.abs(4 * c)
+            c = 2 * c * c - 1
+        X = np.concatenate([grid, pts])
+        w = np.concatenate([np.ones_like(grid), weight * gain / gain.max()])
+        V = np.polynomial.chebyshev.chebvander(X, deg) * w[:, None]
+        return np.linalg.lstsq(V, f(X) * w, rcond=None)[0]
 
     @staticmethod
     def _cheb_fit(deg: int, r: int, bnd: float) -> np.ndarray:
@@ -316,8 +348,9 @@ class Bootstrapper:
         together with its remainder's pairs, its linear terms (x, T_2, T_g with constants, read
         truncated with their scale folded into the constant) and its constant: one
         aesfhe_dot_fma per materialised node.  The depth-1 multiples of x are lincombs that land
-        at the level they are used at; the giants are level-downed once per level needed.  Degree 29: 11 relinearisations
-        (4 of them the giants T_2 .. T_16), depth 5."""
+        at the level they are used at; the giants are level-downed once per level needed.
+        Degree 15: 7 relinearisations (3 of them the giants T_2, T_4, T_8), depth 4; degree 29:
+        11 (4 giants), depth 5."""
         e = self.e
         l0 = x.level
         T = {1: x}

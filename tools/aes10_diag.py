@@ -42,12 +42,13 @@ S = R.add_round_key(st, keys[0])
 check("ark0", S, plain)
 stc = len(bs.stc_bits)
 since = 0
+nref = 0
 for rnd in range(1, 11):
     final = rnd == 10
-    need = R.FINAL_DEPTH if final else R.ROUND_DEPTH
     lvl = min(c.level for row in S for c in row)
-    if lvl < need or (not final and lvl - need < stc) or since >= R.MAX_ROUNDS_PER_REFRESH:
+    if R.needs_refresh(lvl, final, since, nref > 0, stc):
         since = 0
+        nref += 1
         S = R.refresh(S, bs)
         check(f"refresh<{rnd}", S, plain)
     if final:
