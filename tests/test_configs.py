@@ -1,4 +1,4 @@
-"""BASELINE.json configs 1 and 5 at their own parameters.
+"""BASELINE.json configs 1, 4 and 5 at their own parameters.
 
 Config 1 -- "Single AES round, 1 ciphertext, N=2^14, L=8, CPU engine_context (test_total.py
 plumbing)": the reference's AddRoundKey driver (test_all_process.py:12-48: EngineContext ->
@@ -12,6 +12,9 @@ Config 5 -- "Full AES-128 10 rounds, N=2^17, L=35, batch=512 ciphertexts over 8 
 rank's shard runs on one GPU.  Bit-exact ct x ct multiply + rotation against the oracle at
 N = 2^17, L = 35, and full AES-128 (ARK0 + 10 rounds with bit-mode bootstrapping) at those
 parameters, FIPS-197 verified (C.1 vector in block 0).
+
+Config 4 -- "Full AES-128 10 rounds end-to-end, N=2^16, L=30, batch=64 ciphertexts": the whole
+131 072-block batch at the bench's parameters, FIPS-197 verified block by block.
 """
 from pathlib import Path
 
@@ -98,6 +101,34 @@ def test_config5_aes128_ten_rounds(product_lib, gpu_available):
     assert np.array_equal(R.decrypt_blocks(one), T.aes_round(blocks, T.expand_key(key)[1]))
     out, nref = R.encrypt_aes128(st, [R.encrypt_round_key(k) for k in T.expand_key(key)], bs)
     got = R.decrypt_blocks(out)
-    want = np.stack([[T.encrypt_block(b, key) for b in blk] for blk in blocks])
+    want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
     assert np.array_equal(got, want)
     assert bytes(got[0, 0]) == bytes.fromhex("69c4e0d86a7b0430d8cdb78070b4c55a")
+
+
+# config 4 at the bench's parameters (bench.py defaults: scale 40, K = 10)
+CONFIG4 = dict(log_n=16, max_level=30, special_primes=10, scale_bits=40)
+
+
+@pytest.mark.gpu
+def test_config4_full_batch_ten_rounds(product_lib, gpu_available):
+    """Config 4 -- "Full AES-128 10 rounds end-to-end, N=2^16, L=30, batch=64 ciphertexts": the
+    whole batch (64 reference ciphertexts of 2048 blocks = 16 row-sliced sets of 8192 blocks =
+    131 072 blocks) through ARK0 + 10 rounds on three bit-mode refreshes of 8 ciphertexts per
+    call (the bench leg's shape), every block checked against FIPS-197."""
+    from aes_xor_fhe.aes_round_bits import AESRowRound
+    from aes_xor_fhe.bootstrap import Bootstrapper
+    from aes_xor_fhe.fhe import Engine
+    e = Engine(_lib=product_lib, seed=23, **CONFIG4)
+    sk = e.create_secret_key()
+    rlk = e.create_relinearization_key(sk)
+    R = AESRowRound(e, sk, e.create_public_key(sk), rlk)
+    bs = Bootstrapper(e, sk, rlk)
+    key = np.random.default_rng(4).integers(0, 256, 16, dtype=np.uint8)
+    blocks = np.random.default_rng(6).integers(0, 256, (16, R.n_blk, 16), dtype=np.uint8)
+    assert blocks.shape[0] * R.n_blk == 64 * 2048
+    out, nref = R.encrypt_aes128(R.encrypt_blocks(blocks), [R.encrypt_round_key(k) for k in T.expand_key(key)],
+                                 bs, pairs_per_call=2)
+    assert nref == 3
+    want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
+    assert np.array_equal(R.decrypt_blocks(out), want)
