@@ -96,6 +96,69 @@ def test_bootstrap_bits_oracle(oracle_lib):
         bs.bootstrap_bits(e.encrypt(a, pk, level=2))
 
 
+@pytest.mark.parametrize("deg", [3, 7, 15, 29])
+def test_chebyshev_opt_depth_and_values(oracle_lib, deg):
+    """chebyshev_opt (bootstrap.py): a random Chebyshev series of degree deg lands exactly
+    ceil(log2(deg + 1)) levels down -- never deeper than the recursive `chebyshev`, one level
+    shallower at degrees 7 and 15 -- and decrypts to numpy's chebval of the slots; both evaluators
+    agree."""
+    e, sk, pk, rlk = _engine(oracle_lib, max_level=12)
+    bs = Bootstrapper(e, sk, rlk, groups=1)
+    rng = np.random.default_rng(deg)
+    c = rng.uniform(-1, 1, deg + 1) / (1 + np.arange(deg + 1))
+    x = rng.uniform(-1, 1, e.slot_count)
+    ct = e.encrypt(x, pk, level=10)
+    y = bs.chebyshev_opt(ct, c)
+    assert y.level == 10 - math.ceil(math.log2(deg + 1))
+    want = np.polynomial.chebyshev.chebval(x, c)
+    assert np.abs(e.decrypt(y, sk).real - want).max() < 1e-6
+    if deg >= 7:
+        z = bs.chebyshev(ct, c)
+        assert z.level == (y.level - 1 if deg in (7, 15) else y.level)
+        assert np.abs(e.decrypt(z, sk).real - want).max() < 1e-6
+
+
+def test_bits_fit_error_at_the_evaluated_points():
+    """_bits_fit: degree 15 with 4 double angles matches sin(2 pi t / q0) to 1e-6 wherever the bit
+    mode evaluates it (t / q0 = I +- 1/4 + d, |I| <= K, |d| <= 1e-2), where the plain Chebyshev
+    interpolant of rounds 1-2 was off by 5.4e-5 (at I = 0, +1/4)."""
+    B, K, r = 13.0, 12.0, 4
+    c = Bootstrapper._bits_fit(15, r, B, K)
+    cheb = Bootstrapper._cheb_fit(15, r, B)
+    I = np.arange(-int(K), int(K) + 1)
+    pts = np.concatenate([(i + s + np.linspace(-1e-2, 1e-2, 41)) / B for i in I for s in (0.25, -0.25)])
+
+    def post(cc):
+        g = np.polynomial.chebyshev.chebval(pts, cc)
+        for _ in range(r):
+            g = 2 * g * g - 1
+        return g
+    ideal = np.cos(2 * np.pi * (B * pts - 0.25))  # = sin(2 pi B x)
+    assert np.abs(post(c) - ideal).max() < 1e-6
+    assert np.abs(post(cheb) - ideal).max() > 4e-5
+
+
+def test_refresh_schedule():
+    """AESRowRound.needs_refresh: ten rounds on three refreshes at L = 30 (bootstrap output 19)
+    and at config 5's L = 35 (output 24); at most 2 middle rounds after a refresh."""
+    from aes_xor_fhe.aes_round_bits import AESRowRound
+    R = AESRowRound.__new__(AESRowRound)
+    for L, out in ((30, 19), (35, 24)):
+        lvl, since, nref, plan = L - 1, 0, 0, []
+        for rnd in range(1, 11):
+            final = rnd == 10
+            if R.needs_refresh(lvl, final, since, nref > 0, 3):
+                lvl, since, nref = out, 0, nref + 1
+                plan.append("R")
+            lvl -= R.FINAL_DEPTH if final else R.ROUND_DEPTH
+            assert lvl >= 0
+            since += 1
+            plan.append(str(rnd))
+        assert nref == 3, (L, plan)
+        segs = "".join(plan).split("R")
+        assert all(len([ch for ch in seg if ch != "0"]) <= 3 for seg in segs)
+
+
 @pytest.mark.gpu
 def test_bootstrap_bits_bit_exact_vs_oracle(product_lib, oracle_lib, gpu_available):
     outs = []

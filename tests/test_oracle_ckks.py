@@ -172,6 +172,26 @@ def test_poly2_int_semantics(env):
         e.poly2_int(xb, yb, np.full((1, 4, 5), 300), 64, rlk)
 
 
+def test_dot_fma_semantics(env):
+    """aesfhe_dot_fma = sum a_i b_i + sum gamma_j c_j + beta at level l - 1, products level-aligned,
+    addends truncated (include/aesfhe.h); an addend below the products' level is refused."""
+    e, sk, pk, rlk, _ = env
+    rng = np.random.default_rng(12)
+    z = [rng.uniform(-1, 1, e.slot_count) for _ in range(5)]
+    a0, b0 = e.encrypt(z[0], pk, level=4), e.encrypt(z[1], pk, level=5)
+    a1, b1 = e.encrypt(z[2], pk, level=6), e.encrypt(z[3], pk, level=4)
+    c0 = e.encrypt(z[4], pk, level=6)
+    out = e.dot_fma([a0, a1], [b0, b1], rlk, [(c0, -0.5), (a1, 2.0)], 0.25)
+    assert out.level == 3
+    want = z[0] * z[1] + z[2] * z[3] - 0.5 * z[4] + 2.0 * z[2] + 0.25
+    np.testing.assert_allclose(e.decrypt(out, sk).real, want, atol=1e-5)
+    only = e.dot_fma([a1], [a1], rlk)
+    assert only.level == 5
+    np.testing.assert_allclose(e.decrypt(only, sk).real, z[2] * z[2], atol=1e-5)
+    with pytest.raises(RuntimeError, match="below the product level"):
+        e.dot_fma([a1], [b0], rlk, [(a0, 1.0)])
+
+
 def test_rotate_hoisted_oracle(oracle_lib):
     """Hoisted rotations (shared ModUp; DESIGN.md 3.16 / include/aesfhe.h) = np.roll, batched,
     and agree with the ordinary rotation up to key-switch noise."""
