@@ -69,12 +69,18 @@ def log(msg):
     print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
-def pmc_record():
-    """The committed PMC measurement of one round step (None if absent)."""
+def pmc_record(args=None):
+    """The committed PMC measurement of one round step (None if absent); with args, only when it
+    measured this run's workload shape (N, L, K, sets per GPU, layout)."""
     try:
-        return json.loads(PMC_FILE.read_text())
+        rec = json.loads(PMC_FILE.read_text())
     except (OSError, ValueError):
         return None
+    if args is not None and rec.get("workload") != {"log_n": args.log_n, "max_level": args.max_level,
+                                                     "special_primes": args.special_primes,
+                                                     "batch": args.batch, "layout": args.layout}:
+        return None
+    return rec
 
 
 def kernel_table(eng, pmc, steps):
@@ -134,7 +140,7 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=2,
                     help="profiled (HIP-event) round steps after the timed region, for the roofline")
     ap.add_argument("--aes10-ppc", type=int, default=0,
-                    help="bit-ciphertext pairs per bootstrap call (0: 32 / aes10-batch)")
+                    help="bit-ciphertext pairs per bootstrap call (0: 64 / aes10-batch at N = 2^16, 16 / aes10-batch at 2^17)")
     ap.add_argument("--aes10-batch", type=int, default=16,
                     help="ciphertext sets for the full 10-round AES-128 measurement (0: skip)")
     ap.add_argument("--client-batch", type=int, default=8,
@@ -213,9 +219,11 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     keys = [R.encrypt_round_key(rk) for rk in T.expand_key(key)]
     rng = np.random.default_rng(2000 + rank)
     nb = args.aes10_batch
-    # ~32 ciphertexts per Bootstrapper call at N = 2^16; half that per doubling of N (a bit
-    # ciphertext at N = 2^17, L = 35 is 2.3x larger: 32 per call overflowed the pool, measured)
-    ppc = args.aes10_ppc or max(1, (32 >> max(0, args.log_n - 16)) // nb)
+    # ~64 ciphertexts per Bootstrapper call at N = 2^16 (32: 14.18 k blocks/s, 64: 14.51 k, pool
+    # peak 157 GB); 16 at N = 2^17 (a bit ciphertext at L = 35 is 2.3x larger: 32 per call
+    # overflowed the pool, measured)
+    per_call = 64 if args.log_n <= 16 else 16 >> (args.log_n - 17)
+    ppc = args.aes10_ppc or max(1, per_call // nb)
     # warm-up of the same shape: materialises the bootstrap plaintexts and fills the device pool
     # with every buffer size of the run, so the timed run makes no hipMalloc
     log("aes10: bootstrapper ready; warm-up run")
@@ -684,7 +692,7 @@ def main():
         prof_ms = (time.perf_counter() - t0) * 1e3 / args.profile_steps
         eng._check(eng._lib.engine_profile_read(eng._h, b"ntt", C.byref(n_ntt), C.byref(ms_ntt), C.byref(by_ntt)))
         eng._check(eng._lib.engine_profile_read(eng._h, b"keyswitch", C.byref(n_ks), C.byref(ms_ks), C.byref(by_ks)))
-        kernels = kernel_table(eng, pmc_record(), args.profile_steps)
+        kernels = kernel_table(eng, pmc_record(args), args.profile_steps)  # PMC bytes only for this shape
         eng._check(eng._lib.engine_profile(eng._h, 0))
 
     # the round's buffers and cached blocks (other sizes) would otherwise crowd the device in
@@ -728,11 +736,9 @@ def main():
         avg_launch_ms = ms_ntt.value / max(n_ntt.value, 1)
         achieved = by_ntt.value / (ms_ntt.value * 1e-3) / 1e9 if ms_ntt.value else 0.0
         alg_per_launch = by_ntt.value / max(n_ntt.value, 1)
-        pmc = pmc_record()
+        pmc = pmc_record(args)
         fam = (pmc or {}).get("ntt_family") or {}
-        same_shape = bool(fam) and pmc.get("workload") == {"log_n": args.log_n, "max_level": args.max_level,
-                                                           "special_primes": args.special_primes,
-                                                           "batch": args.batch, "layout": args.layout}
+        same_shape = bool(fam)
         rec = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -767,7 +773,7 @@ def main():
                 "traffic": round(fam["hbm_bytes_per_launch"]) if same_shape else None,
                 "traffic_over_alg": round(fam["hbm_bytes_per_launch"] / alg_per_launch, 3) if same_shape and alg_per_launch else None,
                 "traffic_source": PMC_NOTE if same_shape else "no PMC record of this workload",
-                "traffic_head": (pmc or {}).get("head") if same_shape else None,
+                "traffic_head": pmc.get("head") if same_shape else None,
                 "measured_over": f"{args.profile_steps} profiled round steps after the timed region",
                 "launches": n_ntt.value, "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "alg_bytes_per_launch": round(by_ntt.value / max(n_ntt.value, 1)),
