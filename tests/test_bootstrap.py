@@ -75,16 +75,19 @@ def test_bootstrap_general_oracle(oracle_lib):
     assert np.abs(e.decrypt(out, sk) - z).max() < 1e-3
 
 
-def test_bootstrap_bits_oracle(oracle_lib):
+@pytest.mark.parametrize("opt", [True, False], ids=["bits_opt", "round2_path"])
+def test_bootstrap_bits_oracle(oracle_lib, opt):
+    """Bit mode: depth 11 with bits_opt (c_in in CtS, depth-optimal degree-15 EvalMod), 13 on the
+    round-2 path; both square the input error."""
     e, sk, pk, rlk = _engine(oracle_lib)
-    bs = Bootstrapper(e, sk, rlk)
+    bs = Bootstrapper(e, sk, rlk, bits_opt=opt)
     n = e.slot_count
     rng = np.random.default_rng(4)
     a, b = rng.choice([-1.0, 1.0], n), rng.choice([-1.0, 1.0], n)
     noise = 0.03 * rng.standard_normal((2, n))
     ya, yb = bs.bootstrap_bits(e.encrypt(a + noise[0], pk, level=6),
                                e.encrypt(b + noise[1], pk, level=4))
-    assert ya.level == yb.level == bs.bits_level == e.max_level - 11
+    assert ya.level == yb.level == bs.bits_level == e.max_level - (11 if opt else 13)
     # the input error enters squared: 1 - cos(2 pi e / 4) <= 1.24 e^2
     for y, v, nz in ((ya, a, noise[0]), (yb, b, noise[1])):
         err = np.abs(e.decrypt(y, sk) - v)
