@@ -703,31 +703,40 @@ def main():
     eng.pool_trim()
 
     log(f"checked ({ok}), profiled")
+
+    def secondary(name, fn):
+        """A secondary leg: on one GPU its failure is reported in the line (the round above is
+        already measured); under torchrun it propagates, so that no rank waits in a collective
+        its peer left."""
+        try:
+            return fn()
+        except Exception as ex:
+            if world > 1:
+                raise
+            log(f"{name} failed: {ex!r}")
+            return {"error": repr(ex)}
+        finally:
+            gc.collect()
+            eng.pool_trim()
+
     sg = None
     if dist is not None:
-        sg = scatter_gather_leg(args, eng, R, rank, world, barrier, allmax)
-        gc.collect()
-        eng.pool_trim()
+        sg = secondary("scatter/gather", lambda: scatter_gather_leg(args, eng, R, rank, world, barrier, allmax))
     configs = None
     log("scatter/gather done" if sg else "no scatter/gather leg")
     if world == 1 and not args.no_configs and args.log_n == 16:
-        configs = config_legs(args, eng, R)
-        gc.collect()
-        eng.pool_trim()
-        if not args.no_harness:
-            configs["reference_harness"] = reference_harness_leg(args)
-            gc.collect()
+        configs = secondary("config legs", lambda: config_legs(args, eng, R))
+        if not args.no_harness and "error" not in configs:
+            configs["reference_harness"] = secondary("reference harness", lambda: reference_harness_leg(args))
             log("reference harness leg done")
     client = None
     if world == 1 and args.client_batch > 0 and args.layout == "rows":
-        client = client_path_leg(args, eng, R, key)
-        gc.collect()
-        eng.pool_trim()
+        client = secondary("client path", lambda: client_path_leg(args, eng, R, key))
         log("client path leg done")
     aes10 = None
     log("config legs done" if configs else "no config legs")
     if args.aes10_batch > 0 and args.layout == "rows":
-        aes10 = aes128_full(args, eng, R, rank, barrier, allmax)
+        aes10 = secondary("aes10", lambda: aes128_full(args, eng, R, rank, barrier, allmax))
 
     blocks_per_step = args.batch * R.n_blk * world
     value = blocks_per_step * args.steps / elapsed
