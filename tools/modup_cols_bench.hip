@@ -224,6 +224,17 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         return 1e3 * ms / reps;
     };
+    // the column pass alone: in place (the engine's form) and out of place (into ext2's layout)
+    Span sp2{ext2 + (long)A * N, neN, nt, (l + 1) - A, A, Lp1};
+    auto cols_in = [&]() { hipLaunchKernelGGL(k_nttf_fwd_cols<256>, dim3(16, B * nt), dim3(256), 0, s, sp, sp, T); };
+    auto cols_out = [&]() { hipLaunchKernelGGL(k_nttf_fwd_cols<256>, dim3(16, B * nt), dim3(256), 0, s, sp, sp2, T); };
+    auto modup = [&]() {
+        launch_modup<A>(dim3(N / 256, 1, B), s, (const u64*)dc, lN, ext1, neN, lo, l, ne, (const double*)dhinv,
+                        (const TwD*)dhat, K, (const u64*)dq, (const double*)dqinv, Lp1, logN);
+    };
+    const double tci = timeit(cols_in), tco = timeit(cols_out), tm = timeit(modup), tci2 = timeit(cols_in), tco2 = timeit(cols_out);
+    fprintf(stderr, "{\"cols_inplace_us\": [%.1f, %.1f], \"cols_outofplace_us\": [%.1f, %.1f], \"modup_us\": %.1f, "
+            "\"cols_bytes\": %.0f}\n", tci, tci2, tco, tco2, tm, 16.0 * N * B * nt);
     const double tb = timeit(base), tf = timeit(fused), tb2 = timeit(base), tf2 = timeit(fused);
     CK(hipGetLastError());
     std::vector<u64> h1((size_t)B * neN), h2((size_t)B * neN);
