@@ -49,6 +49,7 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
 
+COPY_HBM_GBS = 6290.0  # measured float4 copy on MI355X (MI355X_MICROARCH.md), for context only
 PEAK_HBM_GBS = 8000.0
 METRIC = "AES-128 blocks/sec (homomorphic full round) at N=2^16, L=30; 1/2/4/8 MI355X"
 SEED = 0x5EED5EED  # the CPU baseline's engine (reproducible); the GPU ranks share a 256-bit seed
@@ -779,6 +780,9 @@ def main():
                 "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "frac_per_pass_rw": round(2 * achieved / PEAK_HBM_GBS, 4),  # each pass's own read+write
+                # context: the streaming-copy rate this part reaches (MI355X_MICROARCH.md, float4 copy)
+                "copy_gbs_measured": COPY_HBM_GBS,
+                "frac_per_pass_rw_vs_copy": round(2 * achieved / COPY_HBM_GBS, 4),
                 "traffic": round(fam["hbm_bytes_per_launch"]) if same_shape else None,
                 "traffic_over_alg": round(fam["hbm_bytes_per_launch"] / alg_per_launch, 3) if same_shape and alg_per_launch else None,
                 "traffic_source": PMC_NOTE if same_shape else "no PMC record of this workload",
