@@ -36,6 +36,7 @@ class Params(C.Structure):
         ("seed", C.c_uint64),
         ("primes", C.POINTER(C.c_uint64)),
         ("seed_ext", C.c_uint64 * 3),
+        ("digit_primes", C.c_int32),
     ]
 
 
@@ -94,6 +95,7 @@ SIGNATURES = [
     ("aesfhe_ct_copy", C.c_int, [c_eng_p, c_ct_p, _P(c_ct_p)]),
     ("aesfhe_ct_slice", C.c_int, [c_eng_p, c_ct_p, C.c_int32, C.c_int32, _P(c_ct_p)]),
     ("aesfhe_ct_concat", C.c_int, [c_eng_p, _P(c_ct_p), C.c_int32, _P(c_ct_p)]),
+    ("aesfhe_ct_gather", C.c_int, [c_eng_p, c_ct_p, _P(C.c_int32), C.c_int32, _P(c_ct_p)]),
     ("aesfhe_ct_zero", C.c_int, [c_eng_p, C.c_int32, C.c_int32, _P(c_ct_p)]),
     ("aesfhe_ct_free", None, [c_ct_p]),
     ("aesfhe_pt_create", C.c_int, [c_eng_p, _P(C.c_int64), C.c_int32, _P(c_pt_p)]),

@@ -77,11 +77,11 @@ class AESRowRound:
         return [np.ascontiguousarray(b[:, :, [r + 4 * c for c in range(4)]].transpose(0, 2, 1)).reshape(b.shape[0], self.sc)
                 for r in range(4)]
 
-    def unpack(self, rows: Sequence[np.ndarray]) -> np.ndarray:
-        nb = rows[0].shape[0]
-        out = np.empty((nb, self.n_blk, 16), dtype=np.uint8)
+    def unpack(self, rows: Sequence[np.ndarray], nb: int | None = None) -> np.ndarray:
+        n = rows[0].shape[0]  # one set per batch element: nothing padded
+        out = np.empty((n, self.n_blk, 16), dtype=np.uint8)
         for r in range(4):
-            v = np.asarray(rows[r], dtype=np.uint8).reshape(nb, 4, self.n_blk)
+            v = np.asarray(rows[r], dtype=np.uint8).reshape(n, 4, self.n_blk)
             for c in range(4):
                 out[:, :, r + 4 * c] = v[:, c, :]
         return out
@@ -100,7 +100,7 @@ class AESRowRound:
                        for j in range(8)])
         return st
 
-    def decrypt_blocks_device(self, bits):
+    def decrypt_blocks_device(self, bits, nb: int | None = None):
         """decrypt_blocks into a (NB, n_blk, 16) uint8 torch tensor on the client device."""
         import torch
         rows = []
@@ -126,7 +126,9 @@ class AESRowRound:
     def encrypt_blocks(self, blocks: np.ndarray) -> List[List[Ciphertext]]:
         return self.encrypt_bytes_rows(self.pack(blocks))
 
-    def decrypt_blocks(self, bits: Sequence[Sequence[Ciphertext]]) -> np.ndarray:
+    def decrypt_blocks(self, bits: Sequence[Sequence[Ciphertext]], nb: int | None = None) -> np.ndarray:
+        """The state's blocks (NB, n_blk, 16); nb: the number of sets encrypted (a layout that
+        pads the batch -- AESSlicedRound -- returns the padding sets too unless told)."""
         rows = []
         for r in range(4):
             acc = 0
@@ -134,7 +136,7 @@ class AESRowRound:
                 v = np.real(np.atleast_2d(self.e.decrypt(bits[r][j], self.sk)))
                 acc = acc | ((v < 0).astype(np.uint8) << j)
             rows.append(acc)
-        return self.unpack(rows)
+        return self.unpack(rows, nb)
 
     decrypt_bits = decrypt_blocks
 
@@ -147,6 +149,10 @@ class AESRowRound:
     # ---- building blocks ---------------------------------------------------------------------
     def mul(self, a: Ciphertext, b: Ciphertext) -> Ciphertext:
         return self.e.multiply(a, b, self.rlk)
+
+    def key_mul(self, a: Ciphertext, k: Ciphertext) -> Ciphertext:
+        """a XOR (round-key bit k): the key ciphertext is broadcast over the batch (B = 1)."""
+        return self.mul(a, k)
 
     def monomials(self, b4: Sequence[Ciphertext]) -> Dict[int, Ciphertext]:
         """All 15 non-empty products of 4 +-1 bit ciphertexts, keyed by bit mask (depth <= 2:
@@ -197,11 +203,11 @@ class AESRowRound:
         out_rj ^ k_rj = xtime(U_r)_j * (U_{r+1,j} * (a_{r+3,j} * K_rj)): 140 products, depth 3."""
         U = [[self.mul(A[r][j], A[(r + 1) % 4][j]) for j in range(8)] for r in range(4)]
         return [[self.mul(self._xtime_terms(U, r, j),
-                          self.mul(U[(r + 1) % 4][j], self.mul(A[(r + 3) % 4][j], key[r][j])))
+                          self.mul(U[(r + 1) % 4][j], self.key_mul(A[(r + 3) % 4][j], key[r][j])))
                  for j in range(8)] for r in range(4)]
 
     def add_round_key(self, S: List[List[Ciphertext]], key) -> List[List[Ciphertext]]:
-        return [[self.mul(S[r][j], key[r][j]) for j in range(8)] for r in range(4)]
+        return [[self.key_mul(S[r][j], key[r][j]) for j in range(8)] for r in range(4)]
 
     ROUND_DEPTH, FINAL_DEPTH = 7, 5
 
@@ -302,4 +308,112 @@ class AESRowRound:
         t = mark("shift_rows", t, A)
         out = self.mix_columns_add_round_key(A, key)
         mark("mix_columns_add_round_key", t, out)
+        return out
+
+
+class AESSlicedRound(AESRowRound):
+    """Fully sliced bit state: the columns move from the slots into the batch.
+
+    One ciphertext per state row r and bit j, as in AESRowRound, but batch element 4 s + c holds
+    column c of slab s, one AES block per slot (slot_count = 4 n_blk blocks per slab; the
+    external unit stays a set of n_blk blocks, four sets per slab, the last slab zero-padded).
+    Every product, the S-box polynomial, MixColumns and the bootstrap are elementwise over the
+    batch exactly as before; what changes:
+
+    * ShiftRows, out(r, c) = in(r, c + r), becomes a permutation of row r's batch elements
+      (Engine.gather, one copy pass): no automorphism and no key switch, where AESRowRound
+      rotates row r by -r n_blk slots (24 key switches per 8192 blocks, ~9 % of the round's).
+    * The round key differs per column: its ciphertexts carry batch 4 (element c = key byte
+      r + 4c), level-downed to the state's level and repeated over the slabs right before each
+      key product (key_mul), which is evaluated at once so that only one repeated key is alive.
+    * The slabs, not the batch elements, are what may be split across ranks (a slab's four
+      columns must stay together): a shard of the batch is a multiple of 4 elements.
+    """
+
+    def __init__(self, engine: Engine, sk, pk, rlk, cjk=None, rotation_keys=None):
+        super().__init__(engine, sk, pk, rlk, cjk, rotation_keys={})
+
+    # ---- layout -----------------------------------------------------------------------------
+    def slabs(self, nb: int) -> int:
+        return -(-int(nb) // 4)
+
+    def pack(self, blocks: np.ndarray) -> List[np.ndarray]:
+        """(NB, n_blk, 16) bytes -> 4 row arrays (4 S, slot_count), S = ceil(NB / 4) slabs:
+        element 4 s + c, slot k holds byte r + 4c (FIPS order) of block k of slab s (the
+        blocks of sets 4 s .. 4 s + 3 in order)."""
+        b = np.asarray(blocks, dtype=np.uint8)
+        nb, S = b.shape[0], self.slabs(b.shape[0])
+        flat = np.zeros((S * self.sc, 16), dtype=np.uint8)
+        flat[:nb * self.n_blk] = b.reshape(-1, 16)
+        sl = flat.reshape(S, self.sc, 16)
+        return [np.ascontiguousarray(sl[:, :, [r + 4 * c for c in range(4)]].transpose(0, 2, 1)).reshape(4 * S, self.sc)
+                for r in range(4)]
+
+    def unpack(self, rows: Sequence[np.ndarray], nb: int | None = None) -> np.ndarray:
+        S = rows[0].shape[0] // 4
+        out = np.empty((S, self.sc, 16), dtype=np.uint8)
+        for r in range(4):
+            v = np.asarray(rows[r], dtype=np.uint8).reshape(S, 4, self.sc)
+            for c in range(4):
+                out[:, :, r + 4 * c] = v[:, c, :]
+        nb = 4 * S if nb is None else int(nb)
+        return out.reshape(-1, 16)[:nb * self.n_blk].reshape(nb, self.n_blk, 16)
+
+    def encrypt_blocks_device(self, blocks):
+        import torch
+        b = blocks.to(self.e.client_device)
+        nb, S = b.shape[0], self.slabs(b.shape[0])
+        flat = torch.zeros((S * self.sc, 16), dtype=torch.uint8, device=b.device)
+        flat[:nb * self.n_blk] = b.reshape(-1, 16)
+        sl = flat.reshape(S, self.sc, 16)
+        st = []
+        for r in range(4):
+            row = sl[:, :, [r + 4 * c for c in range(4)]].permute(0, 2, 1).reshape(4 * S, self.sc).to(torch.int64)
+            st.append([self.e.encrypt_device(1.0 - 2.0 * ((row >> j) & 1).to(torch.float64), self.pk)
+                       for j in range(8)])
+        return st
+
+    def decrypt_blocks_device(self, bits, nb: int | None = None):
+        import torch
+        S = bits[0][0].batch // 4
+        out = None
+        for r in range(4):
+            acc = None
+            for j in range(8):
+                v = self.e.decrypt_device(bits[r][j], self.sk).real
+                t = (v < 0).to(torch.uint8) << j
+                acc = t if acc is None else acc | t
+            if out is None:
+                out = torch.empty((S, self.sc, 16), dtype=torch.uint8, device=acc.device)
+            v = acc.reshape(S, 4, self.sc)
+            for c in range(4):
+                out[:, :, r + 4 * c] = v[:, c, :]
+        nb = 4 * S if nb is None else int(nb)
+        return out.reshape(-1, 16)[:nb * self.n_blk].reshape(nb, self.n_blk, 16)
+
+    def encrypt_round_key(self, rk: np.ndarray, level: int | None = None) -> List[List[Ciphertext]]:
+        """Key bits as +-1 per (row, column): batch 4, element c = key byte r + 4c."""
+        rk = np.asarray(rk, dtype=np.int64)
+        rows = [np.repeat(rk[[r + 4 * c for c in range(4)]], self.sc).reshape(4, self.sc) for r in range(4)]
+        return self.encrypt_bytes_rows(rows, level=level)
+
+    # ---- round steps --------------------------------------------------------------------------
+    def key_mul(self, a: Ciphertext, k: Ciphertext) -> Ciphertext:
+        """a XOR k: the batch-4 key aligned to a's level (the level-down the product would run)
+        and repeated over a's slabs; the product is evaluated now, so the repeated key is freed
+        before the next one is made."""
+        S = a.batch // 4
+        if k.level > a.level:
+            k = self.e.level_down(k, a.level)
+        if S > 1:
+            k = self.e.gather(k, [c for _ in range(S) for c in range(4)])
+        return Engine.materialize(self.mul(a, k))
+
+    def shift_rows(self, bits):
+        """out(r, c) = in(r, c + r): element 4 s + c of row r takes element 4 s + (c + r) mod 4."""
+        S = bits[0][0].batch // 4
+        out = [bits[0]]
+        for r in (1, 2, 3):
+            idx = [4 * s + (c + r) % 4 for s in range(S) for c in range(4)]
+            out.append([self.e.gather(c, idx) for c in bits[r]])
         return out

@@ -49,8 +49,9 @@ def _urandom64() -> int:
 
 
 def _params_for(log_n=None, max_level=None, special_primes=None, scale_bits=None,
-                base_bits=None, special_bits=None, seed=None, threads=0, device=0):
+                base_bits=None, special_bits=None, seed=None, threads=0, device=0, digit_primes=None):
     p = dict(DEFAULT_PARAMS)
+    p["digit_primes"] = int(digit_primes or 0)  # key-switch digit width alpha (0: = special_primes)
     for k, v in dict(log_n=log_n, max_level=max_level, special_primes=special_primes,
                      scale_bits=scale_bits, base_bits=base_bits, special_bits=special_bits,
                      seed=seed).items():
@@ -74,6 +75,26 @@ def _params_for(log_n=None, max_level=None, special_primes=None, scale_bits=None
     # parallel.shared_seed)
     p["seed"], p["seed_ext"] = s & m, ((s >> 64) & m, (s >> 128) & m, (s >> 192) & m)
     return p
+
+
+def widest_digits(log_n: int, max_level: int, special_primes: int, scale_bits: int,
+                  base_bits: int = 50, special_bits: int = 50, lib: Lib | None = None) -> int:
+    """The widest key-switch digit (aesfhe_params.digit_primes, <= 16 primes) whose product stays
+    below P for this chain (the engines' digits_below_p rule, on the primes aesfhe_chain makes):
+    fewer digits -- fewer extension limbs to convert, transform and multiply per key switch."""
+    import math
+    lib = lib if lib is not None else load_product()
+    L1, K = max_level + 1, special_primes
+    cp = Params(log_n, max_level, special_primes, scale_bits, base_bits, special_bits, 0, 0, 0, None)
+    primes = (C.c_uint64 * (L1 + K))()
+    scales = (C.c_double * L1)()
+    lib.check(lib.chain(C.byref(cp), primes, scales))
+    logp = sum(math.log2(float(primes[L1 + k])) for k in range(K))
+    for a in range(16, K, -1):
+        if all(sum(math.log2(float(primes[i])) for i in range(lo, min(lo + a, L1))) <= logp
+               for lo in range(0, L1, a)):
+            return a
+    return K
 
 
 def _as_ptr(a, ctype):
@@ -300,7 +321,8 @@ class Engine:
 
     ``mode`` is accepted for compatibility; execution is always the HIP engine on
     ``device_id`` (the product has no CPU path).  Extra keyword overrides (``log_n``,
-    ``special_primes``, ``scale_bits``, ``base_bits``, ``special_bits``, ``seed``) select explicit parameters; ``_lib`` injects
+    ``special_primes``, ``scale_bits``, ``base_bits``, ``special_bits``, ``seed``, ``digit_primes``
+    -- the key-switch digit width alpha, default K) select explicit parameters; ``_lib`` injects
     another implementation of the ABI (tests use it for the CPU oracle).
 
     ``fuse_linear`` (default True): ``multiply(ct, constant)`` and the ``add`` calls that consume
@@ -323,7 +345,7 @@ class Engine:
                  special_primes: int | None = None, scale_bits: int | None = None,
                  base_bits: int | None = None, special_bits: int | None = None,
                  seed: int | bytes | None = None, nonce_start: int | None = None,
-                 fuse_linear: bool = True, _lib: Lib | None = None):
+                 fuse_linear: bool = True, digit_primes: int | None = None, _lib: Lib | None = None):
         ints = [a for a in args if isinstance(a, (int, np.integer)) and not isinstance(a, bool)]
         strs = [a for a in args if isinstance(a, str)]
         if strs:
@@ -341,11 +363,11 @@ class Engine:
                 // DEFAULT_PARAMS["scale_bits"])
             p = _params_for(log_n=log_n or ln, max_level=lvl, special_primes=special_primes or k,
                             scale_bits=scale_bits, base_bits=base_bits, special_bits=special_bits,
-                            seed=seed, threads=thread_count, device=device_id)
+                            seed=seed, threads=thread_count, device=device_id, digit_primes=digit_primes)
         else:                                    # signatures 1 and 2
             p = _params_for(log_n=log_n, max_level=max_level, special_primes=special_primes,
                             scale_bits=scale_bits, base_bits=base_bits, special_bits=special_bits,
-                            seed=seed, threads=thread_count, device=device_id)
+                            seed=seed, threads=thread_count, device=device_id, digit_primes=digit_primes)
         self.mode = mode
         self.use_bootstrap = use_bootstrap
         self.use_multiparty = use_multiparty
@@ -355,13 +377,15 @@ class Engine:
         self._params = p
         cp = Params(p["log_n"], p["max_level"], p["special_primes"], p["scale_bits"],
                     p["base_bits"], p["special_bits"], p["device"], p["threads"], p["seed"], None,
-                    (C.c_uint64 * 3)(*p["seed_ext"]))
+                    (C.c_uint64 * 3)(*p["seed_ext"]), p["digit_primes"])
         h = C.c_void_p()
         self._check(self._lib.engine_create(C.byref(cp), C.byref(h)))
         self._h = h.value
         dims = (C.c_int32 * 4)()
         self._lib.engine_dims(self._h, dims)
         self.log_coeff_count, self.max_level, self.special_prime_count, self.dnum = list(dims)
+        # key-switch digit width alpha (aesfhe_params.digit_primes; 0 selects K)
+        self.digit_primes = p["digit_primes"] or self.special_prime_count
         self.slot_count = 1 << (self.log_coeff_count - 1)
         np_ = self.max_level + 1 + self.special_prime_count
         primes = (C.c_uint64 * np_)()
@@ -854,6 +878,12 @@ class Engine:
     def slice(self, ct: Ciphertext, start: int, count: int) -> Ciphertext:
         return self._call_ct(self._lib.ct_slice, ct._h, start, count)
 
+    def gather(self, ct: Ciphertext, idx: Sequence[int]) -> Ciphertext:
+        """Batch permutation / repetition: element b of the result is element idx[b] of ct
+        (aesfhe_ct_gather, one copy pass)."""
+        arr = (C.c_int32 * len(idx))(*[int(i) for i in idx])
+        return self._call_ct(self._lib.ct_gather, ct._h, arr, len(idx))
+
     def export_residues(self, ct: Ciphertext) -> np.ndarray:
         n = 1 << self.log_coeff_count
         out = np.empty((ct.batch, ct.npoly, ct.level + 1, n), dtype=np.uint64)
@@ -947,12 +977,18 @@ class Engine:
         ranks before moving ciphertexts between them)."""
         import hashlib
         p = self._params
-        h = hashlib.sha256(repr((p["seed"], tuple(p["seed_ext"]), tuple(self.primes))).encode()).digest()
+        ident = (p["seed"], tuple(p["seed_ext"]), tuple(self.primes))
+        if self.digit_primes != self.special_prime_count:  # another key layout (digits)
+            ident += (self.digit_primes,)
+        h = hashlib.sha256(repr(ident).encode()).digest()
         return int.from_bytes(h[:8], "little") >> 1
 
     def _fingerprint(self) -> dict:
-        return {"log_n": self.log_coeff_count, "max_level": self.max_level,
-                "special_primes": self.special_prime_count, "primes": self.primes}
+        fp = {"log_n": self.log_coeff_count, "max_level": self.max_level,
+              "special_primes": self.special_prime_count, "primes": self.primes}
+        if self.digit_primes != self.special_prime_count:  # keys of another digit layout
+            fp["digit_primes"] = self.digit_primes
+        return fp
 
     def save(self, obj, path) -> None:
         """Write a Ciphertext or key (SecretKey, PublicKey, RelinearizationKey, GaloisKey and

@@ -148,6 +148,22 @@ struct Chain {
     std::vector<double> scale;  // Delta_0..Delta_L
 };
 
+// Hybrid key switching keeps its error small only while every digit's modulus Q_j stays below
+// P (the ModDown divides the digit's inner-product error by P): digits of A primes of q (chain q_0
+// .. q_{Lp1-1}, then the K special primes) checked by their bit sizes.  Applied to digits wider
+// than K (aesfhe_params.digit_primes > K); the default digits of K primes are accepted as before.
+// The oracle applies the same rule (ckks_oracle.c digits_below_p).
+inline bool digits_below_p(const std::vector<uint64_t>& q, int Lp1, int K, int A) {
+    double logp = 0.0;
+    for (int k = 0; k < K; k++) logp += std::log2((double)q[Lp1 + k]);
+    for (int lo = 0; lo < Lp1; lo += A) {
+        double lq = 0.0;
+        for (int i = lo; i < lo + A && i < Lp1; i++) lq += std::log2((double)q[i]);
+        if (lq > logp) return false;
+    }
+    return true;
+}
+
 inline Chain make_chain(int logN, int L, int K, int base_bits, int special_bits, int scale_bits) {
     const u64 M = 2ULL << logN;
     Chain c;

@@ -125,7 +125,7 @@ struct aesfhe_engine {
     // stream outlive aesfhe_engine_destroy until the last object is freed (Python's cycle
     // collector finalises an engine and its ciphertexts in arbitrary order)
     std::atomic<int> refs{1};
-    int logN, N, L, K, dnum, np, Lp1;
+    int logN, N, L, K, A, dnum, np, Lp1;  // A: key-switch digit width (alpha)
     int device;
     u64 seed;
     ChaKey ck;  // ChaCha20 key of every random stream
@@ -569,31 +569,32 @@ static void build_tables(aesfhe_engine* e) {
         up(hitw, &e->itw);
     }
 
-    // ModUp tables per (digit j, alpha a): hatinv[i], hat[i][pid]
-    const size_t mu_sets = (size_t)e->dnum * K;
-    std::vector<u64> hhatinv(mu_sets * K, 0), hhat(mu_sets * K * np, 0);
-    std::vector<double> hhatinvf(mu_sets * K, 0);
-    std::vector<TwD> hhatf(mu_sets * K * np, TwD{0, 0});
+    // ModUp tables per (digit j, width a <= alpha): hatinv[i], hat[i][pid]; stride A = alpha
+    const int A = e->A;
+    const size_t mu_sets = (size_t)e->dnum * A;
+    std::vector<u64> hhatinv(mu_sets * A, 0), hhat(mu_sets * A * np, 0);
+    std::vector<double> hhatinvf(mu_sets * A, 0);
+    std::vector<TwD> hhatf(mu_sets * A * np, TwD{0, 0});
     for (int j = 0; j < e->dnum; j++)
-        for (int a = 1; a <= K; a++) {
-            int lo = j * K, hi = lo + a;
+        for (int a = 1; a <= A; a++) {
+            int lo = j * A, hi = lo + a;
             if (hi > Lp1) continue;
-            size_t set = (size_t)j * K + (a - 1);
+            size_t set = (size_t)j * A + (a - 1);
             for (int i = lo; i < hi; i++) {
                 u64 prod = 1;
                 for (int i2 = lo; i2 < hi; i2++)
                     if (i2 != i) prod = h_mulmod(prod, Q[i2] % Q[i], Q[i]);
                 u64 hv = h_invmod(prod, Q[i]);
-                hhatinv[set * K + (i - lo)] = hv;
-                hhatinvf[set * K + (i - lo)] = (double)hv / (double)Q[i];
+                hhatinv[set * A + (i - lo)] = hv;
+                hhatinvf[set * A + (i - lo)] = (double)hv / (double)Q[i];
                 for (int pid = 0; pid < np; pid++) {
                     u64 qt = Q[pid], h = 1;
                     for (int i2 = lo; i2 < hi; i2++)
                         if (i2 != i) h = h_mulmod(h, Q[i2] % qt, qt);
-                    hhat[(set * K + (i - lo)) * np + pid] = h;
+                    hhat[(set * A + (i - lo)) * np + pid] = h;
                     // [set][target pid][i]: a target's alpha constants are contiguous (one
                     // scalar base, immediate offsets in k_modup)
-                    hhatf[(set * np + pid) * K + (i - lo)] = TwD{(double)h, (double)h / (double)qt};
+                    hhatf[(set * np + pid) * A + (i - lo)] = TwD{(double)h, (double)h / (double)qt};
                 }
             }
         }
@@ -722,7 +723,9 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
     e->K = pp->special_primes;
     e->Lp1 = e->L + 1;
     e->np = e->L + 1 + e->K;
-    e->dnum = (e->L + 1 + e->K - 1) / e->K;
+    e->A = pp->digit_primes > 0 ? pp->digit_primes : e->K;
+    if (e->A > 16) throw_err(AESFHE_EARG, "key-switch digit width %d outside 1..16", e->A);
+    e->dnum = (e->L + 1 + e->A - 1) / e->A;
     e->device = pp->device;
     e->seed = pp->seed;
     e->ck = chacha_key(pp->seed, pp->seed_ext);
@@ -734,6 +737,8 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
     }
     for (u64 x : e->chain.q)  // lazy NTT keeps values < 4q, which must stay below 2^52
         if (x >> 50) throw_err(AESFHE_EARG, "prime %llu exceeds 2^50", (unsigned long long)x);
+    if (e->A > e->K && !digits_below_p(e->chain.q, e->Lp1, e->K, e->A))
+        throw_err(AESFHE_EARG, "a key-switch digit of %d primes exceeds P (%d special primes)", e->A, e->K);
     HIPC(hipSetDevice(e->device));
     HIPC(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     build_tables(e.get());
@@ -1007,7 +1012,7 @@ static aesfhe_key* make_ksk_t(aesfhe_engine* e, const u64* starget, u64 keyseed,
         Span sa = span_s(ka, 0, np, e->Lp1, 0, e->Lp1);
         hipLaunchKernelGGL(k_sample_uniform, dim3((N / 8 + 255) / 256, np), dim3(256), 0, e->stream, sa, e->ck, derive(base, 2 * (u64)d), e->q, e->logN, e->Lp1);
         sample_small_ntt(e, et.p, np, derive(base, 2 * (u64)d + 1), 1);
-        int lo = d * e->K, hi = std::min(lo + e->K, e->Lp1);
+        int lo = d * e->A, hi = std::min(lo + e->A, e->Lp1);
         hipLaunchKernelGGL(k_key_combine, dim3(N / 256, np), dim3(256), 0, e->stream, (const u64*)ka, starget, et.p, sprime, e->pmod, lo, hi, kb, e->q, e->qinv, e->logN);
     }
     HIPC(hipGetLastError());
@@ -1222,6 +1227,24 @@ extern "C" int aesfhe_ct_concat(aesfhe_engine* e, const aesfhe_ct* const* parts,
         off += parts[i]->bytes;
     }
     r->is_zero = allz;
+    *out = r;
+    API_END
+}
+extern "C" int aesfhe_ct_gather(aesfhe_engine* e, const aesfhe_ct* c, const int32_t* idx, int32_t n, aesfhe_ct** out) {
+    API_BEGIN
+    if (n < 1 || !idx) throw_err(AESFHE_EARG, "empty gather");
+    for (int b = 0; b < n; b++)
+        if (idx[b] < 0 || idx[b] >= c->B) throw_err(AESFHE_EARG, "gather index out of range");
+    aesfhe_ct* r = ct_new(e, n, c->np, c->level);
+    const long per = (long)(c->bytes / c->B / 8);  // np * (level + 1) * N words
+    const int* di = upload_small(e, (const int*)idx, (size_t)n);
+    const long blocks = std::min<long>(per / 512, 256);
+    {
+        ProfScope ps(e, FAM_EW, 2.0 * 8.0 * per * n, "gather");
+        hipLaunchKernelGGL(k_gather_batch, dim3((unsigned)std::max<long>(blocks, 1), n), dim3(256), 0, e->stream,
+                           (const u64*)c->d, r->d, di, per);
+    }
+    r->is_zero = c->is_zero;
     *out = r;
     API_END
 }
@@ -1881,7 +1904,7 @@ static unsigned bconv_groups(int N, int P, int ntarget) {
 }
 
 static int ks_beta(const aesfhe_engine* e, int l) {
-    const int beta = (l + 1 + e->K - 1) / e->K;
+    const int beta = (l + 1 + e->A - 1) / e->A;
     if (beta > 12) throw_err(AESFHE_EUNSUPPORTED, "more than 12 key-switch digits");
     return beta;
 }
@@ -1908,8 +1931,8 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         ntt(e, sd, sdc, B * (l + 1), true);
     }
     for (int j = 0; j < beta; j++) {
-        const int lo = j * K, hi = std::min(lo + K, l + 1), alpha = hi - lo;
-        const size_t set = (size_t)j * K + (alpha - 1);
+        const int A = e->A, lo = j * A, hi = std::min(lo + A, l + 1), alpha = hi - lo;
+        const size_t set = (size_t)j * A + (alpha - 1);
         u64* exj = ext + (size_t)j * B * neN;
         if (cols_only && alpha == 1) {
             // one-limb digit: the conversion is x mod p_t (hat = hatinv = 1), formed in the column
@@ -1930,8 +1953,8 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne, "modup");
             if (alpha < 1 || alpha > 16) throw_err(AESFHE_EUNSUPPORTED, "ModUp digit width outside 1..16");
             AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, bconv_groups(N, B, ne), B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
-                              (const double*)(e->mu_hatinvf + set * K), (const TwD*)(e->mu_hatf + set * K * e->np),
-                              K, e->q, e->qinv, e->Lp1, e->logN);
+                              (const double*)(e->mu_hatinvf + set * A), (const TwD*)(e->mu_hatf + set * A * e->np),
+                              A, e->q, e->qinv, e->Lp1, e->logN);
         }
         HIPC(hipGetLastError());
         auto fwd = [&](Span sp, int total) {
@@ -1969,7 +1992,7 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
         // row pass of every extension limb (credited half an NTT per limb: 8 N B) + the inner product
         // (key read once per call, accumulators written; ext never leaves the chip) + the Q-limb
         // operands: the own digit's d limbs and the addend (PROD: a0, a1, b0, b1)
-        const int nown = std::min(l + 1, beta * K);
+        const int nown = std::min(l + 1, beta * e->A);
         const double opw = pb ? (4.0 + (pc && pc->ptr ? 2.0 : 0.0)) * (l + 1)
                               : (double)nown + (pmod && addend.ptr ? (double)addend.np * (l + 1) : 0.0);
         ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown + opw) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))), "ks_rows_inner");
@@ -1977,11 +2000,11 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
         const Opnd none{nullptr, 0, 0, 0};
         auto kern = pb ? (R == 256 ? k_nttf_rows_ks<1, 256, true> : k_nttf_rows_ks<1, 512, true>)
                        : (R == 256 ? k_nttf_rows_ks<1, 256, false> : k_nttf_rows_ks<1, 512, false>);
-        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, ne, e->tabs(), addend, pm, (int)accum, pb ? *pb : none, fac, pc ? *pc : none);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, e->A, l, ne, e->tabs(), addend, pm, (int)accum, pb ? *pb : none, fac, pc ? *pc : none);
     } else {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B * (accum ? 2 : 1)), "ks_inner");
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
-        hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, K, l, e->q, e->qinv, e->Lp1, addend, pm, e->logN, (int)accum);
+        hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, e->A, l, e->q, e->qinv, e->Lp1, addend, pm, e->logN, (int)accum);
     }
     HIPC(hipGetLastError());
 }
@@ -2369,7 +2392,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             auto dko = upload_small(e, ko.data(), ko.size());
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + kd.size() * (2.0 * beta + 2.0 * B)), "ks_inner_multi");
             auto inner = beta <= 4 ? k_ks_inner_multi<4, 4> : beta <= 8 ? k_ks_inner_multi<8, 2> : k_ks_inner_multi<12, 1>;
-            hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, c1, cv.bs, (const u64*)ext->p, neN, (long)B * neN, (const u64* const*)dk, (int)kd.size(), 2L * e->np * N, (long)e->np * N, (u64* const*)dko, 2 * neN, neN, B, beta, e->K, l, e->q, e->qinv, e->Lp1, c0, (const double*)e->pmodf, e->logN);
+            hipLaunchKernelGGL(inner, dim3(N / 256, ne, 1), dim3(256), 0, e->stream, c1, cv.bs, (const u64*)ext->p, neN, (long)B * neN, (const u64* const*)dk, (int)kd.size(), 2L * e->np * N, (long)e->np * N, (u64* const*)dko, 2 * neN, neN, B, beta, e->A, l, e->q, e->qinv, e->Lp1, c0, (const double*)e->pmodf, e->logN);
             HIPC(hipGetLastError());
         }
     }

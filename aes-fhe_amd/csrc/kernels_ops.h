@@ -47,6 +47,18 @@ __global__ void k_addsub(Opnd a, Opnd b, Out o, int np, const u64* __restrict__ 
     o.ptr[(long)bb * o.bs + (long)p * o.ps + ((long)l << logN) + k] = sub ? sub_m(va, vb, q) : add_m(va, vb, q);
 }
 
+// Batch gather (aesfhe_ct_gather): element b of dst = element idx[b] of src, `per` words each
+// (a multiple of 2 * 256).  grid (x, n): 16 B per lane per step, grid-stride over the element.
+__global__ void k_gather_batch(const u64* __restrict__ src, u64* __restrict__ dst,
+                               const int* __restrict__ idx, long per) {
+    const int b = blockIdx.y;
+    const ulonglong2* s = (const ulonglong2*)(src + (long)idx[b] * per);
+    ulonglong2* o = (ulonglong2*)(dst + (long)b * per);
+    const long nv = per >> 1;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x)
+        o[i] = s[i];
+}
+
 // Constant factors for x * (A + B X^{N/2}): f[2*l] for k < N/2, f[2*l+1] for k >= N/2.
 // out (+)= in * f ; grid (N/256, nl, B*np)
 __global__ void k_mul_const(Opnd in, Out o, int np, const u64* __restrict__ f,

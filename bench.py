@@ -5,9 +5,12 @@
                     [--no-cpu-baseline] [--cpu-extended] [--no-configs] [--aes10-batch S]
 
 One *step* = one full middle AES-128 round (ShiftRows -> SubBytes -> MixColumns ->
-AddRoundKey) at N = 2^16, L = 30 over a batch of B ciphertext sets per GPU.  Default layout
-"rows" (aes_xor_fhe.aes_round_bits.AESRowRound): a set is 4 state rows x 8 +-1 bit ciphertexts
-carrying 8192 AES blocks; layout "bytes" (aes_xor_fhe.aes_round.AESRoundEngine): a set is one
+AddRoundKey) at N = 2^16, L = 30 over a batch of B ciphertext sets (8192 blocks each) per GPU.
+Default layout "sliced" (aes_xor_fhe.aes_round_bits.AESSlicedRound): 4 state rows x 8 +-1 bit
+ciphertexts of batch B, the 4 state columns of a slab of 4 sets as batch elements (one block
+per slot), so ShiftRows is a batch permutation; layout "rows" (AESRowRound): a set is 4 state
+rows x 8 +-1 bit ciphertexts carrying 8192 blocks, the columns in slot quarters and ShiftRows
+three rotations per bit; layout "bytes" (aes_xor_fhe.aes_round.AESRoundEngine): a set is one
 byte-major (hi, lo) Zeta-16 nibble pair carrying 2048 blocks.  Inputs (encrypted synthetic
 random AES states) and the encrypted round key are resident in HBM before the timed region.
 The timed steps run with kernel profiling OFF; a separate profiled pass afterwards gives the
@@ -52,6 +55,14 @@ sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
 COPY_HBM_GBS = 6290.0  # measured float4 copy on MI355X (MI355X_MICROARCH.md), for context only
 PEAK_HBM_GBS = 8000.0
 METRIC = "AES-128 blocks/sec (homomorphic full round) at N=2^16, L=30; 1/2/4/8 MI355X"
+WORKLOAD = {
+    "sliced": ("fully sliced +-1 bit state (one ciphertext per row and bit, the 4 columns as batch "
+               "elements, one block per slot), ShiftRows as a batch permutation, S-box as Walsh "
+               "polynomial over nibble-bit monomials, bit-domain MixColumns/AddRoundKey"),
+    "rows": ("row-sliced +-1 bit state (columns in slot quarters), ShiftRows by rotations, S-box as "
+             "Walsh polynomial over nibble-bit monomials, bit-domain MixColumns/AddRoundKey"),
+    "bytes": "nibble-domain Zeta-16 LUTs, byte-major SIMD packing",
+}
 SEED = 0x5EED5EED  # the CPU baseline's engine (reproducible); the GPU ranks share a 256-bit seed
 
 PEAK_FP64_TFLOPS = 78.6  # MI355X vector FP64 (AMD spec: 256 CUs x 128 FLOP/clk x 2.4 GHz)
@@ -72,13 +83,14 @@ def log(msg):
 
 def pmc_record(args=None):
     """The committed PMC measurement of one round step (None if absent); with args, only when it
-    measured this run's workload shape (N, L, K, sets per GPU, layout)."""
+    measured this run's workload shape (N, L, K, alpha, sets per GPU, layout)."""
     try:
         rec = json.loads(PMC_FILE.read_text())
     except (OSError, ValueError):
         return None
     if args is not None and rec.get("workload") != {"log_n": args.log_n, "max_level": args.max_level,
                                                      "special_primes": args.special_primes,
+                                                     "digit_primes": digit_primes(args),
                                                      "batch": args.batch, "layout": args.layout}:
         return None
     return rec
@@ -123,11 +135,17 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32, help="ciphertext sets per GPU per step (8192 blocks each)")
-    ap.add_argument("--layout", choices=("rows", "bytes"), default="rows")
+    ap.add_argument("--layout", choices=("sliced", "rows", "bytes"), default="sliced",
+                    help="sliced: columns as batch elements, ShiftRows a batch permutation "
+                         "(AESSlicedRound); rows: columns in slot quarters, ShiftRows by rotations "
+                         "(AESRowRound); bytes: byte-major nibble round (AESRoundEngine)")
     ap.add_argument("--log-n", type=int, default=16)
     ap.add_argument("--max-level", type=int, default=30)
     ap.add_argument("--special-primes", type=int, default=10,
                     help="K special primes = key-switch digit size alpha (dnum = ceil((L+1)/K))")
+    ap.add_argument("--digit-primes", type=int, default=-1,
+                    help="primes per key-switch digit alpha (-1: the widest whose product stays below P "
+                         "-- 12 at the default chain, dnum 3 at levels 24..30; 0: = K)")
     ap.add_argument("--scale-bits", type=int, default=40,
                     help="log2 of the top-level scale (config 5, N=2^17 L=35: 44)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -161,6 +179,9 @@ class RoundDriver:
         if layout == "rows":
             from aes_xor_fhe.aes_round_bits import AESRowRound
             self.R = AESRowRound(eng, sk, pk, rlk, cjk, rotation_keys=rotation_keys)
+        elif layout == "sliced":
+            from aes_xor_fhe.aes_round_bits import AESSlicedRound
+            self.R = AESSlicedRound(eng, sk, pk, rlk, cjk)
         else:
             from aes_xor_fhe.aes_round import AESRoundEngine
             self.R = AESRoundEngine(eng, sk, pk, rlk, cjk, rotation_keys=rotation_keys)
@@ -169,23 +190,32 @@ class RoundDriver:
 
     def encrypt(self, blocks):
         st = self.R.encrypt_blocks(blocks)
-        return st if self.layout == "rows" else tuple(st)
+        return tuple(st) if self.layout == "bytes" else st
 
     def key(self, rk):
         return self.R.encrypt_round_key(rk)
 
     def round(self, st, key):
-        return self.R.round(st, key) if self.layout == "rows" else self.R.round(st[0], st[1], key)
+        return self.R.round(st[0], st[1], key) if self.layout == "bytes" else self.R.round(st, key)
 
-    def decrypt(self, st):
-        return self.R.decrypt_blocks(st) if self.layout == "rows" else self.R.decrypt_blocks(*st)
+    def decrypt(self, st, nb=None):
+        """The blocks of the state (nb: the sets encrypted; the sliced layout pads to slabs of 4)."""
+        return self.R.decrypt_blocks(*st) if self.layout == "bytes" else self.R.decrypt_blocks(st, nb)
 
     def cts(self, st):
         """The state's ciphertexts, flat (for scatter / gather)."""
-        return [c for row in st for c in row] if self.layout == "rows" else list(st)
+        return list(st) if self.layout == "bytes" else [c for row in st for c in row]
 
     def from_cts(self, cts):
-        return [cts[8 * r:8 * r + 8] for r in range(4)] if self.layout == "rows" else tuple(cts)
+        return tuple(cts) if self.layout == "bytes" else [cts[8 * r:8 * r + 8] for r in range(4)]
+
+
+def digit_primes(args, lib=None):
+    """--digit-primes resolved for this chain (-1: fhe.widest_digits)."""
+    if args.digit_primes >= 0:
+        return args.digit_primes
+    from aes_xor_fhe.fhe import widest_digits
+    return widest_digits(args.log_n, args.max_level, args.special_primes, args.scale_bits, lib=lib)
 
 
 def setup_engine(args, device, rank):
@@ -194,7 +224,7 @@ def setup_engine(args, device, rank):
     # one 256-bit engine key drawn on rank 0 and broadcast: every rank derives the same keys
     eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes,
                  scale_bits=args.scale_bits, device_id=device, seed=shared_seed(),
-                 nonce_start=rank_nonce_start(rank))
+                 nonce_start=rank_nonce_start(rank), digit_primes=digit_primes(args))
     sk = eng.create_secret_key(1)
     pk = eng.create_public_key(sk)
     rlk = eng.create_relinearization_key(sk)
@@ -205,8 +235,8 @@ def setup_engine(args, device, rank):
 
 
 def aes128_full(args, eng, drv, rank, barrier, allmax):
-    """Full AES-128 (ARK0 + 10 rounds, FIPS-197 5.1) with bit-mode bootstrapping on the rows
-    layout: a warm-up encryption of the same shape (bootstrap plaintexts, device pool), then one
+    """Full AES-128 (ARK0 + 10 rounds, FIPS-197 5.1) with bit-mode bootstrapping on the bit
+    layouts (sliced / rows): a warm-up encryption of the same shape (bootstrap plaintexts, device pool), then one
     timed encryption of args.aes10_batch ciphertext sets (x 8192 blocks at N = 2^16)."""
     from aes_xor_fhe import aes_tables as T
     from aes_xor_fhe.bootstrap import Bootstrapper
@@ -249,7 +279,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     timed_mallocs = eng.pool_stats()["mallocs"] - m0
     ok = None
     if args.check:
-        got = R.decrypt_blocks(out)
+        got = R.decrypt_blocks(out, nb)
         want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
         ok = bool(np.array_equal(got, want))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -418,7 +448,7 @@ def client_path_leg(args, eng, drv, key):
         _materialize([c for row in out for c in row])
         eng.synchronize()
         t2 = time.perf_counter()
-        got = R.decrypt_blocks_device(out).cpu().numpy()
+        got = R.decrypt_blocks_device(out, nb).cpu().numpy()
         t3 = time.perf_counter()
         return got, (t0, t1, t2, t3)
 
@@ -441,8 +471,11 @@ def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
     from aes_xor_fhe import aes_tables as T
     from aes_xor_fhe.parallel import gather_ciphertext, scatter_ciphertext
     rk = np.random.default_rng(31).integers(0, 256, 16, dtype=np.uint8)
-    blocks = np.random.default_rng(77).integers(0, 256, (world, drv.n_blk, 16), dtype=np.uint8)
-    cts = drv.cts(drv.encrypt(blocks)) if rank == 0 else [None] * (32 if drv.layout == "rows" else 2)
+    # one set per rank (sliced layout: one slab = 4 sets per rank, its columns stay together)
+    per_rank = 4 if drv.layout == "sliced" else 1
+    nsets = per_rank * world
+    blocks = np.random.default_rng(77).integers(0, 256, (nsets, drv.n_blk, 16), dtype=np.uint8)
+    cts = drv.cts(drv.encrypt(blocks)) if rank == 0 else [None] * (2 if drv.layout == "bytes" else 32)
     key = drv.key(rk)
     # untimed warm-up: the first RCCL collective sets up the communicator (hundreds of ms), which
     # is not part of the data path's rate
@@ -464,8 +497,8 @@ def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
     t_ga = allmax(time.perf_counter() - t0)
     ok = None
     if rank == 0 and args.check:
-        ok = bool((drv.decrypt(drv.from_cts(full)) == T.aes_round(blocks, rk)).all())
-    return {"sets": world, "bytes_per_rank_in": bytes_in, "scatter_ms": round(t_sc * 1e3, 2),
+        ok = bool(np.array_equal(drv.decrypt(drv.from_cts(full), nsets), T.aes_round(blocks, rk)))
+    return {"sets": nsets, "bytes_per_rank_in": bytes_in, "scatter_ms": round(t_sc * 1e3, 2),
             "gather_ms": round(t_ga * 1e3, 2),
             "scatter_gbs_per_rank": round(bytes_in / t_sc / 1e9, 2) if t_sc else None,
             "verified": ok, "backend": _dist_backend(),
@@ -519,12 +552,17 @@ def cpu_baseline(args):
     # grants a share of its CPUs (OMP_NUM_THREADS, 16 per GPU) while os.cpu_count() reports the
     # whole machine (256): more threads than the share only oversubscribe it.
     threads = host_cores()
+    # the sliced layout's unit is a slab of 4 sets (a 4x longer CPU run); its per-block work is
+    # the rows layout's minus ShiftRows' rotations, so the CPU runs the rows layout on one set
+    layout = "rows" if args.layout == "sliced" else args.layout
+    eng_digits = digit_primes(args, lib)
 
     def round_time(nthr):
         eng = Engine(log_n=args.log_n, max_level=args.max_level, special_primes=args.special_primes,
-                     scale_bits=args.scale_bits, thread_count=nthr, seed=SEED, _lib=lib)
+                     scale_bits=args.scale_bits, thread_count=nthr, seed=SEED, _lib=lib,
+                     digit_primes=eng_digits)
         sk = eng.create_secret_key(1)
-        R = RoundDriver(args.layout, eng, sk, eng.create_public_key(sk), eng.create_relinearization_key(sk),
+        R = RoundDriver(layout, eng, sk, eng.create_public_key(sk), eng.create_relinearization_key(sk),
                         eng.create_conjugation_key(sk))
         rng = np.random.default_rng(5)
         blocks = rng.integers(0, 256, (1, R.n_blk, 16), dtype=np.uint8)
@@ -534,7 +572,7 @@ def cpu_baseline(args):
         out = R.round(st, key)
         _materialize(R.cts(out))
         t = time.perf_counter() - t0
-        ok = bool((R.decrypt(out) == T.aes_round(blocks, rk)).all())
+        ok = bool(np.array_equal(R.decrypt(out, 1), T.aes_round(blocks, rk)))
         return R.n_blk, t, ok
 
     log(f"cpu baseline: oracle round at {threads} threads")
@@ -543,8 +581,9 @@ def cpu_baseline(args):
            "measured": True, "verified": ok, "os_cpu_count": os.cpu_count(), "cpu_model": _cpu_model(),
            "cores_note": "all CPUs this process may use (affinity set capped by OMP_NUM_THREADS, the box's share)",
            "sample": (f"oracle (oracle/ckks_oracle.c, gcc -O2, OpenMP over limbs, {threads} threads) "
-                      f"timing one full middle AES-128 round ({args.layout} layout) of one set = "
-                      f"{n_blk} blocks at N=2^{args.log_n}, L={args.max_level}, K={args.special_primes}: "
+                      f"timing one full middle AES-128 round ({layout} layout) of one set = "
+                      f"{n_blk} blocks at N=2^{args.log_n}, L={args.max_level}, K={args.special_primes}, "
+                      f"alpha={eng_digits}: "
                       f"{t:.1f} s, FIPS-verified")}
     log("cpu baseline: oracle round at 8 threads (the reference's thread_count default)")
     _, t8, ok8 = round_time(8)
@@ -674,7 +713,7 @@ def main():
     round_pool = eng.pool_stats()
     ok = None
     if args.check:
-        ok = bool((R.decrypt(out) == T.aes_round(blocks, rk)).all())
+        ok = bool(np.array_equal(R.decrypt(out, args.batch), T.aes_round(blocks, rk)))
         if dist is not None:
             ok = allmax(0.0 if ok else 1.0) == 0.0
 
@@ -731,12 +770,12 @@ def main():
             configs["reference_harness"] = secondary("reference harness", lambda: reference_harness_leg(args))
             log("reference harness leg done")
     client = None
-    if world == 1 and args.client_batch > 0 and args.layout == "rows":
+    if world == 1 and args.client_batch > 0 and args.layout != "bytes":
         client = secondary("client path", lambda: client_path_leg(args, eng, R, key))
         log("client path leg done")
     aes10 = None
     log("config legs done" if configs else "no config legs")
-    if args.aes10_batch > 0 and args.layout == "rows":
+    if args.aes10_batch > 0 and args.layout != "bytes":
         aes10 = secondary("aes10", lambda: aes128_full(args, eng, R, rank, barrier, allmax))
 
     blocks_per_step = args.batch * R.n_blk * world
@@ -765,12 +804,10 @@ def main():
             "data": "synthetic random AES states + random round key, encrypted",
             "config": {
                 "workload": ("one full AES-128 middle round (ShiftRows+SubBytes+MixColumns+"
-                             "AddRoundKey): " + ("row-sliced +-1 bit state, S-box as Walsh "
-                             "polynomial over nibble-bit monomials, bit-domain MixColumns/AddRoundKey" if args.layout == "rows"
-                             else "nibble-domain Zeta-16 LUTs, byte-major SIMD packing")),
+                             "AddRoundKey): " + WORKLOAD[args.layout]),
                 "layout": args.layout,
                 "log_n": args.log_n, "max_level": args.max_level, "special_primes": args.special_primes,
-                "scale_bits": args.scale_bits,
+                "digit_primes": eng.digit_primes, "dnum": eng.dnum, "scale_bits": args.scale_bits,
                 "ciphertext_sets_per_gpu": args.batch, "blocks_per_gpu_per_step": args.batch * R.n_blk,
                 "parallelism": f"ciphertext-batch sharding x{world} (no data-path collective)",
                 "verified": ok, "pool_after_round": round_pool,

@@ -76,7 +76,7 @@ typedef struct aesfhe_key aesfhe_key;
 typedef struct aesfhe_params {
     int32_t log_n;          /* log2 of the ring degree N (slots = N/2) */
     int32_t max_level;      /* L: the ciphertext modulus chain has L+1 primes q_0..q_L */
-    int32_t special_primes; /* K = alpha: special primes p_0..p_{K-1}; dnum = ceil((L+1)/K) */
+    int32_t special_primes; /* K: special primes p_0..p_{K-1} (P = their product) */
     int32_t scale_bits;     /* log2 of the top-level scale Delta_L */
     int32_t base_bits;      /* bit size of q_0 */
     int32_t special_bits;   /* bit size of the special primes */
@@ -86,6 +86,9 @@ typedef struct aesfhe_params {
     const uint64_t *primes; /* optional explicit chain q_0..q_L,p_0..p_{K-1} (NULL = generate) */
     uint64_t seed_ext[3];   /* with seed: the 256-bit ChaCha20 key of every random stream
                                (seed, ext[0], ext[1], ext[2]); zeros for a reproducible 64-bit seed */
+    int32_t digit_primes;   /* alpha: primes per key-switch digit, 1..16 (0 = K); digit j covers
+                               q_{j alpha} .. q_{j alpha + alpha - 1}, dnum = ceil((L+1)/alpha).
+                               alpha > K is allowed while a digit's product stays below P */
 } aesfhe_params;
 
 /* ---- diagnostics ---------------------------------------------------------------------- */
@@ -225,6 +228,13 @@ int aesfhe_ct_copy(aesfhe_engine *eng, const aesfhe_ct *ct, aesfhe_ct **out);
 int aesfhe_ct_slice(aesfhe_engine *eng, const aesfhe_ct *ct, int32_t start, int32_t count,
                     aesfhe_ct **out);
 int aesfhe_ct_concat(aesfhe_engine *eng, const aesfhe_ct *const *parts, int32_t n,
+                     aesfhe_ct **out);
+/* batch permutation / repetition: element b of the result (batch n) is element idx[b] of ct
+ * (0 <= idx[b] < batch).  One copy pass.  The fully sliced AES state (aes_round_bits
+ * AESSlicedRound) carries the state columns as batch elements, so ShiftRows -- a rotation in
+ * the reference's slot layouts (shiftrows_service.py:33-51) -- is this permutation, and a round
+ * key held once per column is repeated over the batch with it. */
+int aesfhe_ct_gather(aesfhe_engine *eng, const aesfhe_ct *ct, const int32_t *idx, int32_t n,
                      aesfhe_ct **out);
 /* an all-zero ciphertext (flagged is_zero) */
 int aesfhe_ct_zero(aesfhe_engine *eng, int32_t batch, int32_t level, aesfhe_ct **out);

@@ -231,7 +231,7 @@ static inline u64 uniform_mod(u64 r, u64 q) { return (u64)(((u128)r * q) >> 64);
 /* ------------------------------------------------------------------------------------------ */
 /* engine                                                                                      */
 struct aesfhe_engine {
-    int logN, N, L, K, dnum, np; /* np = L+1+K */
+    int logN, N, L, K, A, dnum, np; /* np = L+1+K; A = key-switch digit width (alpha) */
     u64 q[MAXP];
     double scales[MAXP];
     mont_t mont[MAXP];
@@ -442,6 +442,21 @@ static void prof_add(aesfhe_engine *e, int fam, double ms) {
     e->prof_n[fam] += 1;
 }
 
+/* Hybrid key switching keeps its error small only while every digit's modulus Q_j (A primes of
+ * the chain) stays below P, the product of the K special primes (engine: ckks_host.h
+ * digits_below_p, the same rule on the same bit sizes); checked for digits wider than K. */
+static int digits_below_p(const aesfhe_engine *e) {
+    const int Lp1 = e->L + 1;
+    double logp = 0.0;
+    for (int k = 0; k < e->K; k++) logp += log2((double)e->q[Lp1 + k]);
+    for (int lo = 0; lo < Lp1; lo += e->A) {
+        double lq = 0.0;
+        for (int i = lo; i < lo + e->A && i < Lp1; i++) lq += log2((double)e->q[i]);
+        if (lq > logp) return 0;
+    }
+    return 1;
+}
+
 /* ------------------------------------------------------------------------------------------ */
 int aesfhe_engine_create(const aesfhe_params *pp, aesfhe_engine **out) {
     if (!pp || !out) return fail(AESFHE_EARG, "null argument");
@@ -456,7 +471,12 @@ int aesfhe_engine_create(const aesfhe_params *pp, aesfhe_engine **out) {
     e->L = pp->max_level;
     e->K = pp->special_primes;
     e->np = e->L + 1 + e->K;
-    e->dnum = (e->L + 1 + e->K - 1) / e->K;
+    e->A = pp->digit_primes > 0 ? pp->digit_primes : e->K;
+    if (e->A > 16) {
+        free(e);
+        return fail(AESFHE_EARG, "key-switch digit width %d outside 1..16", pp->digit_primes);
+    }
+    e->dnum = (e->L + 1 + e->A - 1) / e->A;
     e->seed = pp->seed;
     {
         const u64 w[4] = {pp->seed, pp->seed_ext[0], pp->seed_ext[1], pp->seed_ext[2]};
@@ -480,6 +500,11 @@ int aesfhe_engine_create(const aesfhe_params *pp, aesfhe_engine **out) {
             free(e);
             return rc;
         }
+    }
+    if (e->A > e->K && !digits_below_p(e)) {
+        int A = e->A, K = e->K;
+        free(e);
+        return fail(AESFHE_EARG, "a key-switch digit of %d primes exceeds P (%d special primes)", A, K);
     }
     build_tables(e);
     *out = e;
@@ -880,7 +905,7 @@ static aesfhe_key *make_ksk_t(aesfhe_engine *e, const u64 *starget, u64 keyseed,
         u64 ka = derive(base, 2 * (u64)d), ke = derive(base, 2 * (u64)d + 1);
         i64 *ee = malloc(sizeof(i64) * N);
         for (int i = 0; i < N; i++) ee[i] = cbd21(rnd(e->ck, ke, (u64)i));
-        int lo = d * e->K, hi = lo + e->K; /* digit primes [lo, hi) intersect [0, nq) */
+        int lo = d * e->A, hi = lo + e->A; /* digit primes [lo, hi) intersect [0, nq) */
 #pragma omp parallel for schedule(static) num_threads(e->threads)
         for (int p = 0; p < np; p++) {
             u64 *b = k->data + (((size_t)d * 2 + 0) * np + p) * N;
@@ -1193,6 +1218,17 @@ int aesfhe_ct_concat(aesfhe_engine *e, const aesfhe_ct *const *parts, int32_t n,
     *out = r;
     return 0;
 }
+int aesfhe_ct_gather(aesfhe_engine *e, const aesfhe_ct *c, const int32_t *idx, int32_t n, aesfhe_ct **out) {
+    if (n < 1 || !idx) return fail(AESFHE_EARG, "empty gather");
+    for (int b = 0; b < n; b++)
+        if (idx[b] < 0 || idx[b] >= c->B) return fail(AESFHE_EARG, "gather index %d out of [0, %d)", idx[b], c->B);
+    aesfhe_ct *r = ct_new(e, n, c->npoly, c->level);
+    size_t per = (size_t)c->npoly * (c->level + 1) * e->N;
+    for (int b = 0; b < n; b++) memcpy(r->data + per * b, c->data + per * idx[b], sizeof(u64) * per);
+    r->is_zero = c->is_zero;
+    *out = r;
+    return 0;
+}
 int aesfhe_ct_zero(aesfhe_engine *e, int32_t B, int32_t level, aesfhe_ct **out) {
     if (B < 1 || level < 0 || level > e->L) return fail(AESFHE_EARG, "bad zero shape");
     aesfhe_ct *r = ct_new(e, B, 2, level);
@@ -1499,9 +1535,10 @@ static u64 *ks_acc(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k) {
 #pragma omp parallel for schedule(static) num_threads(e->threads)
     for (int i = 0; i <= l; i++) ntt_inv(e, dc + (size_t)i * N, i);
     u64 *acc = calloc((size_t)2 * ne * N, sizeof(u64));
-    int beta = (l + 1 + K - 1) / K;
+    const int A = e->A;
+    int beta = (l + 1 + A - 1) / A;
     for (int j = 0; j < beta; j++) {
-        int lo = j * K, hi = lo + K < l + 1 ? lo + K : l + 1, na = hi - lo;
+        int lo = j * A, hi = lo + A < l + 1 ? lo + A : l + 1, na = hi - lo;
         u64 hatinv[MAXP], hat[MAXP][MAXP];
         for (int i = lo; i < hi; i++) {
             u64 prod = 1;

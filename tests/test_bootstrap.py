@@ -39,9 +39,9 @@ def test_transform_factorisation(log_n, groups):
     np.testing.assert_allclose(y, u[_brv(n)], atol=1e-9)
 
 
-def _engine(lib, log_n=10, scale_bits=44, max_level=24):
-    e = Engine(log_n=log_n, max_level=max_level, special_primes=4, scale_bits=scale_bits, seed=3,
-               _lib=lib)
+def _engine(lib, log_n=10, scale_bits=44, max_level=24, **kw):
+    kw = dict(dict(special_primes=4), **kw)
+    e = Engine(log_n=log_n, max_level=max_level, scale_bits=scale_bits, seed=3, _lib=lib, **kw)
     sk = e.create_secret_key(1)
     return e, sk, e.create_public_key(sk), e.create_relinearization_key(sk)
 
@@ -163,10 +163,14 @@ def test_refresh_schedule():
 
 
 @pytest.mark.gpu
-def test_bootstrap_bits_bit_exact_vs_oracle(product_lib, oracle_lib, gpu_available):
+@pytest.mark.parametrize("kw", [{}, dict(scale_bits=40, max_level=30, special_primes=10, digit_primes=12)],
+                         ids=["K4", "K10A12"])
+def test_bootstrap_bits_bit_exact_vs_oracle(product_lib, oracle_lib, gpu_available, kw):
+    """Bit-mode and general bootstrapping residue for residue; K10A12: the bench's chain (L = 30,
+    K = 10 special primes, 12-prime key-switch digits) at N = 2^10."""
     outs = []
     for lib in (product_lib, oracle_lib):
-        e, sk, pk, rlk = _engine(lib)
+        e, sk, pk, rlk = _engine(lib, **kw)
         bs = Bootstrapper(e, sk, rlk)
         rng = np.random.default_rng(4)
         n = e.slot_count

@@ -12,6 +12,9 @@ from aes_xor_fhe.fhe import Engine
 pytestmark = pytest.mark.gpu
 
 SMALL = dict(log_n=12, max_level=6, special_primes=2, seed=1234)
+# key-switch digits wider than K (aesfhe_params.digit_primes): the bench's chain, alpha = 12 over
+# K = 10 special primes (dnum 3 at every level from 24 to 30; the digit product stays below P)
+DIGITS12 = dict(log_n=12, max_level=30, special_primes=10, digit_primes=12, scale_bits=40, seed=77)
 
 
 def _pair(product_lib, oracle_lib, **kw):
@@ -127,11 +130,14 @@ def test_batched_ops_bit_exact(product_lib, oracle_lib, gpu_available):
     np.testing.assert_allclose(dec, zb * zb[0], atol=1e-5)
 
 
-@pytest.mark.parametrize("k", [8, 10], ids=["K8", "K10"])
-def test_full_params_mul_bit_exact(product_lib, oracle_lib, gpu_available, k):
+@pytest.mark.parametrize("k,a", [(8, 0), (10, 0), (10, 12)], ids=["K8", "K10", "K10A12"])
+def test_full_params_mul_bit_exact(product_lib, oracle_lib, gpu_available, k, a):
     """BASELINE.json's parameter set: N = 2^16, L = 30 (one ct x ct multiply + rotation), with
-    K = 8 (dnum 4) and the bench's K = 10 (dnum 3, alpha 10)."""
-    kw = dict(log_n=16, max_level=30, special_primes=k, seed=99)
+    K = 8 (dnum 4), K = 10 (alpha 10: dnum 4 at level 30, a one-limb digit) and the bench's
+    K = 10 with 12-prime digits (dnum 3)."""
+    kw = dict(log_n=16, max_level=30, special_primes=k, digit_primes=a, seed=99)
+    if a:
+        kw["scale_bits"] = 40  # the bench's chain (12 x 40-bit digits below P = 10 x 50 bits)
     g, o = _pair(product_lib, oracle_lib, **kw)
     kg, ko = _keys(g), _keys(o)
     rng = np.random.default_rng(3)
@@ -189,10 +195,11 @@ def test_poly2_int_bit_exact(product_lib, oracle_lib, gpu_available, scale_bits)
     np.testing.assert_allclose(g.decrypt(res[0][0], kg["sk"]), want, atol=1e-4)
 
 
-def test_rotate_hoisted_bit_exact(product_lib, oracle_lib, gpu_available):
+@pytest.mark.parametrize("kw", [SMALL, DIGITS12], ids=["small", "digits12"])
+def test_rotate_hoisted_bit_exact(product_lib, oracle_lib, gpu_available, kw):
     """aesfhe_rotate_hoisted (one ModUp shared by every key) against the oracle's per-key
     restatement; slots equal np.roll like the ordinary rotation."""
-    g, o = _pair(product_lib, oracle_lib, **SMALL)
+    g, o = _pair(product_lib, oracle_lib, **kw)
     outs = []
     rng = np.random.default_rng(3)
     z = rng.uniform(-1, 1, (2, g.slot_count))
@@ -255,8 +262,10 @@ def test_dot_fma_bit_exact(product_lib, oracle_lib, gpu_available, kw):
 
 
 @pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=3, special_primes=2, seed=5),
-                                dict(log_n=16, max_level=12, special_primes=10, seed=5)],
-                         ids=["n4096", "n65536", "n65536K10"])
+                                dict(log_n=16, max_level=12, special_primes=10, seed=5),
+                                dict(log_n=16, max_level=30, special_primes=10, digit_primes=12,
+                                     scale_bits=40, seed=5)],
+                         ids=["n4096", "n65536", "n65536K10", "n65536K10A12"])
 def test_linear_bsgs_bit_exact(product_lib, oracle_lib, gpu_available, kw):
     """aesfhe_linear_bsgs (hoisted babies and lazy ModDown; at N = 2^16 the giants go through the
     fused ext-NTT row pass with accumulation) against the oracle's restatement, and its slots
@@ -284,15 +293,18 @@ def test_linear_bsgs_bit_exact(product_lib, oracle_lib, gpu_available, kw):
     np.testing.assert_allclose(g.decrypt(outs[0][0], outs[0][1]), want, atol=1e-5)
 
 
-@pytest.mark.parametrize("log_n", [16, 17])
-def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
+@pytest.mark.parametrize("log_n,kx", [(16, {}), (17, {}),
+                                      (16, dict(max_level=30, special_primes=10, digit_primes=12, scale_bits=40))],
+                         ids=["16", "17", "16K10A12"])
+def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n, kx):
     """The fused-NTT engines' ciphertext product (N = 2^16 / 2^17: d2 = a1 b1 formed in the INTT
     copy-in, d0 / d1 and the own digit's term in the key-switch prologue; no tensor ciphertext):
     K = 3 over 7 limbs (a partial last digit), a batch x broadcast product at mismatched levels
     (one operand level-downed first), a square, fused multiply-adds (alpha, a higher-level addend,
     beta) and products at every level down to 1 -- all residue for residue against the oracle's
-    tensor + relinearise + rescale."""
-    kw = dict(log_n=log_n, max_level=6, special_primes=3, seed=21)
+    tensor + relinearise + rescale.  K10A12: the bench's chain with 12-prime digits (L = 30)."""
+    kw = dict(dict(log_n=log_n, max_level=6, special_primes=3, seed=21), **kx)
+    L = kw["max_level"]
     g, o = _pair(product_lib, oracle_lib, **kw)
     rng = np.random.default_rng(9)
     z = rng.uniform(-1, 1, (3, g.slot_count))
@@ -300,7 +312,7 @@ def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
     res, sks = [], []
     for eng in (g, o):
         k = _keys(eng)
-        a, b = eng.encrypt(z, k["pk"], level=6), eng.encrypt(w, k["pk"], level=5)
+        a, b = eng.encrypt(z, k["pk"], level=L), eng.encrypt(w, k["pk"], level=L - 1)
         out = [eng.multiply(a, b, k["rlk"]), eng.multiply(b, a, k["rlk"]), eng.multiply(b, b, k["rlk"]),
                # fused multiply-adds (Chebyshev / double-angle steps): alpha, c at a higher level, beta
                eng.multiply_fma(a, b, k["rlk"], alpha=2, c=a, gamma=-1.0, beta=-1.0),
@@ -309,7 +321,7 @@ def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
                # rescales through the spread-fused column pass: constant products (plain
                # rescale) and exact-scale level-downs by one and by several levels
                eng.multiply(a, 0.37), eng.multiply(b, -1.5),
-               eng.level_down(a, 5), eng.level_down(a, 2), eng.level_down(b, 1)]
+               eng.level_down(a, L - 1), eng.level_down(a, 2), eng.level_down(b, 1)]
         # grouped rescale (lincomb_many: the groups as one batch through the fused rescale)
         out += eng.lincomb_many([a, b, a], [[1.0, 2.0, -1.0], [0.25, 0.0, 1j], [-3.0, 0.5, 0.0]])
         x = a
@@ -323,8 +335,8 @@ def test_fused_product_bit_exact(product_lib, oracle_lib, gpu_available, log_n):
     np.testing.assert_allclose(g.decrypt(res[0][0], sks[0]), z * w, atol=1e-5)
 
 
-@pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=4, special_primes=2, seed=5)],
-                         ids=["n4096", "n65536"])
+@pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=4, special_primes=2, seed=5), DIGITS12],
+                         ids=["n4096", "n65536", "digits12"])
 def test_switching_key_export_bit_exact(product_lib, oracle_lib, gpu_available, kw):
     """Relinearisation, conjugation and hoisted rotation keys: aesfhe_key_export returns
     residues equal to the oracle's, and a saved + loaded key relinearises to the same residues."""

@@ -257,3 +257,32 @@ def test_linear_bsgs_oracle(oracle_lib):
     np.testing.assert_allclose(e.decrypt(out, sk), want, atol=1e-6)
     with pytest.raises(RuntimeError, match="same baby"):
         e.linear_bsgs(c, bk, gk[:1], [[(1, pts[0]), (1, pts[1])]])
+
+
+def test_digit_width_oracle(oracle_lib):
+    """Key-switch digits wider than K (aesfhe_params.digit_primes): at L = 30 with K = 10 special
+    primes, 12-prime digits give dnum 3 instead of 4 (no one-limb digit at the top level) with the
+    same precision through products and rotations; a digit whose product exceeds P is refused."""
+    from aes_xor_fhe.fhe import Engine
+    errs = {}
+    for a in (0, 12):
+        e = Engine(log_n=10, max_level=30, special_primes=10, scale_bits=40, digit_primes=a, seed=3,
+                   _lib=oracle_lib)
+        assert (e.dnum, e.digit_primes) == ((4, 10) if a == 0 else (3, 12))
+        sk = e.create_secret_key(1)
+        pk, rlk, rot = e.create_public_key(sk), e.create_relinearization_key(sk), e.create_rotation_key(sk)
+        v = np.random.default_rng(0).uniform(-1, 1, e.slot_count)
+        ct = e.encrypt(v, pk)
+        x, ref, err = ct, v.copy(), []
+        for _ in range(4):
+            x, ref = e.multiply(x, ct, rlk), ref * v
+            err.append(np.abs(np.real(e.decrypt(x, sk)) - ref).max())
+        err.append(np.abs(np.real(e.decrypt(e.rotate(x, rot, 3), sk)) - np.roll(ref, 3)).max())
+        errs[a] = np.array(err)
+        assert errs[a].max() < 1e-7
+        if a:
+            assert e.key_fingerprint() != Engine(log_n=10, max_level=30, special_primes=10, scale_bits=40,
+                                                 seed=3, _lib=oracle_lib).key_fingerprint()
+    assert np.all(errs[12] < 2 * errs[0] + 1e-9)
+    with pytest.raises(RuntimeError, match="exceeds P"):
+        Engine(log_n=10, max_level=30, special_primes=10, scale_bits=40, digit_primes=16, seed=3, _lib=oracle_lib)

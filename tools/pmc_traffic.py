@@ -118,6 +118,7 @@ def main():
         r = json.loads(open(a.bench).read().strip().splitlines()[-1])
         cfg = r["config"]
         out["workload"] = {"log_n": cfg["log_n"], "max_level": cfg["max_level"], "special_primes": cfg["special_primes"],
+                           "digit_primes": cfg.get("digit_primes", cfg["special_primes"]),
                            "batch": cfg["ciphertext_sets_per_gpu"], "layout": cfg["layout"]}
     text = json.dumps(out, indent=1)
     if a.out:
