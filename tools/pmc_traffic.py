@@ -33,6 +33,7 @@ CLASSES = [
     (r"k_moddown_finish", "moddown_finish"),
     (r"k_poly2_int<", "poly2_int"),
     (r"k_poly2\b", "poly2"),
+    (r"k_gather_batch", "gather"),
     (r"k_lincomb_many", "lincomb_many"),
     (r"k_lincomb\b", "lincomb"),
     (r"k_dot_pt_ext_multi", "dot_pt_ext_multi"),
