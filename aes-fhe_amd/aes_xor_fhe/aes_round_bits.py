@@ -250,14 +250,45 @@ class AESRowRound:
         limit = self.MAX_ROUNDS_AFTER_REFRESH if refreshed else self.MAX_ROUNDS_FRESH
         return level < need or (not final and (level - need < stc or since >= limit))
 
+    def refreshes_after(self, rnd: int, level: int, top: int, stc: int) -> float:
+        """Refreshes that rounds rnd..10 need when they start right after a refresh at `level`,
+        later refreshes returning `top` (inf if a round would run out of levels)."""
+        n, since, lvl = 0, 0, level
+        for r in range(rnd, 11):
+            final = r == 10
+            if self.needs_refresh(lvl, final, since, True, stc):
+                if since == 0:
+                    return float("inf")
+                n, since, lvl = n + 1, 0, top
+            lvl -= self.FINAL_DEPTH if final else self.ROUND_DEPTH
+            since += 1
+            if lvl < 0:
+                return float("inf")
+        return n
+
+    def pick_bootstrapper(self, bss, rnd: int):
+        """The first of `bss` (cheapest first) whose output level keeps the fewest refreshes for
+        rounds rnd..10: a refresh followed by two middle rounds and another refresh needs only
+        2 * 7 + StC levels, the one before the last three rounds 7 + 7 + 5."""
+        if len(bss) == 1:
+            return bss[0]
+        stc = len(bss[0].stc_bits)
+        top = max(b.bits_level for b in bss)
+        counts = [self.refreshes_after(rnd, b.bits_level, top, stc) for b in bss]
+        return bss[counts.index(min(counts))]
+
     def encrypt_aes128(self, bits, keys, bs, timings: dict | None = None, pairs_per_call: int = 8,
                        progress=None):
         """AES-128 encryption of the bit state under the 11 encrypted round keys `keys`
-        (FIPS-197 section 5.1), bootstrapping with `bs` (a bootstrap.Bootstrapper) as the level
-        budget and the error budget (needs_refresh) require.  Returns the state
-        and the number of refreshes.  progress: optional callable(str) told after each step."""
+        (FIPS-197 section 5.1), bootstrapping with `bs` (a bootstrap.Bootstrapper, or a list of them
+        cheapest first: each refresh takes the first whose output level costs no extra refresh,
+        pick_bootstrapper) as the level budget and the error budget (needs_refresh) require.
+        Returns the state and the number of refreshes.  progress: optional callable(str) told
+        after each step."""
         import time
-        stc = len(bs.stc_bits)
+        bss = list(bs) if isinstance(bs, (list, tuple)) else [bs]
+        stc = len(bss[0].stc_bits)
+        assert all(len(b.stc_bits) == stc for b in bss)
         S = self.add_round_key(bits, keys[0])
         refreshes = 0
         since = 0
@@ -267,10 +298,11 @@ class AESRowRound:
             if self.needs_refresh(lvl, final, since, refreshes > 0, stc):
                 since = 0
                 t0 = time.perf_counter()
-                S = self.refresh(S, bs, pairs_per_call)
+                b = self.pick_bootstrapper(bss, rnd)
+                S = self.refresh(S, b, pairs_per_call)
                 refreshes += 1
                 if progress:
-                    progress(f"refresh {refreshes} before round {rnd}")
+                    progress(f"refresh {refreshes} before round {rnd} (CtS in {b.cts_groups} maps, output level {b.bits_level})")
                 if timings is not None:
                     self.e.materialize(S)
                     self.e.synchronize()

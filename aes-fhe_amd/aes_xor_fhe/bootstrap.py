@@ -109,7 +109,11 @@ class Bootstrapper:
     def __init__(self, engine: Engine, sk, rlk, cjk=None, *, hw: int = 32, K: float = 12.0,
                  r: int = 3, deg: int = 31, groups: int = 3, seed: int = 7,
                  bits_deg: int | None = None, bits_r: int | None = None, lazy: bool = True, baby_scale: int = 2,
-                 bits_opt: bool = True):
+                 bits_opt: bool = True, cts_groups: int | None = None):
+        # cts_groups: CoeffToSlot's stages merged into this many maps (default `groups`, which
+        # StC keeps): more groups = more levels, far fewer diagonals per map
+        cts_groups = groups if cts_groups is None else cts_groups
+        self.groups, self.cts_groups = groups, cts_groups
         e = self.e = engine
         self.rlk = rlk
         self.cjk = cjk if cjk is not None else e.create_conjugation_key(sk)
@@ -139,13 +143,13 @@ class Bootstrapper:
         D = e.scales
         n, N = self.n, self.N
         # CtS: (D_L / (2 q0 Bnd)) * prod of inverse stages; StC: (q0 / (2 pi D_0)) * forward stages
-        cts = transform_groups(n, N, groups, inverse=True)
+        cts = transform_groups(n, N, cts_groups, inverse=True)
         stc = transform_groups(n, N, groups, inverse=False)
         # bit mode: c_in = D_L / (2 q0 Bnd) ~ 2^-15.7 spread over the CtS groups' diagonals
         # (c_in^(1/groups) each, plaintext integers ~2^30): the rounding it adds to t / q0 is
         # ~1e-7, and the bit mode's error enters squared
         self.B_bits = K + 1.0
-        f_in = (D[self.L] / (2.0 * q0 * self.B_bits)) ** (1.0 / groups)
+        f_in = (D[self.L] / (2.0 * q0 * self.B_bits)) ** (1.0 / cts_groups)
         cts_bits = [{d: v * f_in for d, v in M.items()} for M in cts] if bits_opt else None
         # General mode: c_in folded into one group's diagonals would leave their plaintext integers
         # ~25 bits, and this mode's error is linear in it.  It is applied as its own constant multiply instead (one level): the
@@ -187,9 +191,9 @@ class Bootstrapper:
             self.cheb_bits = self._bits_fit(bits_deg, bits_r, self.B_bits, K)
         else:
             self.cheb_bits = self._cheb_fit(bits_deg, bits_r, self.B)
-        self.depth = 1 + 2 * groups + math.ceil(math.log2(deg + 1)) + 1 + r
+        self.depth = 1 + groups + cts_groups + math.ceil(math.log2(deg + 1)) + 1 + r
         cheb_depth = math.ceil(math.log2(bits_deg + 1)) + (0 if bits_opt else 1)
-        self.bits_level = self.L - ((0 if bits_opt else 1) + groups + cheb_depth + bits_r)
+        self.bits_level = self.L - ((0 if bits_opt else 1) + cts_groups + cheb_depth + bits_r)
 
     @staticmethod
     def _bits_fit(deg: int, r: int, bnd: float, K: float, width: float = 1e-2,

@@ -160,6 +160,9 @@ def parse():
                     help="profiled (HIP-event) round steps after the timed region, for the roofline")
     ap.add_argument("--aes10-ppc", type=int, default=0,
                     help="bit-ciphertext pairs per bootstrap call (0: 64 / aes10-batch at N = 2^16, 16 / aes10-batch at 2^17)")
+    ap.add_argument("--aes10-cts-groups", type=lambda s: [int(x) for x in s.split(",")], default=[5, 3],
+                    help="CoeffToSlot map counts of the ten-round leg's bootstrappers, cheapest first "
+                         "(each refresh takes the first whose output level costs no extra refresh)")
     ap.add_argument("--aes10-batch", type=int, default=16,
                     help="ciphertext sets for the full 10-round AES-128 measurement (0: skip)")
     ap.add_argument("--client-batch", type=int, default=8,
@@ -243,7 +246,11 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     R = drv.R
     sk, _, rlk, cjk = drv.keys
     t0 = time.perf_counter()
-    bs = Bootstrapper(eng, sk, rlk, cjk)
+    # one bootstrapper per CoeffToSlot group count, cheapest first: a refresh followed by two
+    # middle rounds takes 5 CtS maps (output level L - 13, 200 vs 226 ms per 64-ciphertext call,
+    # tools/gpu_r03_ctsg.sh), the one before the last three rounds keeps 3 (L - 11)
+    # (AESRowRound.pick_bootstrapper)
+    bs = [Bootstrapper(eng, sk, rlk, cjk, cts_groups=g) for g in args.aes10_cts_groups]
     eng.synchronize()
     setup_s = time.perf_counter() - t0
     key = np.random.default_rng(25073103).integers(0, 256, 16, dtype=np.uint8)
@@ -290,6 +297,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
             "bootstrap_share": round(tm.get("bootstrap", 0.0) / max(el, 1e-9), 3),
             "bootstrap_ms_per_bit_ct": round(1e3 * tm.get("bootstrap", 0.0) / max(nref * 32 * nb, 1), 2),
             "bootstrap_setup_s": round(setup_s, 2), "verified": ok,
+            "bootstrap_cts_groups": args.aes10_cts_groups,
             "block_rounds_per_s": round(10 * nb * R.n_blk * world / el, 2),
             "per_round_level_ms": tm.get("per_round"), "pool": eng.pool_stats(),
             "timed_mallocs": timed_mallocs}

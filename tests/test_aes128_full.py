@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from aes_xor_fhe import aes_tables as T
-from aes_xor_fhe.aes_round_bits import AESRowRound
+from aes_xor_fhe.aes_round_bits import AESRowRound, AESSlicedRound
 from aes_xor_fhe.bootstrap import Bootstrapper
 from aes_xor_fhe.fhe import Engine
 
@@ -19,13 +19,13 @@ FIPS_C1_PT = bytes.fromhex("00112233445566778899aabbccddeeff")
 FIPS_C1_CT = bytes.fromhex("69c4e0d86a7b0430d8cdb78070b4c55a")
 
 
-def _run(lib, log_n, nb=1, seed=3):
-    e = Engine(log_n=log_n, max_level=30, special_primes=8 if log_n >= 14 else 4,
-               scale_bits=SCALE_BITS, seed=seed, _lib=lib)
+def _run(lib, log_n, nb=1, seed=3, cls=AESRowRound, cts_groups=(3,), **kw):
+    kw = dict(dict(special_primes=8 if log_n >= 14 else 4, scale_bits=SCALE_BITS), **kw)
+    e = Engine(log_n=log_n, max_level=30, seed=seed, _lib=lib, **kw)
     sk = e.create_secret_key(1)
     rlk = e.create_relinearization_key(sk)
-    R = AESRowRound(e, sk, e.create_public_key(sk), rlk)
-    bs = Bootstrapper(e, sk, rlk)
+    R = cls(e, sk, e.create_public_key(sk), rlk)
+    bs = [Bootstrapper(e, sk, rlk, cts_groups=g) for g in cts_groups]
     rng = np.random.default_rng(seed)
     key = np.frombuffer(FIPS_C1_KEY, dtype=np.uint8)
     blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
@@ -33,7 +33,7 @@ def _run(lib, log_n, nb=1, seed=3):
     rks = T.expand_key(key)
     keys = [R.encrypt_round_key(rk) for rk in rks]
     out, nref = R.encrypt_aes128(R.encrypt_blocks(blocks), keys, bs)
-    got = R.decrypt_blocks(out)
+    got = R.decrypt_blocks(out, nb)
     want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
     return got, want, nref, out
 
@@ -52,6 +52,27 @@ def test_aes128_ten_rounds_oracle(oracle_lib):
 @pytest.mark.gpu
 def test_aes128_ten_rounds_full_params(product_lib, gpu_available):
     got, want, nref, out = _run(product_lib, 16)
+    assert nref == 3 and out[0][0].level == 0
+    assert np.array_equal(got, want)
+    assert bytes(got[0, 0]) == FIPS_C1_CT
+
+
+# the bench's ten-round configuration: sliced state, 12-prime key-switch digits over K = 10,
+# bootstrappers with 5 and 3 CoeffToSlot maps (the two middle refreshes take the 5-map one,
+# output level 17; the last keeps 19 for rounds 8-10)
+BENCH10 = dict(cls=AESSlicedRound, cts_groups=(5, 3), special_primes=10, digit_primes=12, scale_bits=40)
+
+
+def test_aes128_ten_rounds_sliced_two_bootstrappers_oracle(oracle_lib):
+    got, want, nref, out = _run(oracle_lib, 10, nb=2, **BENCH10)
+    assert nref == 3 and out[0][0].level == 0
+    assert np.array_equal(got, want)
+    assert bytes(got[0, 0]) == FIPS_C1_CT
+
+
+@pytest.mark.gpu
+def test_aes128_ten_rounds_sliced_full_params(product_lib, gpu_available):
+    got, want, nref, out = _run(product_lib, 16, nb=4, **BENCH10)
     assert nref == 3 and out[0][0].level == 0
     assert np.array_equal(got, want)
     assert bytes(got[0, 0]) == FIPS_C1_CT

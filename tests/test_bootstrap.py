@@ -162,6 +162,31 @@ def test_refresh_schedule():
         assert all(len([ch for ch in seg if ch != "0"]) <= 3 for seg in segs)
 
 
+def test_pick_bootstrapper():
+    """Per-refresh choice among bootstrappers (AESRowRound.pick_bootstrapper): at L = 30 the
+    5-map CtS (output 17) serves the refreshes before rounds 4 and 6 (two middle rounds + StC =
+    17 levels) and the 3-map one (output 19) the refresh before rounds 8-10 (7 + 7 + 5); at L = 35
+    the cheaper one serves all three."""
+    from types import SimpleNamespace as NS
+    from aes_xor_fhe.aes_round_bits import AESRowRound
+    R = AESRowRound.__new__(AESRowRound)
+    for L, want in ((30, [17, 17, 19]), (35, [22, 22, 22])):
+        bss = [NS(bits_level=L - 13, stc_bits=[0] * 3), NS(bits_level=L - 11, stc_bits=[0] * 3)]
+        lvl, since, got = L - 1, 0, []
+        for rnd in range(1, 11):
+            final = rnd == 10
+            if R.needs_refresh(lvl, final, since, bool(got), 3):
+                b = R.pick_bootstrapper(bss, rnd)
+                got.append(b.bits_level)
+                lvl, since = b.bits_level, 0
+            lvl -= R.FINAL_DEPTH if final else R.ROUND_DEPTH
+            assert lvl >= 0
+            since += 1
+        assert got == want, (L, got)
+    # a single bootstrapper is always taken
+    assert R.pick_bootstrapper(bss[1:], 8) is bss[1]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("kw", [{}, dict(scale_bits=40, max_level=30, special_primes=10, digit_primes=12)],
                          ids=["K4", "K10A12"])

@@ -29,13 +29,16 @@ def main():
     ap.add_argument("--baby-scale", type=int, default=2, help="BSGS baby steps x this (lazy mode)")
     ap.add_argument("--eager", action="store_true", help="rotate_hoisted + dot_pt + galois linear maps")
     ap.add_argument("--no-opt", action="store_true", help="bit mode without bits_opt (c_in multiply, depth-6 Chebyshev)")
+    ap.add_argument("--cts-groups", type=int, default=None, help="CoeffToSlot maps (default: groups = 3)")
+    ap.add_argument("--digit-primes", type=int, default=0, help="key-switch digit width (0: K)")
     a = ap.parse_args()
-    e = Engine(log_n=a.log_n, max_level=a.max_level, special_primes=a.special_primes, scale_bits=a.scale_bits, seed=3)
+    e = Engine(log_n=a.log_n, max_level=a.max_level, special_primes=a.special_primes, scale_bits=a.scale_bits, seed=3,
+               digit_primes=a.digit_primes)
     sk = e.create_secret_key(1)
     pk = e.create_public_key(sk)
     t = time.time()
     bs = Bootstrapper(e, sk, e.create_relinearization_key(sk), lazy=not a.eager, baby_scale=a.baby_scale,
-                      bits_opt=not a.no_opt)
+                      bits_opt=not a.no_opt, cts_groups=a.cts_groups)
     e.synchronize()
     setup = time.time() - t
     n = e.slot_count
@@ -56,7 +59,8 @@ def main():
                       "ms_per_call": round(1e3 * min(ts), 1), "cts_per_call": 2 * a.batch,
                       "ms_per_ct": round(1e3 * min(ts) / (2 * a.batch), 2),
                       "out_level": ya.level, "max_err": float(err), "bits_opt": bs.bits_opt,
-                      "rotation_keys": len(bs.rot)}), flush=True)
+                      "rotation_keys": len(bs.rot), "cts_groups": bs.cts_groups,
+                      "digit_primes": e.digit_primes}), flush=True)
     if a.phases:
         def timed(fn, *xs):
             e.synchronize()
