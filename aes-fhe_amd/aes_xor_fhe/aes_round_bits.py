@@ -277,19 +277,51 @@ class AESRowRound:
         counts = [self.refreshes_after(rnd, b.bits_level, top, stc) for b in bss]
         return bss[counts.index(min(counts))]
 
+    KEY_OFFSET = 4  # a round's key product takes the SubBytes output: input level - 4
+
+    def schedule(self, L: int, bss):
+        """[(round, input level, bootstrapper refreshing before it or None)] that encrypt_aes128
+        runs from a fresh encryption at level L (ARK0 -> L - 1); bss as there (objects with
+        bits_level / stc_bits suffice)."""
+        bss = list(bss) if isinstance(bss, (list, tuple)) else [bss]
+        stc = len(bss[0].stc_bits)
+        out, lvl, since, nref = [], L - 1, 0, 0
+        for rnd in range(1, 11):
+            final = rnd == 10
+            b = None
+            if self.needs_refresh(lvl, final, since, nref > 0, stc):
+                b = self.pick_bootstrapper(bss, rnd)
+                lvl, since, nref = b.bits_level, 0, nref + 1
+            out.append((rnd, lvl, b))
+            lvl -= self.FINAL_DEPTH if final else self.ROUND_DEPTH
+            since += 1
+        return out
+
+    def key_levels(self, L: int, bss) -> List[int]:
+        """The level each of the 11 round keys is consumed at (key 0: ARK0 at L; key i: round i's
+        SubBytes output level): keys encrypted there need no level-down and hold only the limbs
+        they use."""
+        return [L] + [lvl - self.KEY_OFFSET for _, lvl, _ in self.schedule(L, bss)]
+
     def encrypt_aes128(self, bits, keys, bs, timings: dict | None = None, pairs_per_call: int = 8,
-                       progress=None):
+                       progress=None, consume: bool = False):
         """AES-128 encryption of the bit state under the 11 encrypted round keys `keys`
         (FIPS-197 section 5.1), bootstrapping with `bs` (a bootstrap.Bootstrapper, or a list of them
         cheapest first: each refresh takes the first whose output level costs no extra refresh,
         pick_bootstrapper) as the level budget and the error budget (needs_refresh) require.
         Returns the state and the number of refreshes.  progress: optional callable(str) told
-        after each step."""
+        after each step.  consume: empty the rows of `bits` after AddRoundKey(k_0), so that the
+        input state (the largest one, at the top level) is freed if the caller holds it only
+        through that list."""
         import time
         bss = list(bs) if isinstance(bs, (list, tuple)) else [bs]
         stc = len(bss[0].stc_bits)
         assert all(len(b.stc_bits) == stc for b in bss)
         S = self.add_round_key(bits, keys[0])
+        if consume:
+            self.e.materialize(S)
+            for row in bits:
+                row.clear()
         refreshes = 0
         since = 0
         for rnd in range(1, 11):

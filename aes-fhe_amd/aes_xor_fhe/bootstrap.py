@@ -192,8 +192,14 @@ class Bootstrapper:
         else:
             self.cheb_bits = self._cheb_fit(bits_deg, bits_r, self.B)
         self.depth = 1 + groups + cts_groups + math.ceil(math.log2(deg + 1)) + 1 + r
+        self.bits_level = self.bits_output_level(self.L, cts_groups, bits_deg, bits_r, bits_opt)
+
+    @staticmethod
+    def bits_output_level(L: int, cts_groups: int = 3, bits_deg: int = 15, bits_r: int = 4,
+                          bits_opt: bool = True) -> int:
+        """bits_level of a Bootstrapper with these parameters (no keys made)."""
         cheb_depth = math.ceil(math.log2(bits_deg + 1)) + (0 if bits_opt else 1)
-        self.bits_level = self.L - ((0 if bits_opt else 1) + cts_groups + cheb_depth + bits_r)
+        return L - ((0 if bits_opt else 1) + cts_groups + cheb_depth + bits_r)
 
     @staticmethod
     def _bits_fit(deg: int, r: int, bnd: float, K: float, width: float = 1e-2,

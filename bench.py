@@ -245,16 +245,27 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     from aes_xor_fhe.bootstrap import Bootstrapper
     R = drv.R
     sk, _, rlk, cjk = drv.keys
+    from types import SimpleNamespace
     t0 = time.perf_counter()
     # one bootstrapper per CoeffToSlot group count, cheapest first: a refresh followed by two
     # middle rounds takes 5 CtS maps (output level L - 13, 200 vs 226 ms per 64-ciphertext call,
     # tools/gpu_r03_ctsg.sh), the one before the last three rounds keeps 3 (L - 11)
-    # (AESRowRound.pick_bootstrapper)
-    bs = [Bootstrapper(eng, sk, rlk, cjk, cts_groups=g) for g in args.aes10_cts_groups]
+    # (AESRowRound.pick_bootstrapper); only those the schedule uses are built (at L = 35 the
+    # 5-map one serves every refresh)
+    L = eng.max_level
+    cands = [SimpleNamespace(cts_groups=g, bits_level=Bootstrapper.bits_output_level(L, g), stc_bits=[0] * 3)
+             for g in args.aes10_cts_groups]
+    sched = R.schedule(L, cands)
+    used = {b.cts_groups for _, _, b in sched if b is not None}
+    bs = [Bootstrapper(eng, sk, rlk, cjk, cts_groups=g) for g in args.aes10_cts_groups if g in used]
     eng.synchronize()
     setup_s = time.perf_counter() - t0
     key = np.random.default_rng(25073103).integers(0, 256, 16, dtype=np.uint8)
-    keys = [R.encrypt_round_key(rk) for rk in T.expand_key(key)]
+    # each round key encrypted at the level its product consumes it (AESRowRound.key_levels):
+    # the sliced state's per-column keys are 4x the rows layout's, and at N = 2^17, L = 35 the
+    # top-level set (101 GB) did not fit beside the run
+    klv = R.key_levels(L, bs)
+    keys = [R.encrypt_round_key(rk, level=lv) for rk, lv in zip(T.expand_key(key), klv)]
     rng = np.random.default_rng(2000 + rank)
     nb = args.aes10_batch
     # ~64 ciphertexts per Bootstrapper call at N = 2^16 (32: 14.18 k blocks/s, 64: 14.51 k, pool
@@ -270,7 +281,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
         log(f"aes10: {msg} (pool held {ps['held'] / 1e9:.1f} GB live {ps['live'] / 1e9:.1f} GB "
             f"mallocs {ps['mallocs']} trims {ps['trims']})")
     warm = R.encrypt_aes128(R.encrypt_blocks(rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)),
-                            keys, bs, pairs_per_call=ppc, progress=prog)
+                            keys, bs, pairs_per_call=ppc, progress=prog, consume=True)
     del warm
     blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
     st = R.encrypt_blocks(blocks)
@@ -279,7 +290,9 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     barrier()
     m0 = eng.pool_stats()["mallocs"]
     t0 = time.perf_counter()
-    out, nref = R.encrypt_aes128(st, keys, bs, timings=tm, pairs_per_call=ppc, progress=log)
+    # consume: the input state (at the top level) is freed after AddRoundKey(k_0) -- config 5's
+    # shard peaks within a few GB of the 288 GB otherwise
+    out, nref = R.encrypt_aes128(st, keys, bs, timings=tm, pairs_per_call=ppc, progress=log, consume=True)
     _materialize([c for row in out for c in row])
     barrier()
     el = allmax(time.perf_counter() - t0)
@@ -297,7 +310,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
             "bootstrap_share": round(tm.get("bootstrap", 0.0) / max(el, 1e-9), 3),
             "bootstrap_ms_per_bit_ct": round(1e3 * tm.get("bootstrap", 0.0) / max(nref * 32 * nb, 1), 2),
             "bootstrap_setup_s": round(setup_s, 2), "verified": ok,
-            "bootstrap_cts_groups": args.aes10_cts_groups,
+            "bootstrap_cts_groups": [b.cts_groups for b in bs], "round_key_levels": klv,
             "block_rounds_per_s": round(10 * nb * R.n_blk * world / el, 2),
             "per_round_level_ms": tm.get("per_round"), "pool": eng.pool_stats(),
             "timed_mallocs": timed_mallocs}

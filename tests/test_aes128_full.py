@@ -19,7 +19,7 @@ FIPS_C1_PT = bytes.fromhex("00112233445566778899aabbccddeeff")
 FIPS_C1_CT = bytes.fromhex("69c4e0d86a7b0430d8cdb78070b4c55a")
 
 
-def _run(lib, log_n, nb=1, seed=3, cls=AESRowRound, cts_groups=(3,), **kw):
+def _run(lib, log_n, nb=1, seed=3, cls=AESRowRound, cts_groups=(3,), key_levels=False, **kw):
     kw = dict(dict(special_primes=8 if log_n >= 14 else 4, scale_bits=SCALE_BITS), **kw)
     e = Engine(log_n=log_n, max_level=30, seed=seed, _lib=lib, **kw)
     sk = e.create_secret_key(1)
@@ -31,8 +31,12 @@ def _run(lib, log_n, nb=1, seed=3, cls=AESRowRound, cts_groups=(3,), **kw):
     blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
     blocks[0, 0] = np.frombuffer(FIPS_C1_PT, dtype=np.uint8)
     rks = T.expand_key(key)
-    keys = [R.encrypt_round_key(rk) for rk in rks]
+    # key_levels: each round key encrypted at the level its product consumes (as the bench does)
+    lv = R.key_levels(e.max_level, bs) if key_levels else [None] * 11
+    keys = [R.encrypt_round_key(rk, level=v) for rk, v in zip(rks, lv)]
     out, nref = R.encrypt_aes128(R.encrypt_blocks(blocks), keys, bs)
+    if key_levels:  # no level-down was needed anywhere: the state kept the schedule's levels
+        assert [l for _, l, _ in R.schedule(e.max_level, bs)][-1] == 5
     got = R.decrypt_blocks(out, nb)
     want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
     return got, want, nref, out
@@ -60,7 +64,8 @@ def test_aes128_ten_rounds_full_params(product_lib, gpu_available):
 # the bench's ten-round configuration: sliced state, 12-prime key-switch digits over K = 10,
 # bootstrappers with 5 and 3 CoeffToSlot maps (the two middle refreshes take the 5-map one,
 # output level 17; the last keeps 19 for rounds 8-10)
-BENCH10 = dict(cls=AESSlicedRound, cts_groups=(5, 3), special_primes=10, digit_primes=12, scale_bits=40)
+BENCH10 = dict(cls=AESSlicedRound, cts_groups=(5, 3), special_primes=10, digit_primes=12, scale_bits=40,
+               key_levels=True)
 
 
 def test_aes128_ten_rounds_sliced_two_bootstrappers_oracle(oracle_lib):
