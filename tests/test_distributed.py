@@ -99,6 +99,39 @@ def _worker_rows(rank, world, port, so, result_q):
         dist.destroy_process_group()
 
 
+def _worker_sliced(rank, world, port, so, result_q):
+    """The bench's default state (AESSlicedRound, 12-prime digits over K = 10): rank 0 encrypts
+    two slabs (8 sets), each rank receives one slab (its 4 columns together), runs one round
+    (ShiftRows as a batch gather, the batch-4 round key repeated), and rank 0 gathers and checks
+    FIPS-197."""
+    sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from aes_xor_fhe._abi import Lib
+        from aes_xor_fhe.fhe import Engine
+        from aes_xor_fhe.aes_round_bits import AESSlicedRound
+        from aes_xor_fhe.parallel import gather_ciphertext, rank_nonce_start, scatter_ciphertext
+        from aes_xor_fhe import aes_tables as T
+        e = Engine(_lib=Lib(so), log_n=10, max_level=30, special_primes=10, digit_primes=12, scale_bits=40,
+                   seed=5, nonce_start=rank_nonce_start(rank), thread_count=4)
+        sk = e.create_secret_key(1)
+        R = AESSlicedRound(e, sk, e.create_public_key(sk), e.create_relinearization_key(sk))
+        nsets = 4 * world
+        blocks = np.random.default_rng(12).integers(0, 256, (nsets, R.n_blk, 16), dtype=np.uint8)
+        rk = np.random.default_rng(13).integers(0, 256, 16, dtype=np.uint8)
+        st = R.encrypt_blocks(blocks) if rank == 0 else [[None] * 8 for _ in range(4)]
+        mine = [[scatter_ciphertext(e, c) for c in row] for row in st]
+        assert all(c.batch == 4 for row in mine for c in row)
+        out = R.round(mine, R.encrypt_round_key(rk))
+        full = [[gather_ciphertext(e, c) for c in row] for row in out]
+        if rank == 0:
+            result_q.put(bool(np.array_equal(R.decrypt_blocks(full, nsets), T.aes_round(blocks, rk))))
+    finally:
+        dist.destroy_process_group()
+
+
 def _worker_keys(rank, world, port, so, result_q):
     """shared_seed is one 256-bit value on every rank; engines built from it pass the key check;
     engines with their own seeds make scatter raise on every rank; an all-empty gather is None."""
@@ -165,6 +198,11 @@ def test_two_rank_shared_seed_and_key_check(oracle_lib):
 def test_two_rank_scatter_round_gather(oracle_lib):
     from conftest import ORACLE_SO
     assert _spawn(_worker, str(ORACLE_SO)) is True
+
+
+def test_two_rank_sliced_round(oracle_lib):
+    from conftest import ORACLE_SO
+    assert _spawn(_worker_sliced, str(ORACLE_SO)) is True
 
 
 def test_two_rank_rows_aes128_with_bootstrap_uneven(oracle_lib):
