@@ -388,8 +388,8 @@ class AESSlicedRound(AESRowRound):
       (Engine.gather, one copy pass): no automorphism and no key switch, where AESRowRound
       rotates row r by -r n_blk slots (24 key switches per 8192 blocks, ~9 % of the round's).
     * The round key differs per column: its ciphertexts carry batch 4 (element c = key byte
-      r + 4c), level-downed to the state's level and repeated over the slabs right before each
-      key product (key_mul), which is evaluated at once so that only one repeated key is alive.
+      r + 4c); the key product cycles through them (aesfhe_mul: element 4 s + c takes key
+      element c), after a level-down of the 4 elements to the state's level (key_mul).
     * The slabs, not the batch elements, are what may be split across ranks (a slab's four
       columns must stay together): a shard of the batch is a multiple of 4 elements.
     """
@@ -463,15 +463,12 @@ class AESSlicedRound(AESRowRound):
 
     # ---- round steps --------------------------------------------------------------------------
     def key_mul(self, a: Ciphertext, k: Ciphertext) -> Ciphertext:
-        """a XOR k: the batch-4 key aligned to a's level (the level-down the product would run)
-        and repeated over a's slabs; the product is evaluated now, so the repeated key is freed
-        before the next one is made."""
-        S = a.batch // 4
+        """a XOR k: the batch-4 key (element c) against a's elements 4 s + c -- aesfhe_mul's cyclic
+        broadcast (element i takes key element i mod 4), so the key is never repeated in memory.
+        Aligned to a's level first (the level-down the product would run, on 4 elements)."""
         if k.level > a.level:
             k = self.e.level_down(k, a.level)
-        if S > 1:
-            k = self.e.gather(k, [c for _ in range(S) for c in range(4)])
-        return Engine.materialize(self.mul(a, k))
+        return self.mul(a, k)
 
     def shift_rows(self, bits):
         """out(r, c) = in(r, c + r): element 4 s + c of row r takes element 4 s + (c + r) mod 4."""

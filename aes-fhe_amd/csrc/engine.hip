@@ -366,6 +366,7 @@ static Opnd opnd(const View& v, int outB) {
     o.bs = (v.B == 1 && outB > 1) ? 0 : v.bs;
     o.ps = v.ps;
     o.np = v.np;
+    o.bmask = (v.B > 1 && v.B < outB) ? v.B - 1 : -1;  // cyclic broadcast (check_cyclic)
     return o;
 }
 
@@ -1681,6 +1682,13 @@ static View trunc_view(const aesfhe_ct* c, int l) {
 static void check_bcast(int a, int b) {
     if (a != b && a != 1 && b != 1) throw_err(AESFHE_EARG, "batch mismatch %d vs %d", a, b);
 }
+// aesfhe_mul / aesfhe_tensor: the smaller batch may be any power of two dividing the larger --
+// element i of the result takes element i mod B_small of it (a B = 1 broadcast is the special
+// case; the sliced AES state's batch-4 round keys against its 4 s + c batch order)
+static void check_cyclic(int a, int b) {
+    const int lo = std::min(a, b), hi = std::max(a, b);
+    if (a != b && (lo < 1 || (lo & (lo - 1)) || hi % lo)) throw_err(AESFHE_EARG, "batch mismatch %d vs %d", a, b);
+}
 
 extern "C" int aesfhe_rescale(aesfhe_engine* e, const aesfhe_ct* c, aesfhe_ct** out) {
     API_BEGIN
@@ -1924,8 +1932,11 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
     // 1. INTT copy of the input
     Span sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
     if (pa) {
-        intt_prod(e, span_s((u64*)pa->ptr + pa->ps, pa->bs, l + 1, l + 1, 0, e->Lp1),
-                  span_s((u64*)pb->ptr + pb->ps, pb->bs, l + 1, l + 1, 0, e->Lp1), sdc, B * (l + 1), fac);
+        Span sa = span_s((u64*)pa->ptr + pa->ps, pa->bs, l + 1, l + 1, 0, e->Lp1);
+        Span sb = span_s((u64*)pb->ptr + pb->ps, pb->bs, l + 1, l + 1, 0, e->Lp1);
+        sa.pmask = pa->bmask;  // cyclic broadcast of a product operand (check_cyclic)
+        sb.pmask = pb->bmask;
+        intt_prod(e, sa, sb, sdc, B * (l + 1), fac);
     } else {
         Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1);
         ntt(e, sd, sdc, B * (l + 1), true);
@@ -2144,7 +2155,7 @@ static aesfhe_ct* tensor_ct(aesfhe_engine* e, const View& a, const View& b, int 
 extern "C" int aesfhe_tensor(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* b, aesfhe_ct** out) {
     API_BEGIN
     if (a->np != 2 || b->np != 2) throw_err(AESFHE_EDEGREE, "tensor inputs should have 2 polynomials");
-    check_bcast(a->B, b->B);
+    check_cyclic(a->B, b->B);
     int l = std::min(a->level, b->level), B = std::max(a->B, b->B);
     if (a->is_zero || b->is_zero) {
         *out = ct_zero_new(e, B, 3, l);
@@ -2167,7 +2178,7 @@ extern "C" int aesfhe_relinearize(aesfhe_engine* e, const aesfhe_ct* c, const ae
 }
 
 static aesfhe_ct* mul_ct(aesfhe_engine* e, const aesfhe_ct* a, const aesfhe_ct* b, const aesfhe_key* rlk) {
-    check_bcast(a->B, b->B);
+    check_cyclic(a->B, b->B);
     int l = std::min(a->level, b->level), B = std::max(a->B, b->B);
     if (l < 1) throw_err(AESFHE_ELEVEL, "no level left for a ciphertext multiplication");
     if (a->is_zero || b->is_zero) return ct_zero_new(e, B, 2, l - 1);

@@ -109,13 +109,14 @@ struct Span {
     int nq;
     int qpid0;
     int spid0;
+    int pmask = -1;  // polynomial index cycled through (an operand in aesfhe_mul's cyclic broadcast)
 };
 
 __device__ __forceinline__ u64* span_ptr(const Span& s, int y, int logN, int Lp1, int& pid) {
     (void)Lp1;
     int p = y / s.nl, l = y - p * s.nl;
     pid = l < s.nq ? s.qpid0 + l : s.spid0 + (l - s.nq);
-    return s.base + (long)p * s.pstride + ((long)l << logN);
+    return s.base + (long)(p & s.pmask) * s.pstride + ((long)l << logN);
 }
 
 struct Tabs {

@@ -13,13 +13,16 @@ __device__ __forceinline__ u64 red_m(u64 x, u64 q, double qinv) {
     return fix_m(x - qh * q, q);
 }
 
-// An operand for elementwise kernels: element (b, p, l, k) at ptr + b*bs + p*ps + l*N + k.
-// ptr == nullptr or p >= np reads as zero.
+// An operand for elementwise kernels: element (b, p, l, k) at ptr + (b & bmask)*bs + p*ps + l*N + k.
+// ptr == nullptr or p >= np reads as zero.  bmask: batch elements cycled through (B_op - 1 for a
+// power-of-two B_op below the output's batch, the cyclic broadcast of aesfhe_mul; -1 otherwise;
+// a B = 1 broadcast keeps bs = 0).
 struct Opnd {
     const u64* ptr;
     long bs;
     long ps;
     int np;
+    int bmask = -1;
 };
 
 // Absent operands read this zero word: the address is selected, not the load, so a kernel's
@@ -28,7 +31,7 @@ struct Opnd {
 __device__ const u64 kZeroWord = 0;
 __device__ __forceinline__ u64 opnd_get(const Opnd& o, int b, int p, int l, int k, int logN) {
     const bool has = o.ptr && p < o.np;
-    return *(has ? o.ptr + (long)b * o.bs + (long)p * o.ps + ((long)l << logN) + k : &kZeroWord);
+    return *(has ? o.ptr + (long)(b & o.bmask) * o.bs + (long)p * o.ps + ((long)l << logN) + k : &kZeroWord);
 }
 
 struct Out {

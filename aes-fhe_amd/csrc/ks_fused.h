@@ -189,9 +189,9 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
         if (PROD && t <= l) {
             const double f = pmodf[t], w = tw_w(f, q);
             const u64* kp = key + (long)own * kdig + ((long)pid << LOGN) + (long)row * 256 + L;
-            const u64* xa = addend.ptr + (long)bb * addend.bs + roff;
-            const u64* xb = pb.ptr + (long)bb * pb.bs + roff;
-            const u64* xc = pc.ptr ? pc.ptr + (long)bb * pc.bs + roff : xb;
+            const u64* xa = addend.ptr + (long)(bb & addend.bmask) * addend.bs + roff;
+            const u64* xb = pb.ptr + (long)(bb & pb.bmask) * pb.bs + roff;
+            const u64* xc = pc.ptr ? pc.ptr + (long)(bb & pc.bmask) * pc.bs + roff : xb;
             const double fal = fac ? (double)fac[3 * t] : 0.0, fC = fac ? (double)fac[3 * t + 1] : 0.0,
                          fK = fac ? (double)fac[3 * t + 2] : 0.0;
 #pragma unroll

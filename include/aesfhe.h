@@ -43,7 +43,9 @@
  *   - Handles are immutable values (every op returns a new handle, as desilofhe objects are);
  *     the caller frees them with the matching *_free.
  *   - A ciphertext handle holds a BATCH of B ciphertexts at one level; binary operations
- *     accept B_a == B_b or a broadcast operand with B == 1.
+ *     accept B_a == B_b or a broadcast operand with B == 1; aesfhe_mul and aesfhe_tensor also
+ *     cycle through a smaller power-of-two batch dividing the larger one (element i takes
+ *     element i mod B_small).
  *   - Residues are kept in the NTT (evaluation) domain, canonical in [0, q).
  *
  * Two implementations export exactly this ABI:

@@ -1495,7 +1495,7 @@ static void tensor_acc(aesfhe_engine *e, const aesfhe_ct *a, const aesfhe_ct *b,
         for (int i = 0; i <= r->level; i++) {
             const mont_t *m = &e->mont[i];
             const u64 q = e->q[i];
-            int ia = a->B == 1 ? 0 : bb, ib = b->B == 1 ? 0 : bb;
+            int ia = bb % a->B, ib = bb % b->B; /* cyclic broadcast (cyclic_ok; B = 1 included) */
             const u64 *a0 = limb(e, a, ia, 0, i), *a1 = limb(e, a, ia, 1, i);
             const u64 *b0 = limb(e, b, ib, 0, i), *b1 = limb(e, b, ib, 1, i);
             u64 *d0 = limb(e, r, bb, 0, i), *d1 = limb(e, r, bb, 1, i), *d2 = limb(e, r, bb, 2, i);
@@ -1507,9 +1507,16 @@ static void tensor_acc(aesfhe_engine *e, const aesfhe_ct *a, const aesfhe_ct *b,
         }
 }
 
+/* aesfhe_mul / aesfhe_tensor: the smaller batch may be any power of two dividing the larger;
+ * element i of the result takes element i mod B_small of that operand */
+static int cyclic_ok(const aesfhe_ct *a, const aesfhe_ct *b) {
+    const int lo = a->B < b->B ? a->B : b->B, hi = a->B < b->B ? b->B : a->B;
+    return a->B == b->B || (lo >= 1 && (lo & (lo - 1)) == 0 && hi % lo == 0);
+}
+
 int aesfhe_tensor(aesfhe_engine *e, const aesfhe_ct *a0, const aesfhe_ct *b0, aesfhe_ct **out) {
     if (a0->npoly != 2 || b0->npoly != 2) return fail(AESFHE_EDEGREE, "tensor inputs should have 2 polynomials");
-    if (!bcast_ok(a0, b0)) return fail(AESFHE_EARG, "batch mismatch");
+    if (!cyclic_ok(a0, b0)) return fail(AESFHE_EARG, "batch mismatch");
     aesfhe_ct *a, *b;
     align2(e, a0, b0, &a, &b);
     int B = a->B > b->B ? a->B : b->B;

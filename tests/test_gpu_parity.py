@@ -435,3 +435,30 @@ def test_poly2_int_sbox_shape_bit_exact(product_lib, oracle_lib, gpu_available):
         res.append(eng.poly2_int(xb, yb, W, 64, k["rlk"]))
     for a, b in zip(*res):
         _same(g, o, a, b)
+
+
+@pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=6, special_primes=3, seed=13)],
+                         ids=["n4096", "n65536"])
+def test_cyclic_broadcast_mul_bit_exact(product_lib, oracle_lib, gpu_available, kw):
+    """aesfhe_mul with a smaller power-of-two batch cycled through (element i takes element
+    i mod B_small: the sliced AES state's batch-4 round keys), at N = 2^12 (tensor + relinearise)
+    and N = 2^16 (the fused product: cycled reads in the INTT copy-in and the key-switch
+    prologue), either operand order, against the oracle; a non-dividing batch is refused."""
+    g, o = _pair(product_lib, oracle_lib, **kw)
+    rng = np.random.default_rng(21)
+    z8, z4, z2 = (rng.uniform(-1, 1, (b, g.slot_count)) for b in (8, 4, 2))
+    res, sks = [], []
+    for eng in (g, o):
+        k = _keys(eng)
+        a8, a4, a2 = (eng.encrypt(z, k["pk"], level=lv) for z, lv in ((z8, 6), (z4, 6), (z2, 5)))
+        res.append([eng._call_ct(eng._lib.mul, a8._h, a4._h, k["rlk"]._h),
+                    eng._call_ct(eng._lib.mul, a2._h, a8._h, k["rlk"]._h)])
+        sks.append(k["sk"])
+        b6, b3 = eng.encrypt(z8[:6], k["pk"]), eng.encrypt(z8[:3], k["pk"])  # held: handles stay valid
+        with pytest.raises(RuntimeError, match="batch mismatch"):
+            eng._call_ct(eng._lib.mul, b6._h, b3._h, k["rlk"]._h)
+    for cg, co in zip(*res):
+        _same(g, o, cg, co)
+    idx = np.arange(8)
+    np.testing.assert_allclose(g.decrypt(res[0][0], sks[0]).real, z8 * z4[idx % 4], atol=1e-5)
+    np.testing.assert_allclose(g.decrypt(res[0][1], sks[0]).real, z2[idx % 2] * z8, atol=1e-5)

@@ -286,3 +286,18 @@ def test_digit_width_oracle(oracle_lib):
     assert np.all(errs[12] < 2 * errs[0] + 1e-9)
     with pytest.raises(RuntimeError, match="exceeds P"):
         Engine(log_n=10, max_level=30, special_primes=10, scale_bits=40, digit_primes=16, seed=3, _lib=oracle_lib)
+
+
+def test_cyclic_broadcast_mul_oracle(oracle_lib):
+    """aesfhe_mul cycles through a smaller power-of-two batch (element i takes i mod B_small)."""
+    from aes_xor_fhe.fhe import Engine
+    e = Engine(log_n=10, max_level=4, special_primes=2, seed=5, _lib=oracle_lib)
+    sk = e.create_secret_key(1)
+    pk, rlk = e.create_public_key(sk), e.create_relinearization_key(sk)
+    rng = np.random.default_rng(2)
+    z8, z4 = rng.uniform(-1, 1, (8, e.slot_count)), rng.uniform(-1, 1, (4, e.slot_count))
+    out = e.multiply(e.encrypt(z8, pk), e.encrypt(z4, pk), rlk)
+    assert out.batch == 8
+    np.testing.assert_allclose(np.real(e.decrypt(out, sk)), z8 * z4[np.arange(8) % 4], atol=1e-6)
+    with pytest.raises(RuntimeError, match="batch mismatch"):
+        e.multiply(e.encrypt(z8[:6], pk), e.encrypt(z4[:3], pk), rlk)
