@@ -130,6 +130,9 @@ SIGNATURES = [
     ("aesfhe_poly2_int", C.c_int,
      [c_eng_p, _P(c_ct_p), C.c_int32, _P(c_ct_p), C.c_int32, _P(C.c_int32), C.c_int32,
       C.c_int32, c_key_p, _P(c_ct_p)]),
+    ("aesfhe_poly2_int_rot", C.c_int,
+     [c_eng_p, _P(c_ct_p), C.c_int32, _P(c_ct_p), C.c_int32, _P(C.c_int32), C.c_int32,
+      C.c_int32, c_key_p, C.c_int32, _P(c_ct_p)]),
     ("aesfhe_key_secret_sparse", C.c_int, [c_eng_p, C.c_uint64, C.c_int32, _P(c_key_p)]),
     ("aesfhe_key_switch", C.c_int, [c_eng_p, c_key_p, c_key_p, _P(c_key_p)]),
     ("aesfhe_mod_raise", C.c_int, [c_eng_p, c_ct_p, C.c_int32, _P(c_ct_p)]),

@@ -470,8 +470,42 @@ class AESSlicedRound(AESRowRound):
             k = self.e.level_down(k, a.level)
         return self.mul(a, k)
 
+    def sub_bytes_shift_rows(self, bits) -> List[List[Ciphertext]]:
+        """SubBytes with ShiftRows folded into the S-box polynomial's output order: row r's
+        outputs are written rotated by r within each slab (aesfhe_poly2_int_rot) -- no gather, no
+        key switch: ShiftRows costs nothing."""
+        out = []
+        for r, row in enumerate(bits):
+            mh = self.monomials(row[4:8])
+            ml = self.monomials(row[0:4])
+            out.append(self.e.poly2_int([mh[i] for i in range(1, 16)], [ml[j] for j in range(1, 16)],
+                                        self.W64, 64, self.rlk, slab_rot=r))
+        return out
+
+    def round(self, bits, key, timings: dict | None = None):
+        """SubBytes + ShiftRows (one step, sub_bytes_shift_rows) -> MixColumns -> AddRoundKey."""
+        import time
+        t0 = time.perf_counter()
+        A = self.sub_bytes_shift_rows(bits)
+        if timings is not None:
+            self.e.materialize(A)
+            self.e.synchronize()
+            t1 = time.perf_counter()
+            timings["sub_bytes_shift_rows"] = timings.get("sub_bytes_shift_rows", 0.0) + t1 - t0
+        out = self.mix_columns_add_round_key(A, key)
+        if timings is not None:
+            self.e.materialize(out)
+            self.e.synchronize()
+            timings["mix_columns_add_round_key"] = timings.get("mix_columns_add_round_key", 0.0) + time.perf_counter() - t1
+        return out
+
+    def final_round(self, bits, key):
+        """SubBytes + ShiftRows -> AddRoundKey (AES round 10)."""
+        return self.add_round_key(self.sub_bytes_shift_rows(bits), key)
+
     def shift_rows(self, bits):
-        """out(r, c) = in(r, c + r): element 4 s + c of row r takes element 4 s + (c + r) mod 4."""
+        """out(r, c) = in(r, c + r): element 4 s + c of row r takes element 4 s + (c + r) mod 4
+        (a gather; the round folds it into SubBytes instead, sub_bytes_shift_rows)."""
         S = bits[0][0].batch // 4
         out = [bits[0]]
         for r in (1, 2, 3):

@@ -843,9 +843,10 @@ class Engine:
         return [self._ct(outs[i]) for i in range(m)]
 
     def poly2_int(self, x_basis: Sequence[Ciphertext], y_basis: Sequence[Ciphertext], weights,
-                  den: int, relinearization_key: RelinearizationKey) -> list:
+                  den: int, relinearization_key: RelinearizationKey, slab_rot: int = 0) -> list:
         """poly2 with integer-weight coefficients C = weights / den (aesfhe_poly2_int): exact
-        integer inner sums, one constant per pair of basis levels."""
+        integer inner sums, one constant per pair of basis levels.  slab_rot (aesfhe_poly2_int_rot):
+        output element 4 s + c takes the value at input element 4 s + ((c + slab_rot) mod 4)."""
         Wi = np.asarray(weights)
         if Wi.ndim == 2:
             Wi = Wi[None]
@@ -858,8 +859,12 @@ class Engine:
         xa = (c_ct_p * max(nx - 1, 1))(*[c._h for c in x_basis])
         ya = (c_ct_p * max(ny - 1, 1))(*[c._h for c in y_basis])
         outs = (c_ct_p * m)()
-        self._check(self._lib.poly2_int(self._h, xa, nx, ya, ny, _as_ptr(Wi, C.c_int32), int(den), m,
-                                        relinearization_key._h, outs))
+        if slab_rot:
+            self._check(self._lib.poly2_int_rot(self._h, xa, nx, ya, ny, _as_ptr(Wi, C.c_int32), int(den), m,
+                                                relinearization_key._h, int(slab_rot), outs))
+        else:
+            self._check(self._lib.poly2_int(self._h, xa, nx, ya, ny, _as_ptr(Wi, C.c_int32), int(den), m,
+                                            relinearization_key._h, outs))
         return [self._ct(outs[i]) for i in range(m)]
 
     def align(self, cts: Sequence[Ciphertext], level: int | None = None) -> list:

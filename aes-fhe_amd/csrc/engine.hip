@@ -3038,8 +3038,26 @@ extern "C" int aesfhe_poly2(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_
 // first); cy likewise.  H(cx, cy) = llround(S1 * r_x * r_y / den) mod q, times R = llround(D_l)
 // for cx = 0 and again for cy = 0, with S1, r_x, r_y as in aesfhe_poly2; F_ij = w_ij * H mod q.
 // Output: level l - 2, scale exactly D_{l-2} (up to the rounding of H).
+static void poly2_int_impl(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_t nx, const aesfhe_ct* const* yb,
+                           int32_t ny, const int32_t* w, int32_t den, int32_t m, const aesfhe_key* rlk,
+                           aesfhe_ct** outs, int slab_rot);
 extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_t nx, const aesfhe_ct* const* yb, int32_t ny, const int32_t* w, int32_t den, int32_t m, const aesfhe_key* rlk, aesfhe_ct** outs) {
     API_BEGIN
+    poly2_int_impl(e, xb, nx, yb, ny, w, den, m, rlk, outs, 0);
+    API_END
+}
+// the same with every output's batch rotated within slabs of 4: element 4 s + c of output t takes
+// the polynomial's value at input element 4 s + ((c + slab_rot) mod 4) (the sliced AES state's
+// ShiftRows of row r = slab_rot folded into its S-box)
+extern "C" int aesfhe_poly2_int_rot(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_t nx, const aesfhe_ct* const* yb, int32_t ny, const int32_t* w, int32_t den, int32_t m, const aesfhe_key* rlk, int32_t slab_rot, aesfhe_ct** outs) {
+    API_BEGIN
+    if (slab_rot < 0 || slab_rot > 3) throw_err(AESFHE_EARG, "slab rotation %d outside 0..3", slab_rot);
+    poly2_int_impl(e, xb, nx, yb, ny, w, den, m, rlk, outs, slab_rot);
+    API_END
+}
+static void poly2_int_impl(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_t nx, const aesfhe_ct* const* yb,
+                           int32_t ny, const int32_t* w, int32_t den, int32_t m, const aesfhe_key* rlk,
+                           aesfhe_ct** outs, int slab_rot) {
     if (nx < 1 || ny < 1 || nx > kPoly2Max || ny > kPoly2Max || m < 1)
         throw_err(AESFHE_EARG, "poly2 needs 1 <= nx, ny <= %d and m >= 1", kPoly2Max);
     if (nx + ny < 3) throw_err(AESFHE_EARG, "poly2 needs at least one basis ciphertext");
@@ -3059,6 +3077,7 @@ extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, in
     for (int j = 0; j < ny - 1; j++)
         if (yb[j]->B != B && yb[j]->B != 1) throw_err(AESFHE_EARG, "batch mismatch");
     if (l < 2) throw_err(AESFHE_ELEVEL, "no level left for a bivariate polynomial");
+    if (slab_rot && B % 4) throw_err(AESFHE_EARG, "slab rotation needs a batch of whole slabs (4 s), got %d", B);
     // wfac bounds an inner sum a = w_0 c0 + sum_j w_j y'_j (c0 < q, |y'| <= q/2 + 1) by wfac * q:
     // a limb takes the exact-FMA kernel (no folds) when wfac * q < 2^52, else the folding one
     double wfac = 1.0;
@@ -3184,7 +3203,7 @@ extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, in
                     auto kern = big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max, mo> : k_poly2_int<true, 0, mo>)
                                     : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max, mo> : k_poly2_int<false, 0, mo>);
                     hipLaunchKernelGGL(kern, dim3(N / 256, lb - la, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny,
-                                       (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, ml, t0, std::min(mo, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN);
+                                       (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, ml, t0, std::min(mo, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN, slab_rot);
                     la = lb;
                 }
         }
@@ -3196,7 +3215,6 @@ extern "C" int aesfhe_poly2_int(aesfhe_engine* e, const aesfhe_ct* const* xb, in
     }
     for (int t = 0; t < m; t++)
         if (!outs[t]) outs[t] = ct_zero_new(e, B, 2, l - 2);
-    API_END
 }
 
 // -----------------------------------------------------------------------------------------------

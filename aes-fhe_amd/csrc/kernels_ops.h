@@ -912,7 +912,7 @@ __global__ void __launch_bounds__(256, MO > 4 ? 2 : 3) k_poly2_int(const u64* co
                         int cyn, const double* __restrict__ Wt, const TwD* __restrict__ Rt,
                         const double* __restrict__ C0, int mtot, int t0, int mc,
                         u64* __restrict__ out, long oos, long obs, const u64* __restrict__ qs,
-                        const double* __restrict__ qinv, int l0, int nl, int logN) {
+                        const double* __restrict__ qinv, int l0, int nl, int logN, int orot) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int l = l0 + blockIdx.y, bb = blockIdx.z;
     const double q = (double)qs[l];
@@ -993,7 +993,10 @@ __global__ void __launch_bounds__(256, MO > 4 ? 2 : 3) k_poly2_int(const u64* co
         }
     }
     }
-    u64* o = out + (long)bb * obs + off;
+    // orot (aesfhe_poly2_int_rot): element 4 s + c of each output takes input element
+    // 4 s + ((c + orot) & 3) -- the output written rotated within its slab of 4
+    const int ob = (bb & ~3) | ((bb - orot) & 3);
+    u64* o = out + (long)ob * obs + off;
     const long pstr = (long)nl << logN;
 #pragma unroll
     for (int t = 0; t < MO; t++) {

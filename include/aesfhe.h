@@ -341,6 +341,14 @@ int aesfhe_poly2(aesfhe_engine *eng, const aesfhe_ct *const *xb, int32_t nx,
 int aesfhe_poly2_int(aesfhe_engine *eng, const aesfhe_ct *const *xb, int32_t nx,
                      const aesfhe_ct *const *yb, int32_t ny, const int32_t *w, int32_t den,
                      int32_t m, const aesfhe_key *rlk, aesfhe_ct **outs);
+/* aesfhe_poly2_int with each output's batch rotated within slabs of 4 (batch a multiple of 4):
+ * element 4s + c of an output holds the polynomial at input element 4s + ((c + slab_rot) mod 4),
+ * slab_rot in 0..3.  The sliced AES state (aes_round_bits.AESSlicedRound) folds ShiftRows of
+ * row r -- a rotation in the reference's layouts (shiftrows_service.py:33-51) -- into that
+ * row's S-box this way. */
+int aesfhe_poly2_int_rot(aesfhe_engine *eng, const aesfhe_ct *const *xb, int32_t nx,
+                         const aesfhe_ct *const *yb, int32_t ny, const int32_t *w, int32_t den,
+                         int32_t m, const aesfhe_key *rlk, int32_t slab_rot, aesfhe_ct **outs);
 
 /* ---- bootstrapping primitives (Engine.bootstrap, xor_service.py:120-129) ----------------- */
 /* ModRaise: limb 0 of ct (mod q_0, centred) lifted to every limb of `level`; the result encrypts

@@ -2441,6 +2441,31 @@ int aesfhe_poly2_int(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, c
     return 0;
 }
 
+/* aesfhe_poly2_int, then each output's batch rotated within slabs of 4 (include/aesfhe.h) */
+int aesfhe_poly2_int_rot(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, const aesfhe_ct *const *yb,
+                         int32_t ny, const int32_t *w, int32_t den, int32_t m, const aesfhe_key *rlk,
+                         int32_t slab_rot, aesfhe_ct **outs) {
+    if (slab_rot < 0 || slab_rot > 3) return fail(AESFHE_EARG, "slab rotation %d outside 0..3", slab_rot);
+    int B = 1;
+    for (int i = 0; i < nx - 1; i++) B = xb[i]->B > B ? xb[i]->B : B;
+    for (int j = 0; j < ny - 1; j++) B = yb[j]->B > B ? yb[j]->B : B;
+    if (slab_rot && B % 4) return fail(AESFHE_EARG, "slab rotation needs a batch of whole slabs (4 s), got %d", B);
+    int rc = aesfhe_poly2_int(e, xb, nx, yb, ny, w, den, m, rlk, outs);
+    if (rc || !slab_rot) return rc;
+    for (int t = 0; t < m; t++) {
+        aesfhe_ct *c = outs[t];
+        const size_t per = (size_t)c->npoly * (c->level + 1) * e->N;
+        u64 *tmp = malloc(sizeof(u64) * per * c->B);
+        for (int b = 0; b < c->B; b++) {
+            const int src = (b & ~3) | ((b + slab_rot) & 3);
+            memcpy(tmp + per * b, c->data + per * src, sizeof(u64) * per);
+        }
+        memcpy(c->data, tmp, sizeof(u64) * per * c->B);
+        free(tmp);
+    }
+    return 0;
+}
+
 /* ModRaise (include/aesfhe.h aesfhe_mod_raise) */
 int aesfhe_mod_raise(aesfhe_engine *e, const aesfhe_ct *c, int32_t level, aesfhe_ct **out) {
     if (level < 0 || level > e->L) return fail(AESFHE_EARG, "bad mod-raise level");

@@ -232,3 +232,22 @@ def test_sliced_round_full_params(product_lib, gpu_available):
         st = R.round(st, R.encrypt_round_key(rks[r]))
         ref = T.aes_round(ref, rks[r])
         assert np.array_equal(R.decrypt_blocks(st, 8), ref)
+
+
+def test_sub_bytes_shift_rows_oracle(oracle_lib):
+    """ShiftRows folded into the S-box's output order (aesfhe_poly2_int_rot) gives residue for
+    residue what SubBytes followed by the ShiftRows gather gives (the rotation commutes with the
+    batch-elementwise relinearisation)."""
+    e, R = _setup(oracle_lib, 10, seed=9, cls=AESSlicedRound)
+    rng = np.random.default_rng(14)
+    blocks = rng.integers(0, 256, (8, R.n_blk, 16), dtype=np.uint8)
+    st = R.encrypt_blocks(blocks)
+    fused = R.sub_bytes_shift_rows(st)
+    ref = R.shift_rows(R.sub_bytes(st))
+    for rf, rr in zip(fused, ref):
+        for cf, cr in zip(rf, rr):
+            assert np.array_equal(e.export_residues(cf), e.export_residues(cr))
+    assert np.array_equal(R.decrypt_blocks(fused, 8), T.shift_rows(T.sub_bytes(blocks)))
+    with pytest.raises(RuntimeError, match="whole slabs"):
+        odd = e.encrypt(np.ones((3, e.slot_count)), R.pk)
+        e.poly2_int([odd], [odd], np.ones((1, 2, 2)), 64, R.rlk, slab_rot=1)
