@@ -123,8 +123,8 @@ class AESRowRound:
         return [[self.e.encrypt(1.0 - 2.0 * ((row.astype(np.int64) >> j) & 1), self.pk, level=level)
                  for j in range(8)] for row in rows]
 
-    def encrypt_blocks(self, blocks: np.ndarray) -> List[List[Ciphertext]]:
-        return self.encrypt_bytes_rows(self.pack(blocks))
+    def encrypt_blocks(self, blocks: np.ndarray, level: int | None = None) -> List[List[Ciphertext]]:
+        return self.encrypt_bytes_rows(self.pack(blocks), level=level)
 
     def decrypt_blocks(self, bits: Sequence[Sequence[Ciphertext]], nb: int | None = None) -> np.ndarray:
         """The state's blocks (NB, n_blk, 16); nb: the number of sets encrypted (a layout that
@@ -296,6 +296,18 @@ class AESRowRound:
             lvl -= self.FINAL_DEPTH if final else self.ROUND_DEPTH
             since += 1
         return out
+
+    def fresh_level(self, L: int, bss) -> int:
+        """The lowest level a fresh state can be encrypted at (chain top L) whose schedule needs
+        no more refreshes than one from L: the first segment's spare levels (at L = 30 it reaches
+        its refresh at level 8 where StC needs 3) then go unspent, and its three rounds run on
+        fewer limbs -- 25 at L = 30 and at L = 35."""
+        def refreshes(s):
+            return sum(b is not None for _, _, b in self.schedule(s, bss))
+        n, s = refreshes(L), L
+        while s > 1 and refreshes(s - 1) == n:
+            s -= 1
+        return s
 
     def key_levels(self, L: int, bss) -> List[int]:
         """The level each of the 11 round keys is consumed at (key 0: ARK0 at L; key i: round i's

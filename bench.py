@@ -264,7 +264,11 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     # each round key encrypted at the level its product consumes it (AESRowRound.key_levels):
     # the sliced state's per-column keys are 4x the rows layout's, and at N = 2^17, L = 35 the
     # top-level set (101 GB) did not fit beside the run
-    klv = R.key_levels(L, bs)
+    # the client encrypts the states at the lowest level that keeps three refreshes
+    # (AESRowRound.fresh_level: 25 at L = 30): rounds 1-3 then run on 5 fewer limbs instead of
+    # reaching their refresh with levels to spare
+    L0 = R.fresh_level(L, bs)
+    klv = R.key_levels(L0, bs)
     keys = [R.encrypt_round_key(rk, level=lv) for rk, lv in zip(T.expand_key(key), klv)]
     rng = np.random.default_rng(2000 + rank)
     nb = args.aes10_batch
@@ -280,11 +284,11 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
         ps = eng.pool_stats()
         log(f"aes10: {msg} (pool held {ps['held'] / 1e9:.1f} GB live {ps['live'] / 1e9:.1f} GB "
             f"mallocs {ps['mallocs']} trims {ps['trims']})")
-    warm = R.encrypt_aes128(R.encrypt_blocks(rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)),
+    warm = R.encrypt_aes128(R.encrypt_blocks(rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8), level=L0),
                             keys, bs, pairs_per_call=ppc, progress=prog, consume=True)
     del warm
     blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
-    st = R.encrypt_blocks(blocks)
+    st = R.encrypt_blocks(blocks, level=L0)
     log("aes10: timed run")
     tm = {}
     barrier()
@@ -311,6 +315,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
             "bootstrap_ms_per_bit_ct": round(1e3 * tm.get("bootstrap", 0.0) / max(nref * 32 * nb, 1), 2),
             "bootstrap_setup_s": round(setup_s, 2), "verified": ok,
             "bootstrap_cts_groups": [b.cts_groups for b in bs], "round_key_levels": klv,
+            "state_level": L0,
             "block_rounds_per_s": round(10 * nb * R.n_blk * world / el, 2),
             "per_round_level_ms": tm.get("per_round"), "pool": eng.pool_stats(),
             "timed_mallocs": timed_mallocs}

@@ -31,12 +31,14 @@ def _run(lib, log_n, nb=1, seed=3, cls=AESRowRound, cts_groups=(3,), key_levels=
     blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
     blocks[0, 0] = np.frombuffer(FIPS_C1_PT, dtype=np.uint8)
     rks = T.expand_key(key)
-    # key_levels: each round key encrypted at the level its product consumes (as the bench does)
-    lv = R.key_levels(e.max_level, bs) if key_levels else [None] * 11
+    # key_levels: the state encrypted at the lowest level keeping three refreshes and each round
+    # key at the level its product consumes (as the bench does)
+    L0 = R.fresh_level(e.max_level, bs) if key_levels else None
+    lv = R.key_levels(L0, bs) if key_levels else [None] * 11
     keys = [R.encrypt_round_key(rk, level=v) for rk, v in zip(rks, lv)]
-    out, nref = R.encrypt_aes128(R.encrypt_blocks(blocks), keys, bs)
+    out, nref = R.encrypt_aes128(R.encrypt_blocks(blocks, level=L0), keys, bs)
     if key_levels:  # no level-down was needed anywhere: the state kept the schedule's levels
-        assert [l for _, l, _ in R.schedule(e.max_level, bs)][-1] == 5
+        assert L0 == 25 and [l for _, l, _ in R.schedule(L0, bs)][-1] == 5
     got = R.decrypt_blocks(out, nb)
     want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
     return got, want, nref, out
