@@ -57,6 +57,8 @@ class AESRowRound:
     """State: 4 rows x 8 +-1 bit ciphertexts (row r, bit j), each batched over NB sets of
     n_blk blocks."""
 
+    GRANULE = 1  # batch elements a shard across ranks must keep together (parallel.shard_range)
+
     def __init__(self, engine: Engine, sk, pk, rlk, cjk=None, rotation_keys=None):
         self.e = engine
         self.sk, self.pk, self.rlk, self.cjk = sk, pk, rlk, cjk
@@ -396,15 +398,19 @@ class AESSlicedRound(AESRowRound):
     Every product, the S-box polynomial, MixColumns and the bootstrap are elementwise over the
     batch exactly as before; what changes:
 
-    * ShiftRows, out(r, c) = in(r, c + r), becomes a permutation of row r's batch elements
-      (Engine.gather, one copy pass): no automorphism and no key switch, where AESRowRound
-      rotates row r by -r n_blk slots (24 key switches per 8192 blocks, ~9 % of the round's).
+    * ShiftRows, out(r, c) = in(r, c + r), becomes a permutation of row r's batch elements,
+      folded into the S-box's output order (aesfhe_poly2_int_rot, sub_bytes_shift_rows): no
+      automorphism, no key switch and no copy, where AESRowRound rotates row r by -r n_blk slots
+      (24 key switches per 8192 blocks, ~9 % of the round's).
     * The round key differs per column: its ciphertexts carry batch 4 (element c = key byte
       r + 4c); the key product cycles through them (aesfhe_mul: element 4 s + c takes key
       element c), after a level-down of the 4 elements to the state's level (key_mul).
     * The slabs, not the batch elements, are what may be split across ranks (a slab's four
-      columns must stay together): a shard of the batch is a multiple of 4 elements.
+      columns must stay together): a shard of the batch is a multiple of 4 elements
+      (GRANULE, parallel.scatter_ciphertext(..., granule=4)).
     """
+
+    GRANULE = 4
 
     def __init__(self, engine: Engine, sk, pk, rlk, cjk=None, rotation_keys=None):
         super().__init__(engine, sk, pk, rlk, cjk, rotation_keys={})

@@ -24,12 +24,18 @@ from __future__ import annotations
 import numpy as np
 
 
-def shard_range(total: int, world: int, rank: int):
-    """Contiguous [start, stop) share of `total` items for `rank` (the first total % world ranks
-    take one more)."""
-    base, extra = divmod(total, world)
+def shard_range(total: int, world: int, rank: int, granule: int = 1):
+    """Contiguous [start, stop) share of `total` items for `rank`, in whole granules of `granule`
+    items (the sliced AES state's slab of 4 batch elements: its columns must stay on one rank);
+    the first (total / granule) % world ranks take one granule more.  Raises if `total` is not a
+    whole number of granules."""
+    granule = int(granule)
+    if granule < 1 or total % granule:
+        raise ValueError(f"shard_range: {total} items are not whole granules of {granule}")
+    base, extra = divmod(total // granule, world)
     start = rank * base + min(rank, extra)
-    return start, start + base + (1 if rank < extra else 0)
+    stop = start + base + (1 if rank < extra else 0)
+    return start * granule, stop * granule
 
 
 def rank_nonce_start(rank: int) -> int:
@@ -59,9 +65,12 @@ def _check_keys(engine, group, dev):
     """Raise unless every rank's engine derives the same keys (once per engine and group)."""
     import torch
     import torch.distributed as dist
-    done = engine.__dict__.setdefault("_fp_groups", set())
-    gid = id(group)
-    if gid in done:
+    # verified groups are held by weak reference: a destroyed group whose id() is reused by a
+    # new one is checked again
+    import weakref
+    done = engine.__dict__.setdefault("_fp_groups", weakref.WeakSet())
+    key = group if group is not None else dist.distributed_c10d._get_default_group()
+    if key in done:
         return
     mine = torch.tensor([engine.key_fingerprint()], dtype=torch.int64, device=dev)
     allf = [torch.empty_like(mine) for _ in range(dist.get_world_size(group))]
@@ -69,7 +78,7 @@ def _check_keys(engine, group, dev):
     if len({int(t.item()) for t in allf}) != 1:
         raise RuntimeError("ranks hold engines with different keys (engine seed / prime chain): "
                            "create every rank's Engine with one shared seed (parallel.shared_seed)")
-    done.add(gid)
+    done.add(key)
 
 
 def _torch_device(engine, group=None):
@@ -112,10 +121,12 @@ def _words(engine, npoly, level):
     return npoly * (level + 1) * (1 << engine.log_coeff_count)
 
 
-def scatter_ciphertext(engine, ct, src: int = 0, group=None):
+def scatter_ciphertext(engine, ct, src: int = 0, group=None, granule: int = 1):
     """Split a batched ciphertext held by rank `src` across all ranks along the batch dimension
-    (shard_range: uneven batches allowed).  Non-source ranks pass ct=None.  Returns this rank's
-    share (None for a rank whose share is empty)."""
+    (shard_range: uneven batches allowed, in whole granules of `granule` elements -- 4 for the
+    sliced AES state, AESSlicedRound.GRANULE).  Non-source ranks pass ct=None.  Returns this
+    rank's share (None for a rank whose share is empty).  Raises on every rank if the batch is not
+    a whole number of granules."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
@@ -126,21 +137,22 @@ def scatter_ciphertext(engine, ct, src: int = 0, group=None):
         meta = torch.tensor([ct.batch, ct.npoly, ct.level], dtype=torch.int64, device=dev)
     dist.broadcast(meta, src, group=group)
     batch, npoly, level = (int(x) for x in meta.cpu())
+    shares = [shard_range(batch, world, r, granule) for r in range(world)]  # raises alike everywhere
     per = _words(engine, npoly, level)
-    smax = -(-batch // world)  # padded share: scatter needs equal sizes
+    smax = max(b - a for a, b in shares)  # padded share: scatter needs equal sizes
     out = torch.empty((smax, per), dtype=torch.int64, device=dev)
     parts = None
     if rank == src:
         parts = []
         for r in range(world):
-            a, b = shard_range(batch, world, r)
+            a, b = shares[r]
             t = torch.empty((smax, per), dtype=torch.int64, device=dev)
             _sync(dev)
             if b > a:
                 _export(engine, ct, t, a, b - a)
             parts.append(t)
     dist.scatter(out, parts, src=src, group=group)
-    a, b = shard_range(batch, world, rank)
+    a, b = shares[rank]
     if b == a:
         return None
     _sync(dev)  # RCCL wrote `out` on torch's stream

@@ -172,7 +172,69 @@ def parse():
                          "the PMC records between them)")
     ap.add_argument("--no-harness", action="store_true",
                     help="skip the reference-harness leg (full_round on 32768 bytes, xor_cipher)")
+    ap.add_argument("--launch-timeout", type=float, default=0.0,
+                    help="--gpus N > 1 started without torchrun: kill the ranks after this many seconds (0: none)")
+    ap.add_argument("--selftest-launch", action="store_true",
+                    help="launcher self-test: every rank only joins the process group (gloo) and rank 0 "
+                         "reports the world size; no GPU is touched")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`--gpus N > 1` run without torchrun (no WORLD_SIZE): start the N ranks as CHILD processes
+    of `python -m torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1), wait for
+    them, print rank 0's JSON line and return the exit status -- non-zero if any rank failed, the
+    JSON line is missing, or --launch-timeout expired (the whole process group is killed then).
+    This process imports no torch and makes no HIP call, so it never initialises the GPU and
+    never execs (the driver may run `python bench.py --gpus 8` as well as the torchrun form)."""
+    import signal
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "bench.py"), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only (RCCL between ranks)
+    env.setdefault("OMP_NUM_THREADS", "1")  # torchrun's default per rank, stated explicitly
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, start_new_session=True)
+    try:
+        out, _ = proc.communicate(timeout=args.launch_timeout or None)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        proc.communicate()
+        log(f"ranks killed after {args.launch_timeout:.0f} s")
+        return 124
+    lines = [ln for ln in out.decode(errors="replace").splitlines() if ln.startswith("{")]
+    if proc.returncode != 0 or not lines:
+        log(f"ranks failed (exit {proc.returncode}, {len(lines)} JSON lines)")
+        return proc.returncode or 1
+    print(lines[-1], flush=True)
+    return 0
+
+
+def selftest_launch(world, rank):
+    """--selftest-launch: join the process group on gloo (CPU only), agree on the world size with
+    an all-reduce, and report it from rank 0 in the bench line's shape."""
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t = torch.ones(1, dtype=torch.int64)
+        dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "blocks/s", "n_gpus": int(t.item()),
+                              "selftest": True, "backend": dist.get_backend()}), flush=True)
+    finally:
+        dist.destroy_process_group()
 
 
 class RoundDriver:
@@ -495,22 +557,25 @@ def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
     one round per rank, gathered and verified on rank 0.  Times: scatter and gather of the
     whole state (32 bit ciphertexts per set at the round's input/output levels)."""
     from aes_xor_fhe import aes_tables as T
-    from aes_xor_fhe.parallel import gather_ciphertext, scatter_ciphertext
+    from aes_xor_fhe.parallel import gather_ciphertext, scatter_ciphertext, shard_range
     rk = np.random.default_rng(31).integers(0, 256, 16, dtype=np.uint8)
-    # one set per rank (sliced layout: one slab = 4 sets per rank, its columns stay together)
+    # one set per rank (sliced layout: one slab = 4 sets per rank, its columns stay together);
+    # world > 1 adds one granule to rank 0's share, so the shares are uneven
+    gran = getattr(drv.R, "GRANULE", 1)
     per_rank = 4 if drv.layout == "sliced" else 1
-    nsets = per_rank * world
+    nsets = per_rank * world + (per_rank if world > 1 else 0)
     blocks = np.random.default_rng(77).integers(0, 256, (nsets, drv.n_blk, 16), dtype=np.uint8)
     cts = drv.cts(drv.encrypt(blocks)) if rank == 0 else [None] * (2 if drv.layout == "bytes" else 32)
+    cts_batch = nsets if drv.layout != "sliced" else 4 * drv.R.slabs(nsets)
     key = drv.key(rk)
     # untimed warm-up: the first RCCL collective sets up the communicator (hundreds of ms), which
     # is not part of the data path's rate
-    warm = scatter_ciphertext(eng, cts[0])
+    warm = scatter_ciphertext(eng, cts[0], granule=gran)
     warm = gather_ciphertext(eng, warm)
     del warm
     barrier()
     t0 = time.perf_counter()
-    mine = [scatter_ciphertext(eng, c) for c in cts]
+    mine = [scatter_ciphertext(eng, c, granule=gran) for c in cts]
     barrier()
     t_sc = allmax(time.perf_counter() - t0)
     bytes_in = sum(c.batch * c.npoly * (c.level + 1) for c in mine) * 8 * (1 << eng.log_coeff_count)
@@ -524,7 +589,9 @@ def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
     ok = None
     if rank == 0 and args.check:
         ok = bool(np.array_equal(drv.decrypt(drv.from_cts(full), nsets), T.aes_round(blocks, rk)))
-    return {"sets": nsets, "bytes_per_rank_in": bytes_in, "scatter_ms": round(t_sc * 1e3, 2),
+    return {"sets": nsets, "granule": gran, "batch_per_rank": [shard_range(cts_batch, world, r, gran)
+                                                                for r in range(world)],
+            "bytes_per_rank_in": bytes_in, "scatter_ms": round(t_sc * 1e3, 2),
             "gather_ms": round(t_ga * 1e3, 2),
             "scatter_gbs_per_rank": round(bytes_in / t_sc / 1e9, 2) if t_sc else None,
             "verified": ok, "backend": _dist_backend(),
@@ -662,9 +729,20 @@ def cpu_config_legs(args, lib, threads):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        log(f"--gpus {args.gpus}: need at least one")
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args)  # before anything imports torch or touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE {world} but --gpus {args.gpus}: one rank per GPU, the two must agree")
+        return 2
+    if args.selftest_launch:
+        selftest_launch(world, rank)
+        return 0
     import torch
     dist = None
     # one rank per GPU; more ranks than GPUs (a multi-rank rehearsal on a 1-GPU box) share them
@@ -819,6 +897,7 @@ def main():
             "value": round(value, 2),
             "unit": "blocks/s",
             "n_gpus": world,
+            "visible_devices": ndev,  # < n_gpus only in a rehearsal where ranks share a GPU (gloo)
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -873,7 +952,8 @@ def main():
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -101,9 +101,10 @@ def _worker_rows(rank, world, port, so, result_q):
 
 def _worker_sliced(rank, world, port, so, result_q):
     """The bench's default state (AESSlicedRound, 12-prime digits over K = 10): rank 0 encrypts
-    two slabs (8 sets), each rank receives one slab (its 4 columns together), runs one round
-    (ShiftRows as a batch gather, the batch-4 round key repeated), and rank 0 gathers and checks
-    FIPS-197."""
+    three slabs (12 sets, the last one partly padding), scattered in whole slabs
+    (granule = AESSlicedRound.GRANULE = 4: rank 0 gets two slabs, rank 1 one -- an element split
+    would put a slab's columns on two ranks), each rank runs one round (ShiftRows folded into the
+    S-box, the batch-4 round key read cyclically), and rank 0 gathers and checks FIPS-197."""
     sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -118,12 +119,12 @@ def _worker_sliced(rank, world, port, so, result_q):
                    seed=5, nonce_start=rank_nonce_start(rank), thread_count=4)
         sk = e.create_secret_key(1)
         R = AESSlicedRound(e, sk, e.create_public_key(sk), e.create_relinearization_key(sk))
-        nsets = 4 * world
+        nsets = 4 * (world + 1) - 1  # 3 slabs over 2 ranks, the last one padded by one set
         blocks = np.random.default_rng(12).integers(0, 256, (nsets, R.n_blk, 16), dtype=np.uint8)
         rk = np.random.default_rng(13).integers(0, 256, 16, dtype=np.uint8)
         st = R.encrypt_blocks(blocks) if rank == 0 else [[None] * 8 for _ in range(4)]
-        mine = [[scatter_ciphertext(e, c) for c in row] for row in st]
-        assert all(c.batch == 4 for row in mine for c in row)
+        mine = [[scatter_ciphertext(e, c, granule=R.GRANULE) for c in row] for row in st]
+        assert all(c.batch == (8 if rank == 0 else 4) for row in mine for c in row)
         out = R.round(mine, R.encrypt_round_key(rk))
         full = [[gather_ciphertext(e, c) for c in row] for row in out]
         if rank == 0:
@@ -188,6 +189,39 @@ def test_shard_range():
     from aes_xor_fhe.parallel import shard_range
     parts = [shard_range(10, 4, r) for r in range(4)]
     assert parts == [(0, 3), (3, 6), (6, 8), (8, 10)]
+    # whole slabs of 4: 3 slabs over 2 ranks -> 2 + 1, never 6 + 6
+    assert [shard_range(12, 2, r, 4) for r in range(2)] == [(0, 8), (8, 12)]
+    assert [shard_range(8, 3, r, 4) for r in range(3)] == [(0, 4), (4, 8), (8, 8)]
+    with pytest.raises(ValueError, match="whole granules"):
+        shard_range(10, 2, 0, 4)
+
+
+def _bench(*argv, env=None, timeout=300):
+    import subprocess
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *argv], capture_output=True, text=True,
+                          env=e, timeout=timeout, cwd=str(ROOT))
+
+
+def test_bench_launcher_starts_n_ranks():
+    """`python bench.py --gpus 2` (no torchrun) starts two ranks as child processes through
+    torch.distributed.run and prints rank 0's line, which reports n_gpus 2 (--selftest-launch:
+    the ranks only join the gloo group and all-reduce their count; no GPU, no engine)."""
+    import json
+    r = _bench("--gpus", "2", "--selftest-launch")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["selftest"] is True
+
+
+def test_bench_launcher_rejects_mismatch():
+    """A rank whose WORLD_SIZE differs from --gpus exits non-zero instead of timing a different
+    world than it reports."""
+    r = _bench("--gpus", "1", "--selftest-launch", env={"WORLD_SIZE": "2"}, timeout=60)
+    assert r.returncode == 2 and "must agree" in r.stderr
 
 
 def test_two_rank_shared_seed_and_key_check(oracle_lib):
