@@ -42,9 +42,12 @@ class Params(C.Structure):
 
 # (name, restype, argtypes) for every symbol of include/aesfhe.h
 _P = C.POINTER
+ABI_VERSION = 4  # include/aesfhe.h AESFHE_ABI_VERSION
+
 SIGNATURES = [
     ("aesfhe_last_error", C.c_char_p, []),
     ("aesfhe_backend_name", C.c_char_p, []),
+    ("aesfhe_abi_version", C.c_int32, []),
     ("aesfhe_engine_create", C.c_int, [_P(Params), _P(c_eng_p)]),
     ("aesfhe_engine_destroy", None, [c_eng_p]),
     ("aesfhe_engine_dims", C.c_int, [c_eng_p, _P(C.c_int32)]),
@@ -167,6 +170,9 @@ class Lib:
             fn.argtypes = args
             setattr(self, name[len("aesfhe_"):], fn)
         self.backend = self.backend_name().decode()
+        if self.abi_version() != ABI_VERSION:  # a library built against another header revision
+            raise RuntimeError(f"{self.path}: C ABI revision {self.abi_version()}, this package needs "
+                               f"{ABI_VERSION} (include/aesfhe.h AESFHE_ABI_VERSION): rebuild it")
 
     def check(self, rc: int) -> None:
         if rc != 0:

@@ -217,7 +217,7 @@ class _ProductCiphertext(Ciphertext):
     of them), the reference's per-coefficient loop of xor_service.py:271-286 in one launch
     sequence."""
 
-    __slots__ = ("_a", "_b", "_rlk", "_mat")
+    __slots__ = ("_a", "_b", "_rlk", "_mat", "__weakref__")
 
     def __init__(self, engine: "Engine", a: Ciphertext, b: Ciphertext, rlk):
         self._lib, self._free = engine._lib, None
@@ -232,6 +232,7 @@ class _ProductCiphertext(Ciphertext):
             e = self.engine
             self._mat = e._call_ct(e._lib.mul, self._a._h, self._b._h, self._rlk._h)
             self._a = self._b = None  # release the operands
+            e._pending.discard(self)
         return self._mat._h
 
     @property
@@ -329,7 +330,12 @@ class Engine:
     its result are deferred and materialised as one fused linear combination
     (``_LinearCiphertext``), and ``multiply(a, b, rlk)`` is deferred to its first use
     (``_ProductCiphertext``) so that products scaled by constants and summed become one fused
-    bivariate evaluation; False evaluates every call eagerly (a rescale per product).
+    bivariate evaluation; False evaluates every call eagerly (a rescale per product).  What can
+    be checked at the call is checked there (operand levels, batch shapes, polynomial counts, the
+    key's type and owning engine); an error of the evaluation itself (out of device memory, a
+    device fault) surfaces at the first use of the deferred handle, as a RuntimeError naming the
+    C call.  At most ``max_pending`` products (default 256) wait unevaluated per engine: the
+    next one evaluates the waiting ones first, which bounds the operands they keep alive.
 
     Randomness: without ``seed`` the engine seed, every secret key created without a seed and
     the first encryption nonce are drawn from os.urandom.  With an explicit ``seed`` everything
@@ -345,7 +351,8 @@ class Engine:
                  special_primes: int | None = None, scale_bits: int | None = None,
                  base_bits: int | None = None, special_bits: int | None = None,
                  seed: int | bytes | None = None, nonce_start: int | None = None,
-                 fuse_linear: bool = True, digit_primes: int | None = None, _lib: Lib | None = None):
+                 fuse_linear: bool = True, digit_primes: int | None = None, max_pending: int = 256,
+                 _lib: Lib | None = None):
         ints = [a for a in args if isinstance(a, (int, np.integer)) and not isinstance(a, bool)]
         strs = [a for a in args if isinstance(a, str)]
         if strs:
@@ -396,6 +403,9 @@ class Engine:
         self.scales = [float(x) for x in scales]
         self._random_keys = seed is None
         self._fuse_linear = bool(fuse_linear)
+        import weakref
+        self._pending = weakref.WeakSet()  # deferred products not yet evaluated
+        self._max_pending = int(max_pending)
         if nonce_start is None:
             nonce_start = _urandom64() >> 1 if seed is None else 0
         self._nonce = int(nonce_start)
@@ -536,12 +546,25 @@ class Engine:
 
     def encrypt(self, data, key, level: int | None = None) -> Ciphertext:
         """Encrypt a slot vector (or a (B, <=slots) array as one batched ciphertext) under a
-        public key (or, symmetrically, the secret key), zero-padded to slot_count."""
+        public key (or, symmetrically, the secret key), zero-padded to slot_count
+        (engine_context.py:81-85, xor_service.py:59-66).  The HIP engine copies the slots to the
+        GPU once and encodes + encrypts there (encrypt_device: the device codec is bit-identical
+        to the host one, same nonce sequence); the CPU oracle encodes on the host."""
         level = self.max_level if level is None else int(level)
         arr = np.asarray(data)
         rows = arr[None, :] if arr.ndim == 1 else arr
         if rows.ndim != 2 or rows.shape[1] > self.slot_count:
             raise ValueError(f"data must be (<= {self.slot_count},) or (B, <= {self.slot_count})")
+        if self.on_device:
+            import torch
+            src = rows if np.iscomplexobj(rows) else rows.astype(np.float64, copy=False)
+            return self.encrypt_device(torch.from_numpy(np.ascontiguousarray(src)), key, level)
+        return self._encrypt_host(rows, key, level)
+
+    def _encrypt_host(self, rows: np.ndarray, key, level: int) -> Ciphertext:
+        """encrypt with the host codec (aesfhe_encode on the CPU, then aesfhe_encrypt)."""
+        rows = np.asarray(rows)
+        rows = rows[None, :] if rows.ndim == 1 else rows
         n = 1 << self.log_coeff_count
         co = np.empty((rows.shape[0], n), dtype=np.int64)
         for b in range(rows.shape[0]):
@@ -554,6 +577,15 @@ class Engine:
         return self._ct(out.value)
 
     def decrypt(self, ct: Ciphertext, sk: SecretKey) -> np.ndarray:
+        """Slot values of `ct` ((slot_count,) complex, or (B, slot_count) for a batch).  The HIP
+        engine decrypts and decodes on the GPU (decrypt_device) and copies the slots back once."""
+        if self.on_device:
+            out = self.decrypt_device(ct, sk).cpu().numpy()
+            return out[0] if ct.batch == 1 else out
+        return self._decrypt_host(ct, sk)
+
+    def _decrypt_host(self, ct: Ciphertext, sk: SecretKey) -> np.ndarray:
+        """decrypt with the host codec (aesfhe_decrypt's coefficients decoded on the CPU)."""
         n = 1 << self.log_coeff_count
         co = np.empty((ct.batch, n), dtype=np.int64)
         self._check(self._lib.decrypt(self._h, sk._h, ct._h, _as_ptr(co, C.c_int64)))
@@ -606,10 +638,16 @@ class Engine:
     def multiply(self, a, b, relinearization_key: RelinearizationKey | None = None) -> Ciphertext:
         if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
             if relinearization_key is not None:
+                if getattr(relinearization_key, "engine", self) is not self:
+                    raise ValueError("multiply: the relinearization key belongs to another engine")
                 if (self._fuse_linear and a.npoly == 2 and b.npoly == 2 and min(a.level, b.level) >= 1
                         and (a.batch == b.batch or 1 in (a.batch, b.batch))
                         and isinstance(relinearization_key, RelinearizationKey)):
-                    return _ProductCiphertext(self, a, b, relinearization_key)
+                    if len(self._pending) >= self._max_pending:
+                        Engine.materialize([p for p in list(self._pending) if p.pending])
+                    p = _ProductCiphertext(self, a, b, relinearization_key)
+                    self._pending.add(p)
+                    return p
                 return self._call_ct(self._lib.mul, a._h, b._h, relinearization_key._h)
             t = self._call_ct(self._lib.tensor, a._h, b._h)
             return self._call_ct(self._lib.rescale, t._h)

@@ -33,12 +33,18 @@ struct Arena {
     static constexpr size_t kAlign = 256;
     ArenaAllocator A{};
     size_t chunk_bytes = (size_t)1 << 33;
+    // growth cap: once the arena holds more than grow_cap x the largest live set seen, a new
+    // chunk is sized to its request alone -- fragmentation then grows the arena by what it needs,
+    // not by 8 GiB steps (round 3: 211.5 GB held for a 159.4 GB peak in the bench round).  0
+    // disables the cap.
+    double grow_cap = 1.2;
     std::map<char*, size_t> chunks_;                  // base -> size
     std::map<char*, size_t> free_addr_;               // free block -> size (address order)
     std::multimap<size_t, char*> free_size_;          // size -> free block (best fit)
     std::unordered_map<void*, size_t> live_;          // live block -> size
     size_t held = 0, live = 0, peak_live = 0;
     int64_t mallocs = 0, trims = 0, reuse_larger = 0;  // reuse_larger: blocks split off a larger free one
+    int64_t exact_chunks = 0;                          // chunks sized to their request by the growth cap
 
     static size_t round_up(size_t bytes) { return std::max(kAlign, (bytes + kAlign - 1) & ~(kAlign - 1)); }
 
@@ -61,6 +67,10 @@ struct Arena {
     }
     bool new_chunk(size_t need) {
         size_t want = std::max(chunk_bytes, need);
+        if (grow_cap > 0 && want > need && peak_live > 0 && (double)held > grow_cap * (double)peak_live) {
+            want = need;
+            exact_chunks++;
+        }
         void* p = A.alloc(want, A.ctx);
         if (!p && want > need) {  // nearly full: release empty chunks, then the exact need
             trim();

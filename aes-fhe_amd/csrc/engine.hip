@@ -77,6 +77,7 @@ struct ApiError {
 
 extern "C" const char* aesfhe_last_error(void) { return g_err; }
 extern "C" const char* aesfhe_backend_name(void) { return "hip-gfx950"; }
+extern "C" int32_t aesfhe_abi_version(void) { return AESFHE_ABI_VERSION; }
 
 // -----------------------------------------------------------------------------------------------
 // engine state
@@ -113,10 +114,11 @@ struct ProfRec {
     hipEvent_t a, b;
     double bytes;
     const char* label;  // kernel class (static string) or nullptr
+    int disp;           // kernel dispatches recorded inside the scope
 };
 
 struct KernStat {  // per kernel class (aesfhe_engine_profile_kernels)
-    int64_t n = 0;
+    int64_t n = 0, d = 0;  // scopes (calls) and kernel dispatches
     double ms = 0, bytes = 0;
 };
 
@@ -225,6 +227,7 @@ struct ProfScope {
     hipStream_t s;
     bool on;
     const char* label;
+    int disp = 1;  // kernel dispatches inside the scope (the PMC record counts dispatches)
     ProfScope(aesfhe_engine* e_, int f, double by, const char* lab = nullptr, hipStream_t s_ = nullptr)
         : e(e_), fam(f), bytes(by), s(s_ ? s_ : e_->stream), on((e_->prof >> f) & 1), label(lab) {
         if (!on) return;
@@ -245,7 +248,7 @@ struct ProfScope {
     ~ProfScope() {
         if (!on) return;
         hipEventRecord(b, s);
-        e->recs.push_back({fam, a, b, bytes, label});
+        e->recs.push_back({fam, a, b, bytes, label, disp});
     }
 };
 
@@ -261,6 +264,7 @@ static void prof_flush(aesfhe_engine* e) {
         if (r.label) {
             KernStat& k = e->prof_k[r.label];
             k.n++;
+            k.d += r.disp;
             k.ms += ms;
             k.bytes += r.bytes;
         }
@@ -857,8 +861,8 @@ extern "C" int aesfhe_engine_profile_kernels(aesfhe_engine* e, char* buf, int64_
     std::string js = "{";
     char tmp[256];
     for (auto& kv : e->prof_k) {
-        snprintf(tmp, sizeof tmp, "%s\"%s\": [%lld, %.6f, %.1f]", js.size() > 1 ? ", " : "", kv.first.c_str(),
-                 (long long)kv.second.n, kv.second.ms, kv.second.bytes);
+        snprintf(tmp, sizeof tmp, "%s\"%s\": [%lld, %.6f, %.1f, %lld]", js.size() > 1 ? ", " : "", kv.first.c_str(),
+                 (long long)kv.second.n, kv.second.ms, kv.second.bytes, (long long)kv.second.d);
         js += tmp;
     }
     js += "}";
@@ -3187,25 +3191,57 @@ static void poly2_int_impl(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_t
         auto dC0 = upload_small(e, C0.data(), C0.size());
         const long obs = 3L * nl * N;
         aesfhe_ct* d3 = ct_new(e, ml * B, 3, l);
+        // a < 2^52 and the unfolded tensor sums (a + 2 (nx - 1) products of <= 1.5 q) < 2^53
+        auto is_big = [&](int li) {
+            const double q = (double)e->chain.q[li];
+            return wfac * q >= 0x1p52 * 0.999 || (wfac + 3.0 * nx) * q >= 0x1p53 * 0.999;
+        };
+        // the S-box shape (ny = 16, whole blocks of 4 outputs) takes k_poly2_int_s on its exact
+        // limbs, with y' left unreduced where wfac_u = max_row (|w_0| + sum_j |w_j|) keeps the
+        // doubled bound: |a| <= wfac_u q < 2^51 and the tensor sums (a + 2 (nx - 1) products of
+        // <= 1.5 q) < 2^52
+        double wfac_u = 1.0;
+        for (int t = 0; t < ml; t++)
+            for (int i = 0; i < nx; i++) {
+                double f = 0.0;
+                for (int j = 0; j < ny; j++) f += std::fabs(Wt[((size_t)t * nx + i) * ny + j]);
+                wfac_u = std::max(wfac_u, f);
+            }
+        auto lazy_ok = [&](int li) {
+            const double q = (double)e->chain.q[li];
+            return wfac_u * q < 0x1p51 && (wfac_u + 3.0 * nx) * q < 0x1p52;
+        };
         {
             ProfScope ps_(e, FAM_EW, 8.0 * N * nl * (double)B * (2.0 * (nx + ny - 2) + 3.0 * ml), "poly2_int");
-            constexpr int mo = 4;  // outputs per launch (8: 219 VGPRs, 2 waves, measured slower)
-            for (int t0 = 0; t0 < ml; t0 += mo)
+            ps_.disp = 0;
+            constexpr int mo = 4;  // outputs per thread (8: 219 VGPRs, 2 waves, measured slower)
+            for (int t0 = 0; t0 < ml;) {
+                // k_poly2_int_s: 2 blocks per launch, paired on XCDs by 8 workgroups (N >= 2^11)
+                const bool sbox = ny == kPoly2Max && ml - t0 >= 2 * mo && (N / 256) % 8 == 0;
                 for (int la = 0; la < nl;) {  // runs of limbs of one kernel class
-                    // a < 2^52 and the unfolded tensor sums (a + 2 (nx - 1) products of <= 1.5 q) < 2^53
-                    auto is_big = [&](int li) {
-                        const double q = (double)e->chain.q[li];
-                        return wfac * q >= 0x1p52 * 0.999 || (wfac + 3.0 * nx) * q >= 0x1p53 * 0.999;
-                    };
-                    const bool big = is_big(la);
+                    const bool big = is_big(la), lz = !big && lazy_ok(la);
                     int lb = la + 1;
-                    while (lb < nl && is_big(lb) == big) lb++;
-                    auto kern = big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max, mo> : k_poly2_int<true, 0, mo>)
-                                    : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max, mo> : k_poly2_int<false, 0, mo>);
-                    hipLaunchKernelGGL(kern, dim3(N / 256, lb - la, B), dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny,
-                                       (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, ml, t0, std::min(mo, ml - t0), d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN, slab_rot);
+                    while (lb < nl && is_big(lb) == big && (big || lazy_ok(lb) == lz)) lb++;
+                    const dim3 grid(N / 256, lb - la, B);
+                    if (sbox && !big) {
+                        hipLaunchKernelGGL((lz ? k_poly2_int_s<mo, true> : k_poly2_int_s<mo, false>), dim3(2 * N / 256, lb - la, B), dim3(256), 0, e->stream,
+                                           (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy,
+                                           (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, t0,
+                                           d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN, slab_rot);
+                        ps_.disp++;
+                    } else {
+                        auto kern = big ? (ny == kPoly2Max ? k_poly2_int<true, kPoly2Max, mo> : k_poly2_int<true, 0, mo>)
+                                        : (ny == kPoly2Max ? k_poly2_int<false, kPoly2Max, mo> : k_poly2_int<false, 0, mo>);
+                        for (int tb = t0; tb < (sbox ? t0 + 2 * mo : t0 + mo) && tb < ml; tb += mo) {
+                            hipLaunchKernelGGL(kern, grid, dim3(256), 0, e->stream, (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy, ny,
+                                               (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, ml, tb, std::min(mo, ml - tb), d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN, slab_rot);
+                            ps_.disp++;
+                        }
+                    }
                     la = lb;
                 }
+                t0 += sbox ? 2 * mo : mo;
+            }
         }
         HIPC(hipGetLastError());
         aesfhe_ct* r2 = relin_rescale(e, d3, rlk, 2);

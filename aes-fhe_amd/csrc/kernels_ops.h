@@ -1009,6 +1009,101 @@ __global__ void __launch_bounds__(256, MO > 4 ? 2 : 3) k_poly2_int(const u64* co
     }
 }
 
+// k_poly2_int's exact path (BIG = false) for the S-box shape: the full 16-term y basis, whole
+// blocks of MO outputs (no per-output guards), the x^0 term peeled out of the monomial loop (no
+// per-monomial branches), and LAZY: y' = H y left unreduced (|y'| <= q instead of q/2 + 1: the
+// fred of every y' word -- 3 fp64 ops x 30 per class -- dropped; the host takes LAZY where the
+// doubled bound still keeps |a| <= (|w_0| + sum_j |w_j|) q < 2^51 and the tensor sums < 2^52).
+// The inner sums and the tensor accumulators are exact integers congruent to k_poly2_int's, so
+// the canonical outputs are the same words.
+// Both output blocks (t0 .. t0 + MO - 1 and t0 + MO .. t0 + 2 MO - 1) in one launch: workgroups b
+// and b + 8 -- dealt to the same XCD -- take the same 256 coefficients, one block each, so the
+// second one's x / y reads hit that XCD's L2 instead of HBM.  grid (2 N/256, run, B).
+template <int MO, bool LAZY>
+__global__ void __launch_bounds__(256, 3) k_poly2_int_s(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
+                        const long* __restrict__ xps, int nx, const u64* const* __restrict__ yp,
+                        const long* __restrict__ ybs, const long* __restrict__ yps,
+                        const int* __restrict__ xstart, const int* __restrict__ ycls, int cxn,
+                        int cyn, const double* __restrict__ Wt, const TwD* __restrict__ Rt,
+                        const double* __restrict__ C0, int t0, u64* __restrict__ out, long oos, long obs,
+                        const u64* __restrict__ qs, const double* __restrict__ qinv, int l0, int nl,
+                        int logN, int orot) {
+    constexpr int NY = kPoly2Max;
+    const int bx = blockIdx.x, half = (bx >> 3) & 1;            // blocks b, b + 8: one XCD
+    const int k = (((bx >> 4) << 3) | (bx & 7)) * blockDim.x + threadIdx.x;
+    const int l = l0 + blockIdx.y, bb = blockIdx.z;
+    t0 += half * MO;
+    const double q = (double)qs[l];
+    const double qi = qinv[l];
+    const long off = ((long)l << logN) + k;
+    const TwD* Rl = Rt + (size_t)l * cxn * cyn;
+    double y0[NY - 1], y1[NY - 1];
+    auto load_y = [&](int c) {  // y' = H(c, cy(j)) y_j
+        const TwD* Rc = Rl + c * cyn;
+#pragma unroll
+        for (int j = 0; j < NY - 1; j++) {
+            const u64* p = yp[j] + (long)bb * ybs[j] + off;
+            const TwD r = Rc[ycls[j + 1]];
+            const double v0 = fmul_rem_r(u2d(p[0]), r.w, r.wq, q), v1 = fmul_rem_r(u2d(p[yps[j]]), r.w, r.wq, q);
+            y0[j] = LAZY ? v0 : fred(v0, q, qi);
+            y1[j] = LAZY ? v1 : fred(v1, q, qi);
+        }
+    };
+    double d0[MO], d1[MO], d2[MO];
+    // class 0 = the x^0 term: d = (a_0, a_0', 0)
+    load_y(0);
+    {
+        const double c0 = C0[(size_t)l * cxn];
+#pragma unroll
+        for (int t = 0; t < MO; t++) {
+            const double* w = Wt + (size_t)(t0 + t) * nx * NY;
+            double a0 = w[0] * c0, a1 = 0.0;
+#pragma unroll
+            for (int j = 1; j < NY; j++) {
+                a0 = __builtin_fma(w[j], y0[j - 1], a0);
+                a1 = __builtin_fma(w[j], y1[j - 1], a1);
+            }
+            d0[t] = a0;
+            d1[t] = a1;
+            d2[t] = 0.0;
+        }
+    }
+#pragma unroll 1
+    for (int c = 1; c < cxn; c++) {
+        load_y(c);
+        const double c0 = C0[(size_t)l * cxn + c];
+#pragma unroll 1
+        for (int i = xstart[c]; i < xstart[c + 1]; i++) {
+            const u64* p = xp[i - 1] + (long)bb * xbs[i - 1] + off;
+            const double xa = u2d(p[0]), xb = u2d(p[xps[i - 1]]);
+#pragma unroll
+            for (int t = 0; t < MO; t++) {
+                const double* w = Wt + ((size_t)(t0 + t) * nx + i) * NY;
+                double a0 = w[0] * c0, a1 = 0.0;
+#pragma unroll
+                for (int j = 1; j < NY; j++) {
+                    a0 = __builtin_fma(w[j], y0[j - 1], a0);
+                    a1 = __builtin_fma(w[j], y1[j - 1], a1);
+                }
+                const double a0q = a0 * qi, a1q = a1 * qi;
+                d0[t] += fmul_rem(xa, a0, a0q, q);
+                d1[t] += fmul_rem(xa, a1, a1q, q) + fmul_rem(xb, a0, a0q, q);
+                d2[t] += fmul_rem(xb, a1, a1q, q);
+            }
+        }
+    }
+    const int ob = (bb & ~3) | ((bb - orot) & 3);  // aesfhe_poly2_int_rot
+    u64* o = out + (long)ob * obs + off;
+    const long pstr = (long)nl << logN;
+#pragma unroll
+    for (int t = 0; t < MO; t++) {
+        u64* ot = o + (long)(t0 + t) * oos;
+        ot[0] = fcanon(d0[t], q, qi);
+        ot[pstr] = fcanon(d1[t], q, qi);
+        ot[2 * pstr] = fcanon(d2[t], q, qi);
+    }
+}
+
 // ModRaise: x = limb 0 of every polynomial in coefficient form (mod q_0); out limb i =
 // centred x mod q_i for i < nl.  x: [P][N] (P = B * npoly), out: [P][nl][N].  grid (N/256, nl, P)
 __global__ void k_lift0(const u64* __restrict__ x, u64* __restrict__ out, int nl, u64 q0,

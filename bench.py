@@ -57,8 +57,9 @@ PEAK_HBM_GBS = 8000.0
 METRIC = "AES-128 blocks/sec (homomorphic full round) at N=2^16, L=30; 1/2/4/8 MI355X"
 WORKLOAD = {
     "sliced": ("fully sliced +-1 bit state (one ciphertext per row and bit, the 4 columns as batch "
-               "elements, one block per slot), ShiftRows as a batch permutation, S-box as Walsh "
-               "polynomial over nibble-bit monomials, bit-domain MixColumns/AddRoundKey"),
+               "elements, one block per slot), S-box as Walsh polynomial over nibble-bit monomials "
+               "with ShiftRows folded into its output order (aesfhe_poly2_int_rot: no gather, no "
+               "rotation), bit-domain MixColumns/AddRoundKey"),
     "rows": ("row-sliced +-1 bit state (columns in slot quarters), ShiftRows by rotations, S-box as "
              "Walsh polynomial over nibble-bit monomials, bit-domain MixColumns/AddRoundKey"),
     "bytes": "nibble-domain Zeta-16 LUTs, byte-major SIMD packing",
@@ -66,11 +67,23 @@ WORKLOAD = {
 SEED = 0x5EED5EED  # the CPU baseline's engine (reproducible); the GPU ranks share a 256-bit seed
 
 PEAK_FP64_TFLOPS = 78.6  # MI355X vector FP64 (AMD spec: 256 CUs x 128 FLOP/clk x 2.4 GHz)
-PMC_FILE = ROOT / "profiles" / "r03" / "pmc" / "round_traffic.json"
+PMC_FILE = ROOT / "profiles" / "r04" / "pmc" / "round_traffic.json"
 PMC_NOTE = ("HBM bytes per NTT-family launch measured with rocprofv3 --pmc FETCH_SIZE (x2, the gfx950 "
             "correction of MI355X_MICROARCH.md) and --pmc WRITE_SIZE, separate passes, over exactly one "
             "bench round step (tools/pmc_traffic.py -> profiles/r03/pmc/round_traffic.json, stamped "
-            "with the git HEAD it measured)")
+            "with the git HEAD it measured and the hash of the kernel sources it ran)")
+
+
+def csrc_sha16():
+    """sha256 (16 hex digits) of the engine's kernel sources and C ABI header, in a fixed order:
+    the PMC record stores the value of the tree it measured, and the bench uses the record only
+    while its own sources hash the same (the GPU box has no git history to diff against)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted((ROOT / "aes-fhe_amd" / "csrc").glob("*")) + [ROOT / "include" / "aesfhe.h"]:
+        if f.is_file():
+            h.update(f.name.encode() + b"\0" + f.read_bytes())
+    return h.hexdigest()[:16]
 
 
 _T0 = time.perf_counter()
@@ -88,6 +101,8 @@ def pmc_record(args=None):
         rec = json.loads(PMC_FILE.read_text())
     except (OSError, ValueError):
         return None
+    if rec.get("csrc_sha16") != csrc_sha16():
+        return None  # measured on other kernels
     if args is not None and rec.get("workload") != {"log_n": args.log_n, "max_level": args.max_level,
                                                      "special_primes": args.special_primes,
                                                      "digit_primes": digit_primes(args),
@@ -98,33 +113,45 @@ def pmc_record(args=None):
 
 def kernel_table(eng, pmc, steps):
     """Per kernel class of the profiled steps (aesfhe_engine_profile_kernels, HIP events on the
-    engine stream): launches, average duration, algorithmic GB/s and its fraction of the HBM
-    peak; with the PMC record, the measured HBM bytes per launch (-> GB/s, fraction) and, where
-    counted, the fp64 FLOP rate against the FP64 vector peak."""
+    engine stream): calls and kernel dispatches per step, average duration per call, algorithmic
+    GB/s and its fraction of the HBM peak; with the PMC record (per DISPATCH, over one step), the
+    measured HBM bytes per call (-> GB/s, fraction) and, where counted, the fp64 FLOP rate
+    against the FP64 peak -- only where the record's dispatch count per step equals the profiled
+    one (a call of several dispatches, e.g. poly2_int's, scales by its dispatches per call;
+    otherwise the PMC figures are null and `pmc_dispatches_mismatch` says why)."""
     import ctypes as C
     need = C.c_int64()
     eng._check(eng._lib.engine_profile_kernels(eng._h, None, 0, C.byref(need)))
     buf = C.create_string_buffer(need.value)
     eng._check(eng._lib.engine_profile_kernels(eng._h, buf, need.value, C.byref(need)))
     raw = json.loads(buf.value.decode())
-    total = sum(ms for _, ms, _ in raw.values()) or 1.0
+    total = sum(v[1] for v in raw.values()) or 1.0
     pk = (pmc or {}).get("per_kernel", {})
     out = {}
-    for k, (n, ms, by) in sorted(raw.items(), key=lambda kv: -kv[1][1]):
+    for k, v in sorted(raw.items(), key=lambda kv: -kv[1][1]):
+        n, ms, by = v[:3]
+        disp = v[3] if len(v) > 3 else n
         avg_s = ms * 1e-3 / n
-        rec = {"launches_per_step": round(n / steps, 1), "avg_us": round(avg_s * 1e6, 2),
-               "share_of_kernel_time": round(ms / total, 4)}
+        rec = {"launches_per_step": round(n / steps, 1), "dispatches_per_step": round(disp / steps, 1),
+               "avg_us": round(avg_s * 1e6, 2), "share_of_kernel_time": round(ms / total, 4)}
         if by > 0:
             gbs = by / n / avg_s / 1e9
             rec.update(alg_bytes_per_launch=round(by / n), alg_gbs=round(gbs, 1), frac=round(gbs / PEAK_HBM_GBS, 4))
         p = pk.get(k)
         if p:
-            hbm = p["hbm_bytes_per_launch"]
-            rec.update(hbm_bytes_per_launch=round(hbm), hbm_gbs=round(hbm / avg_s / 1e9, 1),
-                       hbm_frac=round(hbm / avg_s / 1e9 / PEAK_HBM_GBS, 4))
-            if p.get("f64_flops_per_launch"):
-                tf = p["f64_flops_per_launch"] / avg_s / 1e12
-                rec.update(f64_tflops=round(tf, 2), fp64_frac=round(tf / PEAK_FP64_TFLOPS, 4))
+            if abs(p["launches"] - disp / steps) > 0.5:
+                rec.update(hbm_bytes_per_launch=None, pmc_dispatches_mismatch={
+                    "pmc_per_step": p["launches"], "profiled_per_step": round(disp / steps, 1)})
+            else:
+                per_call = disp / n  # dispatches per call
+                hbm = p["hbm_bytes_per_launch"] * per_call
+                rec.update(hbm_bytes_per_launch=round(hbm), hbm_gbs=round(hbm / avg_s / 1e9, 1),
+                           hbm_frac=round(hbm / avg_s / 1e9 / PEAK_HBM_GBS, 4))
+                if by > 0:
+                    rec["hbm_over_alg"] = round(hbm / (by / n), 3)
+                if p.get("f64_flops_per_launch"):
+                    tf = p["f64_flops_per_launch"] * per_call / avg_s / 1e12
+                    rec.update(f64_tflops=round(tf, 2), fp64_frac=round(tf / PEAK_FP64_TFLOPS, 4))
         out[k] = rec
     return out
 
@@ -172,6 +199,10 @@ def parse():
                          "the PMC records between them)")
     ap.add_argument("--no-harness", action="store_true",
                     help="skip the reference-harness leg (full_round on 32768 bytes, xor_cipher)")
+    ap.add_argument("--config5", choices=("auto", "on", "off"), default="auto",
+                    help="config 5's per-rank shard (N = 2^17, L = 35, K = 12, scale 44, 16 sets = 64 of the "
+                         "reference's 512 ciphertexts / 8 GPUs): one round + ten rounds on a fresh engine after "
+                         "the N = 2^16 legs; auto = on at one GPU with the default N = 2^16 workload")
     ap.add_argument("--launch-timeout", type=float, default=0.0,
                     help="--gpus N > 1 started without torchrun: kill the ranks after this many seconds (0: none)")
     ap.add_argument("--selftest-launch", action="store_true",
@@ -727,6 +758,64 @@ def cpu_config_legs(args, lib, threads):
     return out
 
 
+def config5_shard_leg(args, device, rank, barrier, allmax, cur):
+    """BASELINE config 5 ("Full AES-128 10 rounds, N=2^17, L=35, batch=512 ciphertexts sharded
+    across 8 MI355X"): one rank's shard -- 512 / 8 = 64 reference ciphertexts of 4096 blocks =
+    16 sets of 16 384 blocks -- on its own engine (the caller has released the N = 2^16 one): a
+    middle round (1 warm-up + 2 timed steps, the sliced state at the top level) and the full
+    ten-round encryption with refreshes (bench's aes128_10_rounds leg at these parameters), both
+    verified against FIPS-197.  No collective: the shards are independent."""
+    import copy
+    import gc
+
+    from aes_xor_fhe import aes_tables as T
+    a = copy.copy(args)
+    a.log_n, a.max_level, a.special_primes, a.scale_bits = 17, 35, 12, 44
+    a.digit_primes, a.batch, a.aes10_batch, a.aes10_ppc, a.layout = -1, 16, 16, 0, "sliced"
+    t0 = time.perf_counter()
+    eng, drv = setup_engine(a, device, rank)
+    cur[0] = eng  # the barrier drains this engine's stream
+    setup_s = time.perf_counter() - t0
+    try:
+        rng = np.random.default_rng(5000 + rank)
+        blocks = rng.integers(0, 256, (a.batch, drv.n_blk, 16), dtype=np.uint8)
+        rk = np.random.default_rng(25073105).integers(0, 256, 16, dtype=np.uint8)
+        st, key = drv.encrypt(blocks), drv.key(rk)
+
+        def step():
+            out = drv.round(st, key)
+            _materialize(drv.cts(out))
+            return out
+        step()
+        barrier()
+        steps = 2
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = step()
+        barrier()
+        el = allmax(time.perf_counter() - t0)
+        ok = bool(np.array_equal(drv.decrypt(out, a.batch), T.aes_round(blocks, rk))) if a.check else None
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rnd = {"value": round(a.batch * drv.n_blk * world * steps / el, 2), "unit": "blocks/s",
+               "ms_per_step": round(el / steps * 1e3, 1), "steps": steps, "verified": ok}
+        del st, out
+        gc.collect()
+        eng.pool_trim()
+        log("config 5 shard: round done; ten rounds")
+        aes10 = aes128_full(a, eng, drv, rank, barrier, allmax)
+        return {"workload": ("config 5 per-rank shard: 16 sets x 16384 blocks (64 of the reference's 512 "
+                             "ciphertexts of 4096 blocks / 8 GPUs), fully sliced state"),
+                "log_n": a.log_n, "max_level": a.max_level, "special_primes": a.special_primes,
+                "digit_primes": eng.digit_primes, "scale_bits": a.scale_bits, "setup_s": round(setup_s, 1),
+                "round": rnd, "aes128_10_rounds": {k: v for k, v in aes10.items() if k != "pool"},
+                "pool_peak_held_gb": round(eng.pool_stats()["held"] / 1e9, 1)}
+    finally:
+        cur[0] = None
+        drv.keys = None
+        del drv, eng
+        gc.collect()
+
+
 def main():
     args = parse()
     if args.gpus < 1:
@@ -759,6 +848,7 @@ def main():
 
     log(f"rank {rank}/{world}: engine N=2^{args.log_n} L={args.max_level} K={args.special_primes}")
     eng, R = setup_engine(args, device, rank)
+    n_blk = R.n_blk
     if eng._lib.backend != "hip-gfx950":
         raise RuntimeError(f"bench needs the HIP engine, got backend {eng._lib.backend!r}")
     log("keys ready")
@@ -766,8 +856,11 @@ def main():
         torch.cuda.set_device(device)
     red_dev = torch.device("cuda", device) if dist is not None and dist.get_backend() == "nccl" else torch.device("cpu")
 
+    cur = [eng]  # the engine whose stream the barrier drains (None once released for config 5)
+
     def barrier():
-        eng.synchronize()
+        if cur[0] is not None:
+            cur[0].synchronize()
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         if dist is not None:
@@ -815,6 +908,7 @@ def main():
     mark()
     log(f"timed: {args.steps} steps, {elapsed / args.steps * 1e3:.1f} ms/step")
     round_pool = eng.pool_stats()
+    round_pool["held_over_peak_live"] = round(round_pool["held"] / max(round_pool["peak_live"], 1), 3)
     ok = None
     if args.check:
         ok = bool(np.array_equal(R.decrypt(out, args.batch), T.aes_round(blocks, rk)))
@@ -861,7 +955,8 @@ def main():
             return {"error": repr(ex)}
         finally:
             gc.collect()
-            eng.pool_trim()
+            if cur[0] is not None:
+                cur[0].pool_trim()
 
     sg = None
     if dist is not None:
@@ -881,8 +976,26 @@ def main():
     log("config legs done" if configs else "no config legs")
     if args.aes10_batch > 0 and args.layout != "bytes":
         aes10 = secondary("aes10", lambda: aes128_full(args, eng, R, rank, barrier, allmax))
+    c5 = None
+    run_c5 = args.config5 == "on" or (args.config5 == "auto" and world == 1 and args.log_n == 16
+                                      and args.max_level == 30 and args.layout == "sliced")
+    backend, digits, dnum = eng._lib.backend, eng.digit_primes, eng.dnum
+    if run_c5:
+        # config 5's shard needs the device to itself: release the N = 2^16 engine, its keys and
+        # its pool first (the round's state and outputs are already gone); verified released
+        import weakref
+        alive = weakref.ref(eng)
+        R.keys = None
+        del R, key
+        cur[0] = None
+        del eng
+        gc.collect()
+        if alive() is not None:
+            raise RuntimeError("the N = 2^16 engine is still referenced; config 5 would not fit beside it")
+        log("N = 2^16 engine released; config 5 shard")
+        c5 = secondary("config5 shard", lambda: config5_shard_leg(args, device, rank, barrier, allmax, cur))
 
-    blocks_per_step = args.batch * R.n_blk * world
+    blocks_per_step = args.batch * n_blk * world
     value = blocks_per_step * args.steps / elapsed
     if rank == 0:
         steps_prof = max(args.profile_steps, 1)
@@ -905,15 +1018,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "backend": eng._lib.backend,
+            "backend": backend,
             "data": "synthetic random AES states + random round key, encrypted",
             "config": {
                 "workload": ("one full AES-128 middle round (ShiftRows+SubBytes+MixColumns+"
                              "AddRoundKey): " + WORKLOAD[args.layout]),
                 "layout": args.layout,
                 "log_n": args.log_n, "max_level": args.max_level, "special_primes": args.special_primes,
-                "digit_primes": eng.digit_primes, "dnum": eng.dnum, "scale_bits": args.scale_bits,
-                "ciphertext_sets_per_gpu": args.batch, "blocks_per_gpu_per_step": args.batch * R.n_blk,
+                "digit_primes": digits, "dnum": dnum, "scale_bits": args.scale_bits,
+                "ciphertext_sets_per_gpu": args.batch, "blocks_per_gpu_per_step": args.batch * n_blk,
                 "parallelism": f"ciphertext-batch sharding x{world} (no data-path collective)",
                 "verified": ok, "pool_after_round": round_pool,
             },
@@ -929,6 +1042,7 @@ def main():
                 "traffic_over_alg": round(fam["hbm_bytes_per_launch"] / alg_per_launch, 3) if same_shape and alg_per_launch else None,
                 "traffic_source": PMC_NOTE if same_shape else "no PMC record of this workload",
                 "traffic_head": pmc.get("head") if same_shape else None,
+                "traffic_csrc_sha16": pmc.get("csrc_sha16") if same_shape else None,
                 "measured_over": f"{args.profile_steps} profiled round steps after the timed region",
                 "launches": n_ntt.value, "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "alg_bytes_per_launch": round(by_ntt.value / max(n_ntt.value, 1)),
@@ -940,6 +1054,7 @@ def main():
             },
             "cpu_baseline": None,
             "aes128_10_rounds": aes10,
+            "config5_shard": c5,
             "configs": configs,
             "client_path": client,
             "scatter_gather": sg,

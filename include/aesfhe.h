@@ -62,6 +62,11 @@
 extern "C" {
 #endif
 
+/* ABI revision: bumped whenever a struct layout or an entry point's meaning changes (4: the
+ * trailing aesfhe_params.digit_primes; a caller compiled against an older header passes a shorter
+ * struct).  Callers check aesfhe_abi_version() == AESFHE_ABI_VERSION before anything else. */
+#define AESFHE_ABI_VERSION 4
+
 #define AESFHE_OK 0
 #define AESFHE_EARG (-1)      /* bad argument / shape / level mismatch */
 #define AESFHE_ENOMEM (-2)    /* host or device allocation failed */
@@ -96,6 +101,7 @@ typedef struct aesfhe_params {
 /* ---- diagnostics ---------------------------------------------------------------------- */
 const char *aesfhe_last_error(void);
 const char *aesfhe_backend_name(void);
+int32_t aesfhe_abi_version(void); /* AESFHE_ABI_VERSION of the library */
 
 /* ---- engine ----------------------------------------------------------------------------- */
 int aesfhe_engine_create(const aesfhe_params *params, aesfhe_engine **out);

@@ -58,6 +58,7 @@ static int fail(int code, const char *fmt, ...) {
 
 const char *aesfhe_last_error(void) { return g_err; }
 const char *aesfhe_backend_name(void) { return "oracle-cpu"; }
+int32_t aesfhe_abi_version(void) { return AESFHE_ABI_VERSION; }
 
 /* ------------------------------------------------------------------------------------------ */
 /* modular arithmetic                                                                          */

@@ -118,6 +118,31 @@ int main() {
     if (a.held != 0 || !a.chunks_.empty() || !a.free_addr_.empty() || !a.free_size_.empty())
         return fail("trim left chunks behind", steps);
     if (cnt.allocs != cnt.frees) return fail("allocator calls unbalanced", steps);
+    // growth cap: an arena holding more than 1.2 x its peak live set grows by the request alone
+    {
+        Arena b;
+        b.A = a.A;
+        b.chunk_bytes = 1 << 20;
+        void* x = b.get(600000);  // peak 600 000 in one 1 MiB chunk
+        b.put(x);
+        void* lo = b.get(400000);
+        void* mid = b.get(100000);
+        b.put(lo);                // free: 400 128 at the start, 548 352 at the end; held 1.75 x peak
+        const size_t held0 = b.held;
+        void* big = b.get(560000);  // fits no free block (548 352 and 400 128 free)
+        if (!big || b.exact_chunks != 1 || b.held != held0 + Arena::round_up(560000))
+            return fail("cap: fragmented growth took a whole chunk", steps);
+        b.grow_cap = 0;             // disabled: a whole chunk again
+        void* big2 = b.get(560000);
+        if (!big2 || b.held != held0 + Arena::round_up(560000) + ((size_t)1 << 20))
+            return fail("cap disabled: chunk size", steps);
+        b.put(big);
+        b.put(big2);
+        b.put(mid);
+        b.trim();
+        if (b.held != 0) return fail("cap: trim", steps);
+    }
+    if (cnt.allocs != cnt.frees) return fail("allocator calls unbalanced (cap)", steps);
     std::printf("arena_asan ok: %ld steps, %ld chunk allocations, peak live %zu bytes\n", steps, cnt.allocs, peak);
     return 0;
 }

@@ -42,6 +42,14 @@ def test_backend_names(product_cdll, oracle_lib):
     assert oracle_lib.backend == "oracle-cpu"
 
 
+def test_abi_version(product_cdll, oracle_lib):
+    """Both libraries report the header's ABI revision (the loader refuses any other)."""
+    from aes_xor_fhe._abi import ABI_VERSION
+    want = int(re.search(r"#define AESFHE_ABI_VERSION (\d+)", HEADER).group(1))
+    assert ABI_VERSION == want
+    assert product_cdll.abi_version() == want and oracle_lib.abi_version() == want
+
+
 @pytest.mark.parametrize("log_n", [10, 12, 16])
 def test_host_codec_bit_identical(product_cdll, oracle_lib, log_n):
     n = 1 << (log_n - 1)

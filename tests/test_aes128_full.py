@@ -36,9 +36,14 @@ def _run(lib, log_n, nb=1, seed=3, cls=AESRowRound, cts_groups=(3,), key_levels=
     L0 = R.fresh_level(e.max_level, bs) if key_levels else None
     lv = R.key_levels(L0, bs) if key_levels else [None] * 11
     keys = [R.encrypt_round_key(rk, level=v) for rk, v in zip(rks, lv)]
-    out, nref = R.encrypt_aes128(R.encrypt_blocks(blocks, level=L0), keys, bs)
-    if key_levels:  # no level-down was needed anywhere: the state kept the schedule's levels
-        assert L0 == 25 and [l for _, l, _ in R.schedule(L0, bs)][-1] == 5
+    tm = {}
+    out, nref = R.encrypt_aes128(R.encrypt_blocks(blocks, level=L0), keys, bs, timings=tm)
+    # every round started at the level the precomputed schedule says (so the round keys, encrypted
+    # at key_levels, met the state without a level-down): measured, not only planned
+    sched = R.schedule(e.max_level if L0 is None else L0, bs)
+    assert [lv for _, lv, _ in tm["per_round"]] == [lv for _, lv, _ in sched]
+    if key_levels:
+        assert L0 == 25 and sched[-1][1] == 5
     got = R.decrypt_blocks(out, nb)
     want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
     return got, want, nref, out

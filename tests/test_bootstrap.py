@@ -187,16 +187,23 @@ def test_pick_bootstrapper():
     assert R.pick_bootstrapper(bss[1:], 8) is bss[1]
 
 
+BENCH_CHAIN = dict(scale_bits=40, max_level=30, special_primes=10, digit_primes=12)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("kw", [{}, dict(scale_bits=40, max_level=30, special_primes=10, digit_primes=12)],
-                         ids=["K4", "K10A12"])
-def test_bootstrap_bits_bit_exact_vs_oracle(product_lib, oracle_lib, gpu_available, kw):
+@pytest.mark.parametrize("kw,groups", [({}, None), (BENCH_CHAIN, None), (BENCH_CHAIN, 5)],
+                         ids=["K4", "K10A12", "K10A12G5"])
+def test_bootstrap_bits_bit_exact_vs_oracle(product_lib, oracle_lib, gpu_available, kw, groups):
     """Bit-mode and general bootstrapping residue for residue; K10A12: the bench's chain (L = 30,
-    K = 10 special primes, 12-prime key-switch digits) at N = 2^10."""
+    K = 10 special primes, 12-prime key-switch digits) at N = 2^10; G5: the 5-map CoeffToSlot
+    bootstrapper the bench's ten-round leg uses for its two middle refreshes (the 3-map one is
+    the default of the other two cases)."""
     outs = []
     for lib in (product_lib, oracle_lib):
         e, sk, pk, rlk = _engine(lib, **kw)
-        bs = Bootstrapper(e, sk, rlk)
+        bs = Bootstrapper(e, sk, rlk, cts_groups=groups)
+        if groups is not None:
+            assert bs.cts_groups == groups and bs.bits_level == e.max_level - 13
         rng = np.random.default_rng(4)
         n = e.slot_count
         a, b = rng.choice([-1.0, 1.0], n), rng.choice([-1.0, 1.0], n)

@@ -100,10 +100,16 @@ def test_device_encrypt_decrypt_equal_host(product_lib, gpu_available, log_n):
     pka, pkb = a.create_public_key(ska), b.create_public_key(skb)
     v = _slots(a, np.random.default_rng(2), 4, a.slot_count)
     ca = a.encrypt_device(torch.from_numpy(v), pka, level=4)
-    cb = b.encrypt(v, pkb, level=4)
+    cb = b._encrypt_host(v, pkb, 4)
     assert np.array_equal(a.export_residues(ca), b.export_residues(cb))
     for ct in (ca, a.multiply(ca, 0.5)):
-        assert np.array_equal(a.decrypt_device(ct, ska).cpu().numpy(), a.decrypt(ct, ska))
+        assert np.array_equal(a.decrypt_device(ct, ska).cpu().numpy(), a._decrypt_host(ct, ska))
+    # the reference surface (Engine.encrypt / decrypt, engine_context.py:81-85) runs the device
+    # codec on the HIP engine: the same words as the host codec, real and complex slots alike
+    for x in (v, v.real, v[0], v[0, :100].real):
+        c1, c2 = a.encrypt(x, pka, level=3), b._encrypt_host(x, pkb, 3)
+        assert np.array_equal(a.export_residues(c1), b.export_residues(c2))
+        assert np.array_equal(a.decrypt(c1, ska), a._decrypt_host(c1, ska))
 
 
 @pytest.mark.gpu
@@ -120,3 +126,25 @@ def test_rows_client_path_gpu(product_lib, gpu_available):
     out = R.decrypt_blocks_device(R.round(st, R.encrypt_round_key(rk)))
     assert out.device.type == "cuda"
     assert np.array_equal(out.cpu().numpy(), T.aes_round(blocks, rk))
+
+
+@pytest.mark.gpu
+def test_sliced_client_path_gpu(product_lib, gpu_available):
+    """The bench's client_path leg in its exact form: AESSlicedRound (columns as batch elements,
+    whole slabs of 4 sets, the last slab padded) packs / bit-slices / encodes / encrypts on the
+    GPU, runs one round (ShiftRows folded into the S-box), decrypts / decodes / unpacks on the
+    GPU == FIPS-197, at N = 2^16 with the bench's 12-prime digits over K = 10."""
+    from aes_xor_fhe.aes_round_bits import AESSlicedRound
+    e = Engine(_lib=product_lib, log_n=16, max_level=10, special_primes=10, digit_primes=12, scale_bits=40, seed=9)
+    sk = e.create_secret_key(1)
+    R = AESSlicedRound(e, sk, e.create_public_key(sk), e.create_relinearization_key(sk))
+    nb = 6  # two slabs, the second half padding
+    blocks = np.random.default_rng(13).integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
+    rk = np.random.default_rng(14).integers(0, 256, 16, dtype=np.uint8)
+    st = R.encrypt_blocks_device(torch.from_numpy(blocks).to(e.client_device))
+    assert st[0][0].batch == 8
+    out = R.decrypt_blocks_device(R.round(st, R.encrypt_round_key(rk)), nb)
+    assert out.device.type == "cuda" and tuple(out.shape) == (nb, R.n_blk, 16)
+    assert np.array_equal(out.cpu().numpy(), T.aes_round(blocks, rk))
+    # the host decryption of the same state agrees (device and host codecs are bit-identical)
+    assert np.array_equal(R.decrypt_blocks(R.round(st, R.encrypt_round_key(rk)), nb), T.aes_round(blocks, rk))

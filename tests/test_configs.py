@@ -112,23 +112,34 @@ CONFIG4 = dict(log_n=16, max_level=30, special_primes=10, scale_bits=40)
 
 @pytest.mark.gpu
 def test_config4_full_batch_ten_rounds(product_lib, gpu_available):
-    """Config 4 -- "Full AES-128 10 rounds end-to-end, N=2^16, L=30, batch=64 ciphertexts": the
-    whole batch (64 reference ciphertexts of 2048 blocks = 16 row-sliced sets of 8192 blocks =
-    131 072 blocks) through ARK0 + 10 rounds on three bit-mode refreshes of 8 ciphertexts per
-    call (the bench leg's shape), every block checked against FIPS-197."""
-    from aes_xor_fhe.aes_round_bits import AESRowRound
+    """Config 4 -- "Full AES-128 10 rounds end-to-end, N=2^16, L=30, batch=64 ciphertexts" -- in
+    exactly the shape bench.py's aes128_10_rounds leg times: the whole batch (64 reference
+    ciphertexts of 2048 blocks = 16 sets of 8192 blocks = 131 072 blocks) in the fully sliced
+    state (AESSlicedRound, 4 slabs), 12-prime key-switch digits over K = 10, the state encrypted
+    at the fresh level (25) with each round key at the level its product consumes, the 5-map and
+    3-map CoeffToSlot bootstrappers picked per refresh, 4 pairs per bootstrap call; every block
+    checked against FIPS-197 and every round's input level against the schedule."""
+    from aes_xor_fhe.aes_round_bits import AESSlicedRound
     from aes_xor_fhe.bootstrap import Bootstrapper
-    from aes_xor_fhe.fhe import Engine
-    e = Engine(_lib=product_lib, seed=23, **CONFIG4)
+    from aes_xor_fhe.fhe import Engine, widest_digits
+    alpha = widest_digits(**CONFIG4, lib=product_lib)
+    assert alpha == 12
+    e = Engine(_lib=product_lib, seed=23, digit_primes=alpha, **CONFIG4)
     sk = e.create_secret_key()
     rlk = e.create_relinearization_key(sk)
-    R = AESRowRound(e, sk, e.create_public_key(sk), rlk)
-    bs = Bootstrapper(e, sk, rlk)
+    R = AESSlicedRound(e, sk, e.create_public_key(sk), rlk)
+    bs = [Bootstrapper(e, sk, rlk, cts_groups=g) for g in (5, 3)]
+    L0 = R.fresh_level(e.max_level, bs)
+    klv = R.key_levels(L0, bs)
+    assert L0 == 25
     key = np.random.default_rng(4).integers(0, 256, 16, dtype=np.uint8)
     blocks = np.random.default_rng(6).integers(0, 256, (16, R.n_blk, 16), dtype=np.uint8)
     assert blocks.shape[0] * R.n_blk == 64 * 2048
-    out, nref = R.encrypt_aes128(R.encrypt_blocks(blocks), [R.encrypt_round_key(k) for k in T.expand_key(key)],
-                                 bs, pairs_per_call=2)
+    keys = [R.encrypt_round_key(k, level=lv) for k, lv in zip(T.expand_key(key), klv)]
+    tm = {}
+    out, nref = R.encrypt_aes128(R.encrypt_blocks(blocks, level=L0), keys, bs, timings=tm,
+                                 pairs_per_call=4, consume=True)
     assert nref == 3
+    assert [lv for _, lv, _ in tm["per_round"]] == [lv for _, lv, _ in R.schedule(L0, bs)]
     want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
-    assert np.array_equal(R.decrypt_blocks(out), want)
+    assert np.array_equal(R.decrypt_blocks(out, 16), want)

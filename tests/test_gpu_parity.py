@@ -415,17 +415,20 @@ def test_power_basis_255_full_params_bit_exact(product_lib, oracle_lib, gpu_avai
         np.testing.assert_allclose(g.decrypt(res[0][p - 1], sks[0]), z ** p, atol=1e-3)
 
 
-def test_poly2_int_sbox_shape_bit_exact(product_lib, oracle_lib, gpu_available):
+@pytest.mark.parametrize("scale_bits,wmax", [(40, 8), (44, 16)], ids=["s40w8", "s44w16"])
+def test_poly2_int_sbox_shape_bit_exact(product_lib, oracle_lib, gpu_available, scale_bits, wmax):
     """aesfhe_poly2_int with the S-box's shape at N = 2^16: 15 x and 15 y basis ciphertexts
-    (ny = 16, the compile-time basis size), full and partial output blocks of 4, integer weights
-    in [-8, 8] / 64, mixed basis levels, the top limb q_0 on the folding kernel -- residue for
-    residue against the oracle."""
-    kw = dict(log_n=16, max_level=7, special_primes=3, seed=41)
+    (ny = 16, the compile-time basis size), a full pair of output blocks of 4 (k_poly2_int_s,
+    both blocks in one launch) and a partial block, integer weights in [-wmax, wmax] / 64, mixed
+    basis levels, the top limb q_0 on the folding kernel -- residue for residue against the
+    oracle.  s40w8: y' left unreduced (the AES S-box's case); s44w16: row sums too large for
+    that on 44-bit limbs, so y' is reduced."""
+    kw = dict(log_n=16, max_level=7, special_primes=3, seed=41, scale_bits=scale_bits)
     g, o = _pair(product_lib, oracle_lib, **kw)
     rng = np.random.default_rng(15)
     zx = rng.uniform(-1, 1, (2, g.slot_count))
     zy = rng.uniform(-1, 1, g.slot_count)
-    W = rng.integers(-8, 9, (10, 16, 16))
+    W = rng.integers(-wmax, wmax + 1, (10, 16, 16))
     W[3] = 0
     res = []
     for eng in (g, o):

@@ -88,3 +88,30 @@ def test_sbox_reference_order_either_way(oracle_lib, fuse):
     trace = dict(w.engine.trace)
     assert trace == TRACES["sub_bytes_array"]
     assert np.array_equal(zeta_decode(w.engine.decrypt(out, w.secret_key), modulus=256), T.SBOX[x])
+
+
+def test_deferred_product_errors(oracle_lib):
+    """Deferred products (fhe._ProductCiphertext): what can be checked at the call is checked
+    there -- a relinearization key of another engine raises at multiply(); an error of the
+    evaluation itself surfaces as a RuntimeError at the first use of the handle; at most
+    max_pending products wait unevaluated (the next one evaluates them first)."""
+    e = Engine(_lib=oracle_lib, max_pending=3, **KW)
+    sk = e.create_secret_key(3)
+    rlk = e.create_relinearization_key(sk)
+    other = Engine(_lib=oracle_lib, **KW)
+    ct = e.encrypt(np.ones(8), e.create_public_key(sk), level=5)
+    with pytest.raises(ValueError, match="another engine"):
+        e.multiply(ct, ct, other.create_relinearization_key(other.create_secret_key(3)))
+    # an evaluation error appears at first use (here: the C call reports a device error)
+    real = e._lib.mul
+    try:
+        e._lib.mul = lambda *a: -3
+        p = e.multiply(ct, ct, rlk)
+        assert p.pending and p.level == 4
+        with pytest.raises(RuntimeError, match="device error"):
+            e.decrypt(p, sk)
+    finally:
+        e._lib.mul = real
+    ps = [e.multiply(ct, ct, rlk) for _ in range(5)]
+    assert sum(p.pending for p in ps) <= 3
+    np.testing.assert_allclose(e.decrypt(ps[-1], sk)[:8].real, np.ones(8), atol=1e-3)

@@ -31,7 +31,7 @@ CLASSES = [
     (r"k_modup<", "modup"),
     (r"k_moddown<", "moddown"),
     (r"k_moddown_finish", "moddown_finish"),
-    (r"k_poly2_int<", "poly2_int"),
+    (r"k_poly2_int(<|_mfma)", "poly2_int"),
     (r"k_poly2\b", "poly2"),
     (r"k_gather_batch", "gather"),
     (r"k_lincomb_many", "lincomb_many"),
@@ -108,7 +108,11 @@ def main():
             per[c]["f64_flops_per_launch"] = g["f64"] / n
     fam = [per[c] for c in per if c in NTT_FAMILY]
     nl = sum(p["launches"] for p in fam)
-    out = {"head": a.head,
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from bench import csrc_sha16
+    out = {"head": a.head, "csrc_sha16": csrc_sha16(),
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE" + (" / --pmc SQ_INSTS_VALU_*_F64" if f64_counted else "")
                      + " (separate passes, --kernel-trace) over one bench round step between marker kernels; "
                        "FETCH_SIZE x 2 (gfx950), tools/pmc_traffic.py",
