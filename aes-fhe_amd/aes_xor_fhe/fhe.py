@@ -246,6 +246,44 @@ class _ProductCiphertext(Ciphertext):
         return f"Ciphertext(level={self.level}, batch={self.batch}, npoly=2, deferred product)"
 
 
+class _GaloisCiphertext(Ciphertext):
+    """A deferred automorphism + key switch (``Engine.conjugate``): level, batch and is_zero are
+    the eager result's.  The first use of any pending one evaluates every pending automorphism
+    of the same key and level together -- one ``aesfhe_galois`` over their concatenated batch,
+    then split -- so the reference's runs of single-ciphertext conjugations
+    (xor_service.py:245-254: seven per power basis, two bases per xor_cipher) become a few
+    batched key switches.  The key switch is elementwise over the batch, so every output's
+    residues equal the eager call's."""
+
+    __slots__ = ("_src", "_key", "_mat", "__weakref__")
+
+    def __init__(self, engine: "Engine", src: Ciphertext, key):
+        self._lib, self._free = engine._lib, None
+        self.engine = engine
+        self._src, self._key, self._mat = src, key, None
+        self.level, self.batch, self.npoly, self.is_zero = src.level, src.batch, 2, src.is_zero
+
+    @property
+    def _h(self):
+        if self._mat is None:
+            e = self.engine
+            e._flush_galois(self._key)
+            if self._mat is None:  # left out of an earlier flush that failed: on its own
+                self._mat = e._call_ct(e._lib.galois, self._src._h, self._key._h)
+                self._src = None
+        return self._mat._h
+
+    @property
+    def pending(self) -> bool:
+        return self._mat is None
+
+    def __del__(self):  # the materialised ciphertext frees itself
+        pass
+
+    def __repr__(self):
+        return f"Ciphertext(level={self.level}, batch={self.batch}, npoly=2, deferred galois)"
+
+
 class _LinearCiphertext(Ciphertext):
     """A deferred linear combination: sum_i c_i * ct_i (each term one level below its input, as
     `multiply(ct, constant)` defines it) + sum of ciphertexts + a constant.
@@ -405,6 +443,7 @@ class Engine:
         self._fuse_linear = bool(fuse_linear)
         import weakref
         self._pending = weakref.WeakSet()  # deferred products not yet evaluated
+        self._pending_gal = []  # deferred automorphisms (weak references), in call order
         self._max_pending = int(max_pending)
         if nonce_start is None:
             nonce_start = _urandom64() >> 1 if seed is None else 0
@@ -756,7 +795,44 @@ class Engine:
         return [self._ct(outs[i]) for i in range(degree)]
 
     def conjugate(self, ct: Ciphertext, conjugation_key: ConjugationKey) -> Ciphertext:
+        """Complex conjugation of the slots.  With fuse_linear the call is deferred and batched
+        with the other pending conjugations of its level (_GaloisCiphertext)."""
+        if getattr(conjugation_key, "engine", self) is not self:
+            raise ValueError("conjugate: the key belongs to another engine")
+        if self._fuse_linear and ct.npoly == 2 and not ct.is_zero:
+            import weakref
+            g = _GaloisCiphertext(self, ct, conjugation_key)
+            self._pending_gal.append(weakref.ref(g))
+            if len(self._pending_gal) > self._max_pending:
+                self._flush_galois(None)
+            return g
         return self._call_ct(self._lib.galois, ct._h, conjugation_key._h)
+
+    def _flush_galois(self, key):
+        """Evaluate the pending deferred automorphisms (of `key`, or all): per (key, level), the
+        sources concatenated along the batch, one aesfhe_galois, the result split back."""
+        live = [r() for r in self._pending_gal]
+        live = [g for g in live if g is not None and g._mat is None]
+        todo = [g for g in live if key is None or g._key is key]
+        self._pending_gal = [r for r in self._pending_gal
+                             if r() is not None and r()._mat is None and r() not in todo]
+        groups = {}
+        for g in todo:
+            groups.setdefault((id(g._key), g.level), []).append(g)
+        for grp in groups.values():
+            k = grp[0]._key
+            if len(grp) == 1:
+                g = grp[0]
+                g._mat = self._call_ct(self._lib.galois, g._src._h, k._h)
+            else:
+                cat = self.concat([g._src for g in grp])
+                out = self._call_ct(self._lib.galois, cat._h, k._h)
+                off = 0
+                for g in grp:
+                    g._mat = self.slice(out, off, g.batch)
+                    off += g.batch
+            for g in grp:
+                g._src = None
 
     def rotate(self, ct: Ciphertext, key, delta: int | None = None) -> Ciphertext:
         """np.roll semantics: rotate(ct, key, k) decrypts to np.roll(v, k)."""

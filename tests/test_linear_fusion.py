@@ -115,3 +115,26 @@ def test_deferred_product_errors(oracle_lib):
     ps = [e.multiply(ct, ct, rlk) for _ in range(5)]
     assert sum(p.pending for p in ps) <= 3
     np.testing.assert_allclose(e.decrypt(ps[-1], sk)[:8].real, np.ones(8), atol=1e-3)
+
+
+def test_deferred_conjugations_batched_residue_exact(oracle_lib):
+    """Engine.conjugate is deferred (fhe._GaloisCiphertext) and the pending conjugations of one
+    key and level run as one batched aesfhe_galois: the residues equal the eager calls' (the key
+    switch is elementwise over the batch), levels / batches are the eager ones, and the
+    reference's xor_cipher (seven conjugations per power basis) decodes the same."""
+    (f, skf, pkf), (g, skg, pkg) = _engines(oracle_lib)
+    rng = np.random.default_rng(4)
+    z = rng.uniform(-1, 1, (3, f.slot_count)) + 1j * rng.uniform(-1, 1, (3, f.slot_count))
+    outs = []
+    for e, sk, pk in ((f, skf, pkf), (g, skg, pkg)):
+        cjk = e.create_conjugation_key(sk)
+        cts = [e.encrypt(z[:2], pk, level=7), e.encrypt(z[2], pk, level=7), e.encrypt(z[:2], pk, level=6),
+               e.encrypt(z[1], pk, level=7)]
+        cj = [e.conjugate(c, cjk) for c in cts]
+        assert [(c.level, c.batch) for c in cj] == [(7, 2), (7, 1), (6, 2), (7, 1)]
+        if e is f:
+            assert all(c.pending for c in cj)
+        outs.append([e.export_residues(c) for c in cj])
+        np.testing.assert_allclose(e.decrypt(cj[1], sk), np.conj(z[2]), atol=1e-4)
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)

@@ -31,7 +31,7 @@ CLASSES = [
     (r"k_modup<", "modup"),
     (r"k_moddown<", "moddown"),
     (r"k_moddown_finish", "moddown_finish"),
-    (r"k_poly2_int(<|_mfma)", "poly2_int"),
+    (r"k_poly2_int(_s)?<", "poly2_int"),
     (r"k_poly2\b", "poly2"),
     (r"k_gather_batch", "gather"),
     (r"k_lincomb_many", "lincomb_many"),
