@@ -1,0 +1,73 @@
+"""bench.py's bookkeeping (CPU): the PMC traffic record is used only for the kernels it measured
+(its kernel-source hash) and the workload shape it measured; the per-class table scales the
+record's per-dispatch bytes and FLOPs by dispatches per call, and reports null where the record's
+dispatch count per step is not the profiled one (poly2_int's 4-dispatch calls)."""
+import ctypes as C
+import json
+import sys
+from types import SimpleNamespace
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402
+
+
+def _args(**kw):
+    a = SimpleNamespace(log_n=16, max_level=30, special_primes=10, digit_primes=12, scale_bits=40,
+                        batch=32, layout="sliced")
+    a.__dict__.update(kw)
+    return a
+
+
+def test_csrc_hash_gates_the_pmc_record(tmp_path, monkeypatch):
+    rec = {"csrc_sha16": bench.csrc_sha16(), "workload": {"log_n": 16, "max_level": 30, "special_primes": 10,
+                                                          "digit_primes": 12, "batch": 32, "layout": "sliced"},
+           "ntt_family": {"hbm_bytes_per_launch": 1.0}, "per_kernel": {}}
+    f = tmp_path / "round_traffic.json"
+    monkeypatch.setattr(bench, "PMC_FILE", f)
+    f.write_text(json.dumps(rec))
+    assert bench.pmc_record(_args()) is not None
+    assert bench.pmc_record(_args(batch=16)) is None          # another workload shape
+    rec["csrc_sha16"] = "0" * 16
+    f.write_text(json.dumps(rec))
+    assert bench.pmc_record(_args()) is None                  # measured on other kernels
+    assert bench.pmc_record() is None
+
+
+class _FakeEngine:
+    """engine_profile_kernels of two classes over 2 profiled steps: 'a' one dispatch per call,
+    'b' three dispatches per call (as poly2_int's)."""
+
+    def __init__(self, raw):
+        self.js = json.dumps(raw).encode()
+        self._h = None
+        self._lib = SimpleNamespace(engine_profile_kernels=self._prof)
+
+    def _check(self, rc):
+        assert rc == 0
+
+    def _prof(self, h, buf, cap, need):
+        need._obj.value = len(self.js) + 1
+        if buf is not None:
+            C.memmove(buf, self.js, len(self.js))
+        return 0
+
+
+def test_kernel_table_scales_by_dispatches():
+    raw = {"a": [20, 2.0, 20 * 1e6, 20], "b": [8, 16.0, 8 * 4e7, 24]}  # calls, ms, bytes, dispatches
+    pmc = {"per_kernel": {"a": {"launches": 10, "hbm_bytes_per_launch": 2e6, "f64_flops_per_launch": 1e9},
+                          "b": {"launches": 12, "hbm_bytes_per_launch": 1.4e7, "f64_flops_per_launch": 3e11}}}
+    t = bench.kernel_table(_FakeEngine(raw), pmc, 2)
+    assert t["a"]["dispatches_per_step"] == 10 and t["a"]["hbm_bytes_per_launch"] == 2e6
+    b = t["b"]
+    assert b["launches_per_step"] == 4 and b["dispatches_per_step"] == 12
+    assert b["hbm_bytes_per_launch"] == pytest.approx(3 * 1.4e7)  # per call = 3 dispatches
+    assert b["hbm_over_alg"] == pytest.approx(3 * 1.4e7 / 4e7)
+    assert b["f64_tflops"] == pytest.approx(3 * 3e11 / 2e-3 / 1e12, rel=1e-3)
+    # a record whose dispatch count per step differs from the profiled one gives no figures
+    pmc["per_kernel"]["b"]["launches"] = 16
+    b = bench.kernel_table(_FakeEngine(raw), pmc, 2)["b"]
+    assert b["hbm_bytes_per_launch"] is None and b["pmc_dispatches_mismatch"]["pmc_per_step"] == 16
