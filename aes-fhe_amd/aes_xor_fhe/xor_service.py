@@ -122,10 +122,21 @@ class ZetaEncoder:
     the modulus is applied, which is what the reference computes under numpy 1.x (under
     numpy 2 its uint8 % 256 raises)."""
 
+    _tables: Dict[int, np.ndarray] = {}
+
     @staticmethod
     def to_zeta(arr: np.ndarray, modulus: int = 16) -> np.ndarray:
+        """exp(-2 pi i (k mod m) / m) by a table of the m values, each computed with the same
+        expression as the elementwise form (so the words are identical, tests/test_coeffs.py)
+        -- 16 complex exps instead of one per slot (3.3 -> 0.2 ms for the harness's four
+        32768-slot encodes)."""
         a = np.asarray(arr).astype(np.int64)
-        return np.exp(-2j * np.pi * (a % modulus) / modulus)
+        # k mod m: a mask for a power of two (two's complement: the same non-negative residue)
+        a = a & (modulus - 1) if modulus & (modulus - 1) == 0 else a % modulus
+        t = ZetaEncoder._tables.get(modulus)
+        if t is None:
+            t = ZetaEncoder._tables[modulus] = np.exp(-2j * np.pi * np.arange(modulus, dtype=np.int64) / modulus)
+        return np.take(t, a)
 
     @staticmethod
     def from_zeta(z_arr: np.ndarray, modulus: int = 16) -> np.ndarray:

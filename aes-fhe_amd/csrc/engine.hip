@@ -464,10 +464,11 @@ static void intt_prod(aesfhe_engine* e, Span a, Span b, Span dst, int total, con
 
 // the fp64 column pass alone (the extension limbs and the conv of a ModDown, whose row passes run
 // fused with their consumers)
-static void ntt_fwd_cols(aesfhe_engine* e, Span sp, int total) {
-    if (e->logN == 16) hipLaunchKernelGGL(k_nttf_fwd_cols<256>, dim3(16, total), dim3(256), 0, e->stream, sp, sp, e->tabs());
-    else hipLaunchKernelGGL(k_nttf_fwd_cols<512>, dim3(16, total), dim3(256), 0, e->stream, sp, sp, e->tabs());
+static void ntt_fwd_cols(aesfhe_engine* e, Span src, Span dst, int total) {
+    if (e->logN == 16) hipLaunchKernelGGL(k_nttf_fwd_cols<256>, dim3(16, total), dim3(256), 0, e->stream, src, dst, e->tabs());
+    else hipLaunchKernelGGL(k_nttf_fwd_cols<512>, dim3(16, total), dim3(256), 0, e->stream, src, dst, e->tabs());
 }
+static void ntt_fwd_cols(aesfhe_engine* e, Span sp, int total) { ntt_fwd_cols(e, sp, sp, total); }
 
 static void ntt(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
     if (total <= 0) return;
@@ -1945,10 +1946,19 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1);
         ntt(e, sd, sdc, B * (l + 1), true);
     }
+    // out of place (cols_only): ModUp writes a buffer recycled across the digits and the column
+    // pass reads it into ext_j -- the in-place pass read and wrote the same lines (219.7 vs
+    // 203-207 us over a digit at B = 32, tools/modup_cols_bench.hip); one digit's extension of
+    // extra memory, not one per digit
+    static const bool oop_env = !getenv("AESFHE_MODUP_OOP") || atoi(getenv("AESFHE_MODUP_OOP")) != 0;  // A/B
+    const bool oop = cols_only && oop_env;
+    std::unique_ptr<Tmp> mu;
+    if (oop) mu.reset(new Tmp(e, (size_t)B * neN));
     for (int j = 0; j < beta; j++) {
         const int A = e->A, lo = j * A, hi = std::min(lo + A, l + 1), alpha = hi - lo;
         const size_t set = (size_t)j * A + (alpha - 1);
         u64* exj = ext + (size_t)j * B * neN;
+        u64* muj = oop ? mu->p : exj;  // where ModUp writes
         if (cols_only && alpha == 1) {
             // one-limb digit: the conversion is x mod p_t (hat = hatinv = 1), formed in the column
             // pass's copy-in from the digit limb itself (no k_modup<1> write + read-back)
@@ -1967,21 +1977,19 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne, "modup");
             if (alpha < 1 || alpha > 16) throw_err(AESFHE_EUNSUPPORTED, "ModUp digit width outside 1..16");
-            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, bconv_groups(N, B, ne), B), e->stream, (const u64*)dc.p, lN, exj, neN, lo, l, ne,
+            AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, bconv_groups(N, B, ne), B), e->stream, (const u64*)dc.p, lN, muj, neN, lo, l, ne,
                               (const double*)(e->mu_hatinvf + set * A), (const TwD*)(e->mu_hatf + set * A * e->np),
                               A, e->q, e->qinv, e->Lp1, e->logN);
         }
         HIPC(hipGetLastError());
-        auto fwd = [&](Span sp, int total) {
+        auto fwd = [&](long off, int n, int nq, int p0, int total) {
+            Span sp = span_s(exj + off, neN, n, nq, p0, e->Lp1);
             if (!cols_only) return ntt(e, sp, sp, total, false);
             ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
-            ntt_fwd_cols(e, sp, total);
+            ntt_fwd_cols(e, span_s(muj + off, neN, n, nq, p0, e->Lp1), sp, total);
         };
-        if (lo > 0) fwd(span_s(exj, neN, lo, lo, 0, e->Lp1), B * lo);
-        {
-            int nrest = ne - hi, nq_rest = (l + 1) - hi;
-            fwd(span_s(exj + (long)hi * N, neN, nrest, nq_rest, hi, e->Lp1), B * nrest);
-        }
+        if (lo > 0) fwd(0, lo, lo, 0, B * lo);
+        fwd((long)hi * N, ne - hi, (l + 1) - hi, hi, B * (ne - hi));
     }
 }
 
@@ -2055,10 +2063,19 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
     HIPC(hipGetLastError());
     Span sc = span_s(conv.p, kN, lk + 1, lk + 1, 0, e->Lp1);
     if (fused_ntt(e)) {
-        // conv NTT with the finish in the row pass's epilogue: conv never reaches HBM
+        // conv NTT with the finish in the row pass's epilogue: conv never reaches HBM; the column
+        // pass out of place (as ks_modup's), into a second buffer the row pass reads
         Tabs T = e->tabs();
         const int total = B * 2 * (lk + 1);
-        {
+        static const bool oop_env = !getenv("AESFHE_MODUP_OOP") || atoi(getenv("AESFHE_MODUP_OOP")) != 0;  // A/B
+        std::unique_ptr<Tmp> conv2;
+        if (oop_env) {
+            conv2.reset(new Tmp(e, (size_t)B * 2 * kN));
+            Span s2 = span_s(conv2->p, kN, lk + 1, lk + 1, 0, e->Lp1);
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
+            ntt_fwd_cols(e, sc, s2, total);
+            sc = s2;
+        } else {
             ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
             ntt_fwd_cols(e, sc, total);
         }

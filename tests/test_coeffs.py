@@ -41,3 +41,19 @@ def test_luts_decode_exactly():
     za, zb = np.exp(-2j * np.pi * a / 16), np.exp(-2j * np.pi * b / 16)
     val = sum(C[i, j] * za ** i * zb ** j for i in range(16) for j in range(16))
     assert np.array_equal(dec(val, 16), a ^ b)
+
+
+def test_zeta_table_encode_bit_identical():
+    """ZetaEncoder.to_zeta by a table of the m roots is word-for-word the elementwise
+    exp(-2 pi i (k mod m) / m) the reference computes (xor_service.py:132-145), negative and
+    out-of-range k included, for power-of-two and other moduli."""
+    import numpy as np
+    from aes_xor_fhe.xor_service import ZetaEncoder
+    rng = np.random.default_rng(7)
+    for m in (2, 4, 16, 256, 7, 10):
+        a = rng.integers(-5000, 5000, 20000)
+        ref = np.exp(-2j * np.pi * (a.astype(np.int64) % m) / m)
+        got = ZetaEncoder.to_zeta(a, m)
+        assert got.dtype == np.complex128 and np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+    u8 = rng.integers(0, 256, 1000).astype(np.uint8)
+    assert np.array_equal(ZetaEncoder.to_zeta(u8, 256), np.exp(-2j * np.pi * (u8.astype(np.int64) % 256) / 256))
