@@ -1947,11 +1947,10 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         ntt(e, sd, sdc, B * (l + 1), true);
     }
     // out of place (cols_only): ModUp writes a buffer recycled across the digits and the column
-    // pass reads it into ext_j -- the in-place pass read and wrote the same lines (219.7 vs
-    // 203-207 us over a digit at B = 32, tools/modup_cols_bench.hip); one digit's extension of
-    // extra memory, not one per digit
-    static const bool oop_env = !getenv("AESFHE_MODUP_OOP") || atoi(getenv("AESFHE_MODUP_OOP")) != 0;  // A/B
-    const bool oop = cols_only && oop_env;
+    // pass reads it into ext_j -- the in-place pass read and wrote the same lines; one digit's
+    // extension of extra memory, not one per digit (with the ModDown conv pass out of place as
+    // well: round +0.8 %, A/B/A/B/A on one box, profiles/r04/ab/oop/)
+    const bool oop = cols_only;
     std::unique_ptr<Tmp> mu;
     if (oop) mu.reset(new Tmp(e, (size_t)B * neN));
     for (int j = 0; j < beta; j++) {
@@ -2067,17 +2066,12 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
         // pass out of place (as ks_modup's), into a second buffer the row pass reads
         Tabs T = e->tabs();
         const int total = B * 2 * (lk + 1);
-        static const bool oop_env = !getenv("AESFHE_MODUP_OOP") || atoi(getenv("AESFHE_MODUP_OOP")) != 0;  // A/B
-        std::unique_ptr<Tmp> conv2;
-        if (oop_env) {
-            conv2.reset(new Tmp(e, (size_t)B * 2 * kN));
-            Span s2 = span_s(conv2->p, kN, lk + 1, lk + 1, 0, e->Lp1);
+        Tmp conv2(e, (size_t)B * 2 * kN);
+        {
+            Span s2 = span_s(conv2.p, kN, lk + 1, lk + 1, 0, e->Lp1);
             ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
             ntt_fwd_cols(e, sc, s2, total);
             sc = s2;
-        } else {
-            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
-            ntt_fwd_cols(e, sc, total);
         }
         RowFin f{(const u64*)acc, 2 * neN, neN, Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}, o->d,
                  2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf, lk + 1};

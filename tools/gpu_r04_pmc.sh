@@ -17,4 +17,4 @@ run fetch FETCH_SIZE \
  && run f64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 \
  && run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SMEM \
  && run tcc TCC_HIT_sum TCC_MISS_sum \
- && TAG=${TAG}_boot bash tools/gpu_r04_bootprof.sh
+ && if [ -z "$NOBOOT" ]; then TAG=${TAG}_boot bash tools/gpu_r04_bootprof.sh; fi
