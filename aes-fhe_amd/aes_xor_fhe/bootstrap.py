@@ -109,7 +109,7 @@ class Bootstrapper:
     def __init__(self, engine: Engine, sk, rlk, cjk=None, *, hw: int = 32, K: float = 12.0,
                  r: int = 3, deg: int = 31, groups: int = 3, seed: int = 7,
                  bits_deg: int | None = None, bits_r: int | None = None, lazy: bool = True, baby_scale: int = 2,
-                 bits_opt: bool = True, cts_groups: int | None = None):
+                 bits_opt: bool = True, cts_groups: int | None = None, stc_baby_scale: float | None = None):
         # cts_groups: CoeffToSlot's stages merged into this many maps (default `groups`, which
         # StC keeps): more groups = more levels, far fewer diagonals per map
         cts_groups = groups if cts_groups is None else cts_groups
@@ -135,6 +135,10 @@ class Bootstrapper:
         # split takes baby_scale x more of them (fewer giants)
         self.lazy = lazy
         self.baby_scale = baby_scale if lazy else 1
+        # SlotToCoeff runs at the bottom levels, where the K special primes are most of every
+        # limb set: a giant's key switch costs about what a baby's Q u P ciphertext costs to
+        # write and read back, so its split may take fewer babies (stc_baby_scale)
+        self.stc_baby_scale = self.baby_scale if stc_baby_scale is None or not lazy else stc_baby_scale
         # sparse-secret encapsulation keys
         s_sparse = e.create_sparse_secret_key(hw, seed)
         self.to_sparse = e.create_switching_key(sk, s_sparse)
@@ -164,8 +168,9 @@ class Bootstrapper:
         # bit mode: slots b + i b' -> coefficients (q0 / 4) (b, b') at level 0
         c_bits = q0 / (4.0 * D[0])
         stc_bits[-1] = {d: v * c_bits for d, v in stc_bits[-1].items()}
-        self.cts, self.stc = [self._prepare(M) for M in cts], [self._prepare(M) for M in stc]
-        self.stc_bits = [self._prepare(M) for M in stc_bits]
+        self.cts = [self._prepare(M) for M in cts]
+        self.stc = [self._prepare(M, self.stc_baby_scale) for M in stc]
+        self.stc_bits = [self._prepare(M, self.stc_baby_scale) for M in stc_bits]
         self.cts_bits = [self._prepare(M) for M in cts_bits] if bits_opt else self.cts
         # rotation keys: hoisted keys for the baby steps (one ModUp per group input), ordinary
         # keys for the giant steps
@@ -232,9 +237,10 @@ class Bootstrapper:
         f = np.cos(2 * np.pi * (bnd * xs - 0.25) / (1 << r))
         return np.polynomial.chebyshev.chebfit(xs, f, deg)
 
-    def _prepare(self, M: Dict[int, np.ndarray]):
+    def _prepare(self, M: Dict[int, np.ndarray], baby_scale: float | None = None):
         u, ks, g = _bsgs_plan(list(M), self.n)
-        g = min(g * self.baby_scale, 1 << max(0, math.ceil(math.log2(max(ks) - min(ks) + 1))))
+        scale = self.baby_scale if baby_scale is None else baby_scale
+        g = min(max(1, int(g * scale)), 1 << max(0, math.ceil(math.log2(max(ks) - min(ks) + 1))))
         giants = sorted({(k - (k % g)) // g for k in ks})
         terms = {}
         for k in ks:

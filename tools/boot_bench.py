@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1, help="ciphertext pairs per call")
     ap.add_argument("--phases", action="store_true", help="also time each bootstrap phase")
     ap.add_argument("--baby-scale", type=int, default=2, help="BSGS baby steps x this (lazy mode)")
+    ap.add_argument("--stc-baby-scale", type=float, default=None, help="the same for the SlotToCoeff maps")
     ap.add_argument("--eager", action="store_true", help="rotate_hoisted + dot_pt + galois linear maps")
     ap.add_argument("--no-opt", action="store_true", help="bit mode without bits_opt (c_in multiply, depth-6 Chebyshev)")
     ap.add_argument("--cts-groups", type=int, default=None, help="CoeffToSlot maps (default: groups = 3)")
@@ -37,7 +38,7 @@ def main():
     sk = e.create_secret_key(1)
     pk = e.create_public_key(sk)
     t = time.time()
-    bs = Bootstrapper(e, sk, e.create_relinearization_key(sk), lazy=not a.eager, baby_scale=a.baby_scale,
+    bs = Bootstrapper(e, sk, e.create_relinearization_key(sk), lazy=not a.eager, baby_scale=a.baby_scale, stc_baby_scale=a.stc_baby_scale,
                       bits_opt=not a.no_opt, cts_groups=a.cts_groups)
     e.synchronize()
     setup = time.time() - t
