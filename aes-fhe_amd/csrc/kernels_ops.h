@@ -1009,6 +1009,32 @@ __global__ void __launch_bounds__(256, MO > 4 ? 2 : 3) k_poly2_int(const u64* co
     }
 }
 
+// a = w_0 c0 + sum_j w_j y'_j (polynomial 0) and a' = sum_j w_j y''_j (polynomial 1): exact FMAs
+// (the sums stay below 2^52), or for BIG limbs remainder products folded as they are added
+template <int NY, bool BIG>
+__device__ __forceinline__ void inner_sums(const double* __restrict__ w, double c0, const double (&y0)[NY - 1],
+                                           const double (&y1)[NY - 1], double q, double qi, double& a0, double& a1) {
+    if constexpr (!BIG) {
+        a0 = w[0] * c0;  // exact: |w0| <= 1024, c0 < 2^45
+        a1 = 0.0;
+#pragma unroll
+        for (int j = 1; j < NY; j++) {
+            a0 = __builtin_fma(w[j], y0[j - 1], a0);
+            a1 = __builtin_fma(w[j], y1[j - 1], a1);
+        }
+    } else {
+        const double w0 = w[0];
+        a0 = fmul_rem(c0, w0, w0 * qi, q);
+        a1 = 0.0;
+#pragma unroll
+        for (int j = 1; j < NY; j++) {
+            const double wj = w[j], wjq = wj * qi;
+            a0 = fred(a0 + fmul_rem(y0[j - 1], wj, wjq, q), q, qi);
+            a1 = fred(a1 + fmul_rem(y1[j - 1], wj, wjq, q), q, qi);
+        }
+    }
+}
+
 // k_poly2_int's exact path (BIG = false) for the S-box shape: the full 16-term y basis, whole
 // blocks of MO outputs (no per-output guards), the x^0 term peeled out of the monomial loop (no
 // per-monomial branches), and LAZY: y' = H y left unreduced (|y'| <= q instead of q/2 + 1: the
@@ -1019,7 +1045,10 @@ __global__ void __launch_bounds__(256, MO > 4 ? 2 : 3) k_poly2_int(const u64* co
 // Both output blocks (t0 .. t0 + MO - 1 and t0 + MO .. t0 + 2 MO - 1) in one launch: workgroups b
 // and b + 8 -- dealt to the same XCD -- take the same 256 coefficients, one block each, so the
 // second one's x / y reads hit that XCD's L2 instead of HBM.  grid (2 N/256, run, B).
-template <int MO, bool LAZY>
+// BIG (q_0 and other limbs past the exact-FMA bound): every inner-sum term a remainder product,
+// folded as it is added, and the tensor accumulators folded per monomial (k_poly2_int<true>'s
+// arithmetic), so the whole 8-output block of those limbs is one launch as well.
+template <int MO, bool LAZY, bool BIG = false>
 __global__ void __launch_bounds__(256, 3) k_poly2_int_s(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
                         const long* __restrict__ xps, int nx, const u64* const* __restrict__ yp,
                         const long* __restrict__ ybs, const long* __restrict__ yps,
@@ -1029,6 +1058,7 @@ __global__ void __launch_bounds__(256, 3) k_poly2_int_s(const u64* const* __rest
                         const u64* __restrict__ qs, const double* __restrict__ qinv, int l0, int nl,
                         int logN, int orot) {
     constexpr int NY = kPoly2Max;
+    static_assert(!(BIG && LAZY), "the folding path needs reduced y'");
     const int bx = blockIdx.x, half = (bx >> 3) & 1;            // blocks b, b + 8: one XCD
     const int k = (((bx >> 4) << 3) | (bx & 7)) * blockDim.x + threadIdx.x;
     const int l = l0 + blockIdx.y, bb = blockIdx.z;
@@ -1057,12 +1087,8 @@ __global__ void __launch_bounds__(256, 3) k_poly2_int_s(const u64* const* __rest
 #pragma unroll
         for (int t = 0; t < MO; t++) {
             const double* w = Wt + (size_t)(t0 + t) * nx * NY;
-            double a0 = w[0] * c0, a1 = 0.0;
-#pragma unroll
-            for (int j = 1; j < NY; j++) {
-                a0 = __builtin_fma(w[j], y0[j - 1], a0);
-                a1 = __builtin_fma(w[j], y1[j - 1], a1);
-            }
+            double a0, a1;
+            inner_sums<NY, BIG>(w, c0, y0, y1, q, qi, a0, a1);
             d0[t] = a0;
             d1[t] = a1;
             d2[t] = 0.0;
@@ -1079,16 +1105,17 @@ __global__ void __launch_bounds__(256, 3) k_poly2_int_s(const u64* const* __rest
 #pragma unroll
             for (int t = 0; t < MO; t++) {
                 const double* w = Wt + ((size_t)(t0 + t) * nx + i) * NY;
-                double a0 = w[0] * c0, a1 = 0.0;
-#pragma unroll
-                for (int j = 1; j < NY; j++) {
-                    a0 = __builtin_fma(w[j], y0[j - 1], a0);
-                    a1 = __builtin_fma(w[j], y1[j - 1], a1);
-                }
+                double a0, a1;
+                inner_sums<NY, BIG>(w, c0, y0, y1, q, qi, a0, a1);
                 const double a0q = a0 * qi, a1q = a1 * qi;
                 d0[t] += fmul_rem(xa, a0, a0q, q);
                 d1[t] += fmul_rem(xa, a1, a1q, q) + fmul_rem(xb, a0, a0q, q);
                 d2[t] += fmul_rem(xb, a1, a1q, q);
+                if constexpr (BIG) {
+                    d0[t] = fred(d0[t], q, qi);
+                    d1[t] = fred(d1[t], q, qi);
+                    d2[t] = fred(d2[t], q, qi);
+                }
             }
         }
     }
