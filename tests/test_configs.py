@@ -106,6 +106,24 @@ def test_config5_aes128_ten_rounds(product_lib, gpu_available):
     assert bytes(got[0, 0]) == bytes.fromhex("69c4e0d86a7b0430d8cdb78070b4c55a")
 
 
+@pytest.mark.gpu
+def test_config5_sliced_round(product_lib, gpu_available):
+    """Config 5's shard in the bench's layout (the config5_shard leg): the fully sliced state at
+    N = 2^17, L = 35, K = 12 with the widest key-switch digits, one slab of 4 sets (65 536 blocks)
+    through a middle round from the top level, FIPS-197 for every block."""
+    from aes_xor_fhe.aes_round_bits import AESSlicedRound
+    from aes_xor_fhe.fhe import Engine, widest_digits
+    e = Engine(_lib=product_lib, seed=29, digit_primes=widest_digits(**CONFIG5, lib=product_lib), **CONFIG5)
+    sk = e.create_secret_key()
+    R = AESSlicedRound(e, sk, e.create_public_key(sk), e.create_relinearization_key(sk))
+    assert R.n_blk == 16384
+    blocks = np.random.default_rng(31).integers(0, 256, (4, R.n_blk, 16), dtype=np.uint8)
+    rk = np.random.default_rng(32).integers(0, 256, 16, dtype=np.uint8)
+    out = R.round(R.encrypt_blocks(blocks), R.encrypt_round_key(rk))
+    assert out[0][0].level == 35 - 7
+    assert np.array_equal(R.decrypt_blocks(out, 4), T.aes_round(blocks, rk))
+
+
 # config 4 at the bench's parameters (bench.py defaults: scale 40, K = 10)
 CONFIG4 = dict(log_n=16, max_level=30, special_primes=10, scale_bits=40)
 

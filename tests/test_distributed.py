@@ -25,11 +25,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, so, result_q):
+def _worker(rank, world, init, so, result_q):
     sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         from aes_xor_fhe._abi import Lib
         from aes_xor_fhe.fhe import Engine
@@ -59,11 +58,10 @@ def _worker(rank, world, port, so, result_q):
         dist.destroy_process_group()
 
 
-def _worker_rows(rank, world, port, so, result_q):
+def _worker_rows(rank, world, init, so, result_q):
     sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         from aes_xor_fhe._abi import Lib
         from aes_xor_fhe.fhe import Engine
@@ -99,7 +97,7 @@ def _worker_rows(rank, world, port, so, result_q):
         dist.destroy_process_group()
 
 
-def _worker_sliced(rank, world, port, so, result_q):
+def _worker_sliced(rank, world, init, so, result_q):
     """The bench's default state (AESSlicedRound, 12-prime digits over K = 10): rank 0 encrypts
     three slabs (12 sets, the last one partly padding), scattered in whole slabs
     (granule = AESSlicedRound.GRANULE = 4: rank 0 gets two slabs, rank 1 one -- an element split
@@ -107,8 +105,7 @@ def _worker_sliced(rank, world, port, so, result_q):
     S-box, the batch-4 round key read cyclically), and rank 0 gathers and checks FIPS-197."""
     sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         from aes_xor_fhe._abi import Lib
         from aes_xor_fhe.fhe import Engine
@@ -133,13 +130,12 @@ def _worker_sliced(rank, world, port, so, result_q):
         dist.destroy_process_group()
 
 
-def _worker_keys(rank, world, port, so, result_q):
+def _worker_keys(rank, world, init, so, result_q):
     """shared_seed is one 256-bit value on every rank; engines built from it pass the key check;
     engines with their own seeds make scatter raise on every rank; an all-empty gather is None."""
     sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         import torch
         from aes_xor_fhe._abi import Lib
@@ -175,8 +171,11 @@ def _spawn(target, so, world=2, timeout=900):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, so, q)) for r in range(world)]
+    # a file store per test, not a probed TCP port: concurrent test processes (pytest -n) cannot
+    # race for the same rendezvous port
+    import tempfile
+    init = "file://" + os.path.join(tempfile.mkdtemp(prefix="aesfhe_pg_"), "store")
+    procs = [ctx.Process(target=target, args=(r, world, init, so, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
