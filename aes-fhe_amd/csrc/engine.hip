@@ -2022,7 +2022,7 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
         const Opnd none{nullptr, 0, 0, 0};
         auto kern = pb ? (R == 256 ? k_nttf_rows_ks<1, 256, true> : k_nttf_rows_ks<1, 512, true>)
                        : (R == 256 ? k_nttf_rows_ks<1, 256, false> : k_nttf_rows_ks<1, 512, false>);
-        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, e->A, l, ne, e->tabs(), addend, pm, (int)accum, pb ? *pb : none, fac, pc ? *pc : none);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d, 2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, e->A, l, ne, e->tabs(), addend, pm, (int)accum, pb ? *pb : none, fac, pc ? *pc : none, 0, ne, KsFin{});
     } else {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)ne * (beta * B + 2.0 * beta + 2.0 * B * (accum ? 2 : 1)), "ks_inner");
         auto inner = beta <= 4 ? k_ks_inner_all<4> : beta <= 8 ? k_ks_inner_all<8> : k_ks_inner_all<12>;
@@ -2034,7 +2034,10 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
 // Key switch, second half, part 2: ModDown of acc (2 components, layout [B][2][l+1+K][N]; its
 // dropped limbs are overwritten) by D = P q_l ... q_{l-r+1} (fused with r rescales, DESIGN.md
 // 3.12) into o (level l - r) = (acc - conv) D^{-1} + fin_add.
-static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fin_add, aesfhe_ct* o) {
+// ModDown, first part: INTT of acc's dropped limbs (top r Q limbs + the special limbs, layout
+// [B][2][l+1+K][N]) and their exact base conversion to the lk + 1 = l - r + 1 kept limbs, into conv
+// ([B][2][lk+1][N], coefficient form).  Returns D^{-1} mod q_i (as w / q) for the finish.
+static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int r, u64* conv) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long neN = (long)ne * N;
     if (r < 0 || r > kMdrMaxR || K + r > kMdrMaxE || l - r < 0) throw_err(AESFHE_EARG, "bad combined rescale depth %d", r);
@@ -2049,17 +2052,26 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
     const double* invf = r ? e->mdr_invf + cell * kMdrMaxE : e->md_phatinvf;
     const TwD* hatf = r ? e->mdr_hatf + cell * kMdrMaxE * e->Lp1 : e->md_phatf;
     const int hs = r ? kMdrMaxE : K;  // hatf row stride (sources of one target)
-    const u64* dinv = r ? e->mdr_dinv + cell * e->Lp1 : e->md_pinv;
-    const double* dinvf = r ? e->mdr_dinvf + cell * e->Lp1 : e->md_pinvf;
-    Tmp conv(e, (size_t)B * 2 * kN);
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1), "moddown");
         if (K + r < 1 || K + r > 16) throw_err(AESFHE_EUNSUPPORTED, "ModDown source width outside 1..16");
-        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, bconv_groups(N, B * 2, lk + 1), B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv.p, 2 * kN, kN,
+        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, bconv_groups(N, B * 2, lk + 1), B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv, 2 * kN, kN,
                            invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv,
                            r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN, hs);
     }
     HIPC(hipGetLastError());
+    return r ? e->mdr_dinvf + cell * e->Lp1 : e->md_pinvf;
+}
+
+static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fin_add, aesfhe_ct* o) {
+    const int N = e->N, K = e->K, ne = l + 1 + K;
+    const long neN = (long)ne * N;
+    const int lk = l - r;  // output level
+    const long kN = (long)(lk + 1) * N;
+    Tmp conv(e, (size_t)B * 2 * kN);
+    const double* dinvf = moddown_conv(e, acc, B, l, r, conv.p);
+    const size_t cell = r ? (size_t)(r - 1) * e->Lp1 + l : 0;
+    const u64* dinv = r ? e->mdr_dinv + cell * e->Lp1 : e->md_pinv;
     Span sc = span_s(conv.p, kN, lk + 1, lk + 1, 0, e->Lp1);
     if (fused_ntt(e)) {
         // conv NTT with the finish in the row pass's epilogue: conv never reaches HBM; the column
@@ -2089,14 +2101,82 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
 }
 
 
+// Key switch, second half, for fused_ntt engines (ext holds column-pass intermediates), with the
+// ModDown finish fused into the Q limbs' row pass: k_nttf_rows_ks runs twice --
+//   1. the dropped limbs t = lk + 1 .. l + K (top r Q limbs + P) into acc, as ks_inner_acc;
+//   2. ModDown's INTT of those, the base conversion (conv) and conv's column pass (conv2);
+//   3. the kept limbs t = 0 .. lk (FIN): the inner product, conv's row pass and the finish
+//      (acc - conv) D^{-1} (+ fin_add) written straight into o.
+// The kept limbs' accumulators (2 B (lk + 1) limbs) are neither written nor read back, which is
+// what the unfused order (ks_inner_acc over every limb, then moddown_acc's finishing row pass)
+// spends on them.  Residues identical: every step is exact mod q, outputs canonical.
+// pmod: P * addend joins the accumulators (combined ModDown + rescale, 3.12; the giants of
+// aesfhe_linear_bsgs with r = 0).  pb / fac / pc: the product relinearisation of keyswitch_prod
+// (k_nttf_rows_ks PROD).  acc_in / accum: add to the accumulators of earlier key switches in
+// acc_in (layout [B][2][l+1+K][N]; the last giant of aesfhe_linear_bsgs) instead of a fresh sum.
+static void ks_finish_fused(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, int B, int l,
+                            const aesfhe_key* k, Opnd addend, bool pmod, int r, Opnd fin_add, aesfhe_ct* o,
+                            const Opnd* pb = nullptr, const u64* fac = nullptr, const Opnd* pc = nullptr,
+                            u64* acc_in = nullptr, bool accum = false) {
+    const int N = e->N, K = e->K, ne = l + 1 + K, R = N / 256;
+    const long neN = (long)ne * N;
+    const int beta = ks_beta(e, l), lk = l - r;
+    if (r < 0 || r > kMdrMaxR || K + r > kMdrMaxE || lk < 0) throw_err(AESFHE_EARG, "bad combined rescale depth %d", r);
+    if (pb && r < 1) throw_err(AESFHE_EARG, "product key switch needs the fused combined path");
+    const long kN = (long)(lk + 1) * N;
+    const double* pm = pmod ? (const double*)e->pmodf : (const double*)nullptr;
+    const Opnd none{nullptr, 0, 0, 0};
+    if (accum && (!acc_in || pb)) throw_err(AESFHE_EARG, "accumulating key switch without accumulators");
+    // bytes of a launch over limbs [t0, t0 + nt), nq of them Q limbs: ext rows (every digit but
+    // the limb's own), the own digit's d rows and the addend (PROD: a0, a1, b0, b1 [, c0, c1]),
+    // the key words, and the outputs (acc: 2 B nt limbs; FIN: conv read + out written, + fin_add)
+    auto bytes = [&](int nt, int nq, bool fin) {
+        const double opw = pb ? (4.0 + (pc && pc->ptr ? 2.0 : 0.0)) * nq
+                              : (double)nq + (pm && addend.ptr ? (double)addend.np * nq : 0.0);
+        const double outw = (fin ? 2.0 * 2 * nq + (fin_add.ptr ? (double)fin_add.np * nq : 0.0) : 2.0 * nt) +
+                            (accum ? 2.0 * nt : 0.0);  // accum: the earlier sums read
+        return 8.0 * N * ((double)B * ((double)beta * nt - nq + opw + outw) + 2.0 * beta * nt);
+    };
+    auto launch = [&](int t0, int nt, bool fin, u64* acc, const KsFin& kf) {
+        const int blocks = 8 * B * (nt * (R / 8) / 8 + ((nt * (R / 8)) % 8 ? 1 : 0));
+        const int nq = std::max(0, std::min(t0 + nt, l + 1) - t0);
+        ProfScope ps(e, FAM_KS, bytes(nt, nq, fin), fin ? "ks_rows_fin" : "ks_rows_inner");
+        auto kern = R == 256 ? (pb ? (fin ? k_nttf_rows_ks<1, 256, true, true> : k_nttf_rows_ks<1, 256, true, false>)
+                                   : (fin ? k_nttf_rows_ks<1, 256, false, true> : k_nttf_rows_ks<1, 256, false, false>))
+                             : (pb ? (fin ? k_nttf_rows_ks<1, 512, true, true> : k_nttf_rows_ks<1, 512, true, false>)
+                                   : (fin ? k_nttf_rows_ks<1, 512, false, true> : k_nttf_rows_ks<1, 512, false, false>));
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d,
+                           2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, e->A, l, ne, e->tabs(), addend, pm,
+                           (int)accum, pb ? *pb : none, fac, pc ? *pc : none, t0, nt, kf);
+        HIPC(hipGetLastError());
+    };
+    std::unique_ptr<Tmp> own;  // only the dropped limbs lk + 1 .. ne - 1 are written
+    if (!acc_in) own.reset(new Tmp(e, (size_t)B * 2 * neN));
+    u64* acc = acc_in ? acc_in : own->p;
+    launch(lk + 1, ne - (lk + 1), false, acc, KsFin{});
+    Tmp conv(e, (size_t)B * 2 * kN);
+    const double* dinvf = moddown_conv(e, acc, B, l, r, conv.p);
+    Tmp conv2(e, (size_t)B * 2 * kN);
+    {
+        const int total = B * 2 * (lk + 1);
+        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
+        ntt_fwd_cols(e, span_s(conv.p, kN, lk + 1, lk + 1, 0, e->Lp1), span_s(conv2.p, kN, lk + 1, lk + 1, 0, e->Lp1), total);
+    }
+    HIPC(hipGetLastError());
+    const KsFin kf{conv2.p, 2 * kN, kN, o->d, 2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf,
+                   Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}};
+    launch(0, lk + 1, true, acc, kf);
+}
+
 // Key switch, second half: inner product of ext (ks_modup of d) with key k, ModDown (fused with
 // r rescales) and the finish into o (+ addend).  ext_cols: see ks_inner_acc.
 static void ks_apply(aesfhe_engine* e, const u64* d, long dbs, const u64* ext, int B, int l,
                      const aesfhe_key* k, Opnd addend, aesfhe_ct* o, int r, bool ext_cols = false) {
-    Tmp acc(e, (size_t)B * 2 * (l + 1 + e->K) * e->N);
-    ks_inner_acc(e, d, dbs, ext, B, l, k, addend, r != 0, acc.p, ext_cols);
     Opnd fin_add = addend;
     if (r) fin_add.ptr = nullptr;  // already inside the accumulators (times P)
+    if (ext_cols) return ks_finish_fused(e, d, dbs, ext, B, l, k, addend, r != 0, r, fin_add, o);
+    Tmp acc(e, (size_t)B * 2 * (l + 1 + e->K) * e->N);
+    ks_inner_acc(e, d, dbs, ext, B, l, k, addend, r != 0, acc.p, ext_cols);
     moddown_acc(e, acc.p, B, l, r, fin_add, o);
 }
 
@@ -2123,9 +2203,7 @@ static void keyswitch_prod(aesfhe_engine* e, const Opnd& pa, const Opnd& pb, int
     const long neN = (long)(l + 1 + e->K) * e->N;
     Tmp ext(e, (size_t)ks_beta(e, l) * B * neN);
     ks_modup(e, nullptr, 0, B, l, ext.p, true, &pa, &pb, fac);
-    Tmp acc(e, (size_t)B * 2 * neN);
-    ks_inner_acc(e, nullptr, 0, ext.p, B, l, k, pa, true, acc.p, true, false, &pb, fac, pc);
-    moddown_acc(e, acc.p, B, l, r, Opnd{nullptr, 0, 0, 0}, o);
+    ks_finish_fused(e, nullptr, 0, ext.p, B, l, k, pa, true, r, Opnd{nullptr, 0, 0, 0}, o, &pb, fac, pc);
 }
 
 static aesfhe_ct* relin_ct(aesfhe_engine* e, const aesfhe_ct* c, const aesfhe_key* rlk) {
@@ -2473,6 +2551,10 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
         const long ne2N = (long)ne2 * N, l2N = (long)(l2 + 1) * N;
         std::unique_ptr<Tmp> accg;
         const bool fuse = fused_ntt(e);
+        int last = -1;  // the last keyed giant: its key switch carries the ModDown (fused_ntt engines)
+        for (int j = 0; j < ng; j++)
+            if (gkeys[j]) last = j;
+        aesfhe_ct* fused_out = nullptr;
         for (int j = 0; j < ng; j++) {
             if (!gkeys[j]) {
                 if (!sumq) {
@@ -2496,9 +2578,25 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             ks_modup(e, sg.p + l2N, 2 * l2N, B, l2, ext.p, fuse);
             const bool first = !accg;
             if (first) accg.reset(new Tmp(e, (size_t)B * 2 * ne2N));
+            if (fuse && j == last) {
+                // the sum's ModDown by P fused into this key switch's row pass (ks_finish_fused):
+                // the kept limbs' accumulators are finished in registers, with sumq added
+                fused_out = ct_new(e, B, 2, l2);
+                Opnd add = sumq ? opnd(view_of(sumq), B) : Opnd{nullptr, 0, 0, 0};
+                try {
+                    ks_finish_fused(e, sg.p + l2N, 2 * l2N, ext.p, B, l2, gkeys[j], s0, true, 0, add, fused_out,
+                                    nullptr, nullptr, nullptr, accg->p, !first);
+                } catch (...) {
+                    aesfhe_ct_free(fused_out);
+                    throw;
+                }
+                if (sumq) aesfhe_ct_free(sumq);
+                sumq = fused_out;
+                continue;
+            }
             ks_inner_acc(e, sg.p + l2N, 2 * l2N, ext.p, B, l2, gkeys[j], s0, true, accg->p, fuse, !first);
         }
-        if (accg) {
+        if (accg && !fused_out) {
             aesfhe_ct* r = ct_new(e, B, 2, l2);
             Opnd add = sumq ? opnd(view_of(sumq), B) : Opnd{nullptr, 0, 0, 0};
             moddown_acc(e, accg->p, B, l2, 0, add, r);

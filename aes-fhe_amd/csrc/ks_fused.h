@@ -137,14 +137,31 @@ __device__ __forceinline__ void row_ntt8_stages(double (&x)[8], double* sr, int 
 // |x| < 3q before the P / key product.  fac (optional; aesfhe_mul_fma): per-prime {alpha, C, K};
 // the product becomes alpha (a (x) b) + C (c0, c1, 0) + (K, 0, 0) (pc = c, absent: no C term),
 // |x| < 4.5q + K before the P / key product.
-template <int G, int R = 256, bool PROD = false>
+//
+// Target limbs t0 .. t0 + nt - 1 only (the grid covers nt limbs).  FIN (G = 1, no accum): the
+// ModDown finish of the key switch in the epilogue, for Q limbs t <= lk (engine.hip
+// ks_finish_fused): the limb's two accumulators never reach HBM.  The conv limbs (column pass
+// done, raw doubles, fin.conv[b][c][t]) get their row pass here -- same prime, same row, so the
+// staged twiddles serve them -- and out[b][c][t] = (acc_c - conv_c) D^{-1} (+ fin.add_c) is
+// written canonical; the dropped limbs (t > lk) ran through the non-FIN launch first, into acc.
+struct KsFin {
+    const u64* conv;
+    long cbs, cps;
+    u64* out;
+    long obs, ops;
+    const double* dinvf;  // D^{-1} mod q_t as w / q
+    Opnd2 add;            // plain ModDown (r = 0): the addend joins here, not in the accumulators
+};
+template <int G, int R = 256, bool PROD = false, bool FIN = false>
 __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64* __restrict__ d, long dbs,
                                                       const u64* __restrict__ ext, long exs, long exj,
                                                       const u64* __restrict__ key, long kdig, long kcomp,
                                                       u64* __restrict__ acc, long abs_, long acs, int B,
                                                       int beta, int K, int l, int ne, Tabs T, Opnd addend,
                                                       const double* __restrict__ pmodf, int accum, Opnd pb,
-                                                      const u64* __restrict__ fac, Opnd pc) {
+                                                      const u64* __restrict__ fac, Opnd pc, int t0, int nt,
+                                                      KsFin fin) {
+    static_assert(!FIN || G == 1, "the fused finish runs one batch element per workgroup");
     // one LDS array (row transposes, then the 8 rows' twiddles -- see row_ntt8_fwd's rt)
     __shared__ double s[8 * 288 + 8 * 256];
     const int nbg = (B + G - 1) / G;
@@ -152,8 +169,9 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
     const int b0 = (rest % nbg) * G, pair = (rest / nbg) * 8 + x8;
     constexpr int RB = R / 8;  // 8-row blocks per limb
     constexpr int LOGN = R == 256 ? 16 : 17;
-    const int t = pair / RB, rb = pair - t * RB;
-    if (t >= ne) return;
+    const int tq = pair / RB, rb = pair - tq * RB;
+    if (tq >= nt) return;
+    const int t = t0 + tq;
     const int pid = t <= l ? t : T.Lp1 + (t - l - 1);
     const int own = t <= l ? t / K : -1;  // the digit whose limbs include t (Q limbs only)
     const int tid = threadIdx.x, L = tid & 31, rl = tid >> 5;
@@ -281,6 +299,31 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
                     a1[g][r] = fred(a1[g][r], q, qi);
                 }
         }
+    }
+    if constexpr (FIN) {
+        // ranges: |acc| < 19q and |conv| <= 17q below 2^42 (file header), so |acc - conv| < 2^48;
+        // big primes fold both to q/2 + 1 first -- fmul_rem's input bound either way
+        const int bb = b0;
+        if (bb >= B) return;
+        const double f = fin.dinvf[t], w = tw_w(f, q);
+        const long coff = ((long)t << LOGN) + (long)row * 256;
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            double cv[8];
+            row_ntt8_fwd(cv, fin.conv + (long)bb * fin.cbs + (long)c * fin.cps + coff, sr, L, 1, tw, q, qi, big);
+            const u64* ap = fin.add.ptr && c < fin.add.np ? fin.add.ptr + (long)bb * fin.add.bs + (long)c * fin.add.ps + roff
+                                                          : nullptr;
+            u64* op = fin.out + (long)bb * fin.obs + (long)c * fin.ops + roff;
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                double a = c ? a1[0][r] : a0[0][r];
+                if (big) a = fred(a, q, qi);
+                double v = fmul_rem(a - cv[r], w, f, q);
+                if (ap) v += u2d(ap[32 * r]);
+                __builtin_nontemporal_store(fcanon(v, q, qi), &op[32 * r]);  // streaming
+            }
+        }
+        return;
     }
 #pragma unroll
     for (int g = 0; g < G; g++) {

@@ -71,3 +71,21 @@ def test_kernel_table_scales_by_dispatches():
     pmc["per_kernel"]["b"]["launches"] = 16
     b = bench.kernel_table(_FakeEngine(raw), pmc, 2)["b"]
     assert b["hbm_bytes_per_launch"] is None and b["pmc_dispatches_mismatch"]["pmc_per_step"] == 16
+
+
+def test_dominant_roofline_picks_the_largest_share():
+    """The line's roofline is the dominant kernel class's (largest share of the profiled kernel
+    time); its achieved rate is algorithmic bytes per call over the call's average duration, and
+    its traffic is the PMC record's per-call bytes only where the record measured that class."""
+    raw = {"a": [20, 2.0, 20 * 1e6, 20], "b": [8, 16.0, 8 * 4e7, 24]}
+    pmc = {"head": "abc", "csrc_sha16": "0" * 16,
+           "per_kernel": {"b": {"launches": 12, "hbm_bytes_per_launch": 1.4e7}}}
+    t = bench.kernel_table(_FakeEngine(raw), pmc, 2)
+    r = bench.dominant_roofline(t, 2, pmc)
+    assert r["kernel"].startswith("b") and r["frac"] == t["b"]["frac"]
+    assert r["achieved"] == pytest.approx(4e7 / 2e-3 / 1e9, rel=1e-3)  # 4e7 B per 2 ms call
+    assert r["traffic"] == pytest.approx(3 * 1.4e7) and r["traffic_head"] == "abc"
+    assert r["launches"] == 8
+    r = bench.dominant_roofline(bench.kernel_table(_FakeEngine(raw), {}, 2), 2, {})
+    assert r["traffic"] is None and r["traffic_head"] is None
+    assert bench.dominant_roofline(None, 2, {})["frac"] is None
