@@ -58,7 +58,7 @@ struct ApiError {
 #define HIPC(x)                                                                              \
     do {                                                                                     \
         hipError_t e_ = (x);                                                                 \
-        if (e_ != hipSuccess) throw_err(AESFHE_EDEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+        if (e_ != hipSuccess) throw_err(AESFHE_EDEVICE, "%s: %s (engine.hip:%d)", #x, hipGetErrorString(e_), __LINE__); \
     } while (0)
 
 #define API_BEGIN try {
@@ -2037,7 +2037,9 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
 // ModDown, first part: INTT of acc's dropped limbs (top r Q limbs + the special limbs, layout
 // [B][2][l+1+K][N]) and their exact base conversion to the lk + 1 = l - r + 1 kept limbs, into conv
 // ([B][2][lk+1][N], coefficient form).  Returns D^{-1} mod q_i (as w / q) for the finish.
-static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int r, u64* conv) {
+// rows_done (fused_ntt engines): the dropped limbs already hold their inverse row pass (raw
+// doubles, k_nttf_rows_ks EPI 2), so only the inverse column pass runs.
+static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int r, u64* conv, bool rows_done = false) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long neN = (long)ne * N;
     if (r < 0 || r > kMdrMaxR || K + r > kMdrMaxE || l - r < 0) throw_err(AESFHE_EARG, "bad combined rescale depth %d", r);
@@ -2046,7 +2048,15 @@ static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int 
     // 4. ModDown: INTT the dropped limbs (top r Q limbs + the special limbs) of both accumulators
     {
         Span ssp = span_s(acc + (long)(lk + 1) * N, neN, K + r, r, lk + 1, e->Lp1);
-        ntt(e, ssp, ssp, B * 2 * (K + r), true);
+        const int total = B * 2 * (K + r);
+        if (rows_done) {
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_inv_cols");
+            if (N == 65536) hipLaunchKernelGGL(k_nttf_inv_cols<256>, dim3(16, total), dim3(256), 0, e->stream, ssp, e->tabs());
+            else hipLaunchKernelGGL(k_nttf_inv_cols<512>, dim3(16, total), dim3(256), 0, e->stream, ssp, e->tabs());
+            HIPC(hipGetLastError());
+        } else {
+            ntt(e, ssp, ssp, total, true);
+        }
     }
     const size_t cell = r ? (size_t)(r - 1) * e->Lp1 + l : 0;
     const double* invf = r ? e->mdr_invf + cell * kMdrMaxE : e->md_phatinvf;
@@ -2141,10 +2151,11 @@ static void ks_finish_fused(aesfhe_engine* e, const u64* d, long dbs, const u64*
         const int blocks = 8 * B * (nt * (R / 8) / 8 + ((nt * (R / 8)) % 8 ? 1 : 0));
         const int nq = std::max(0, std::min(t0 + nt, l + 1) - t0);
         ProfScope ps(e, FAM_KS, bytes(nt, nq, fin), fin ? "ks_rows_fin" : "ks_rows_inner");
-        auto kern = R == 256 ? (pb ? (fin ? k_nttf_rows_ks<1, 256, true, true> : k_nttf_rows_ks<1, 256, true, false>)
-                                   : (fin ? k_nttf_rows_ks<1, 256, false, true> : k_nttf_rows_ks<1, 256, false, false>))
-                             : (pb ? (fin ? k_nttf_rows_ks<1, 512, true, true> : k_nttf_rows_ks<1, 512, true, false>)
-                                   : (fin ? k_nttf_rows_ks<1, 512, false, true> : k_nttf_rows_ks<1, 512, false, false>));
+        // the dropped limbs leave with their inverse row pass done (EPI 2), the kept ones finished (EPI 1)
+        auto kern = R == 256 ? (pb ? (fin ? k_nttf_rows_ks<1, 256, true, 1> : k_nttf_rows_ks<1, 256, true, 2>)
+                                   : (fin ? k_nttf_rows_ks<1, 256, false, 1> : k_nttf_rows_ks<1, 256, false, 2>))
+                             : (pb ? (fin ? k_nttf_rows_ks<1, 512, true, 1> : k_nttf_rows_ks<1, 512, true, 2>)
+                                   : (fin ? k_nttf_rows_ks<1, 512, false, 1> : k_nttf_rows_ks<1, 512, false, 2>));
         hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d,
                            2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, e->A, l, ne, e->tabs(), addend, pm,
                            (int)accum, pb ? *pb : none, fac, pc ? *pc : none, t0, nt, kf);
@@ -2155,7 +2166,7 @@ static void ks_finish_fused(aesfhe_engine* e, const u64* d, long dbs, const u64*
     u64* acc = acc_in ? acc_in : own->p;
     launch(lk + 1, ne - (lk + 1), false, acc, KsFin{});
     Tmp conv(e, (size_t)B * 2 * kN);
-    const double* dinvf = moddown_conv(e, acc, B, l, r, conv.p);
+    const double* dinvf = moddown_conv(e, acc, B, l, r, conv.p, true);
     Tmp conv2(e, (size_t)B * 2 * kN);
     {
         const int total = B * 2 * (lk + 1);

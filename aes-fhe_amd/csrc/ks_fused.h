@@ -122,6 +122,72 @@ __device__ __forceinline__ void row_ntt8_stages(double (&x)[8], double* sr, int 
     wave_lds_sync();  // the next digit rewrites sr
 }
 
+// Inverse (Gentleman-Sande) row pass in the same layouts, mirrored: C (distances 1, 2), B (4, 8,
+// 16), A (32, 64, 128); x in and out in layout A.  W: the row's inverse twiddles staged like the
+// forward ones (entry ml + g = ipsi^brv(ml (R + row) + g), ml = 128 / distance groups per row).
+// Raw doubles out, as k_nttf_inv_rows: inputs folded to |x| <= q/2 + 1, so below 2^42 the sums
+// reach 2^8 (q/2 + 1) < 2^50; larger primes fold every sum (the inverse column pass folds its
+// input first either way).
+__device__ __forceinline__ void row_intt8(double (&x)[8], double* sr, int L, const double* W, double q, double qi,
+                                          bool big) {
+    auto gs = [&](double& a, double& b, double wq) {
+        if (big) gs_f<true>(a, b, wq, q, qi);
+        else gs_f<false>(a, b, wq, q, qi);
+    };
+#pragma unroll
+    for (int r = 0; r < 8; r++) sr[r8p(L + 32 * r)] = x[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 8; r++) x[r] = sr[r8p(8 * L + r)];
+    // C: distance 1 (ml = 128, group 4L + j), distance 2 (ml = 64, group 2L + (r >> 2))
+#pragma unroll
+    for (int j = 0; j < 4; j++) gs(x[2 * j], x[2 * j + 1], W[128 + 4 * L + j]);
+    {
+        const double w0 = W[64 + 2 * L], w1 = W[64 + 2 * L + 1];
+        gs(x[0], x[2], w0);
+        gs(x[1], x[3], w0);
+        gs(x[4], x[6], w1);
+        gs(x[5], x[7], w1);
+    }
+    wave_lds_sync();  // every lane has read its C elements
+#pragma unroll
+    for (int r = 0; r < 8; r++) sr[r8p(8 * L + r)] = x[r];
+    wave_lds_sync();
+    const int eb = 32 * (L >> 2) + (L & 3);
+#pragma unroll
+    for (int r = 0; r < 8; r++) x[r] = sr[r8p(eb + 4 * r)];
+    // B: distances 4, 8, 16 = ml 32, 16, 8 (register distance h = 1, 2, 4; nj = ml / 8 groups)
+#pragma unroll
+    for (int st = 5; st >= 3; st--) {
+        const int ml = 1 << st, h = 4 >> (st - 3), nj = ml >> 3;
+        const int base = ml + (L >> 2) * nj;
+#pragma unroll
+        for (int j = 0; j < nj; j++) {
+            const double wq = W[base + j];
+#pragma unroll
+            for (int k = 0; k < h; k++) gs(x[j * 2 * h + k], x[j * 2 * h + k + h], wq);
+        }
+    }
+    wave_lds_sync();  // every lane has read its B elements
+#pragma unroll
+    for (int r = 0; r < 8; r++) sr[r8p(eb + 4 * r)] = x[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 8; r++) x[r] = sr[r8p(L + 32 * r)];
+    // A: distances 32, 64, 128 = ml 4, 2, 1 (h = 1, 2, 4)
+#pragma unroll
+    for (int st = 2; st >= 0; st--) {
+        const int ml = 1 << st, h = 4 >> st;
+#pragma unroll
+        for (int j = 0; j < ml; j++) {
+            const double wq = W[ml + j];
+#pragma unroll
+            for (int k = 0; k < h; k++) gs(x[j * 2 * h + k], x[j * 2 * h + k + h], wq);
+        }
+    }
+    wave_lds_sync();  // sr is free again
+}
+
 // grid: 8 * ceil(B / G) * (ne * (R / 8) / 8) blocks of 256 (8 rows x 32 lanes; R = N / 256 rows:
 // 256 or 512); block id -> (xcd group
 // x = id & 7, batch group, pair), pair = (t, 8-row block): all batch groups of one (t, row block)
@@ -138,7 +204,10 @@ __device__ __forceinline__ void row_ntt8_stages(double (&x)[8], double* sr, int 
 // the product becomes alpha (a (x) b) + C (c0, c1, 0) + (K, 0, 0) (pc = c, absent: no C term),
 // |x| < 4.5q + K before the P / key product.
 //
-// Target limbs t0 .. t0 + nt - 1 only (the grid covers nt limbs).  FIN (G = 1, no accum): the
+// Target limbs t0 .. t0 + nt - 1 only (the grid covers nt limbs).  EPI selects the epilogue:
+// 0 the canonical accumulators into acc; 2 (INV) their inverse row pass instead, raw doubles into
+// acc (ModDown's INTT then runs only its column pass: the dropped limbs of ks_finish_fused);
+// 1 (FIN, G = 1): the
 // ModDown finish of the key switch in the epilogue, for Q limbs t <= lk (engine.hip
 // ks_finish_fused): the limb's two accumulators never reach HBM.  The conv limbs (column pass
 // done, raw doubles, fin.conv[b][c][t]) get their row pass here -- same prime, same row, so the
@@ -152,7 +221,7 @@ struct KsFin {
     const double* dinvf;  // D^{-1} mod q_t as w / q
     Opnd2 add;            // plain ModDown (r = 0): the addend joins here, not in the accumulators
 };
-template <int G, int R = 256, bool PROD = false, bool FIN = false>
+template <int G, int R = 256, bool PROD = false, int EPI = 0>
 __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64* __restrict__ d, long dbs,
                                                       const u64* __restrict__ ext, long exs, long exj,
                                                       const u64* __restrict__ key, long kdig, long kcomp,
@@ -161,6 +230,7 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
                                                       const double* __restrict__ pmodf, int accum, Opnd pb,
                                                       const u64* __restrict__ fac, Opnd pc, int t0, int nt,
                                                       KsFin fin) {
+    constexpr bool FIN = EPI == 1, INV = EPI == 2;
     static_assert(!FIN || G == 1, "the fused finish runs one batch element per workgroup");
     // one LDS array (row transposes, then the 8 rows' twiddles -- see row_ntt8_fwd's rt)
     __shared__ double s[8 * 288 + 8 * 256];
@@ -321,6 +391,36 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
                 double v = fmul_rem(a - cv[r], w, f, q);
                 if (ap) v += u2d(ap[32 * r]);
                 __builtin_nontemporal_store(fcanon(v, q, qi), &op[32 * r]);  // streaming
+            }
+        }
+        return;
+    }
+    if constexpr (INV) {
+        // the row's inverse twiddles replace its forward ones in LDS (the row's own 32 lanes;
+        // row_ntt8_stages ended with a wave barrier, so every forward read is done)
+        const double* IW = T.ipsif + ((long)pid << LOGN);
+#pragma unroll
+        for (int m = 0; m < 8; m++) {
+            const int e = L + 32 * m;
+            if (e > 0) {
+                const int ml = 1 << (31 - __clz(e));
+                tw[e] = IW[(long)ml * (R + row) + (e - ml)];
+            }
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int bb = b0 + g;
+            if (bb >= B) break;
+            u64* o0 = acc + (long)bb * abs_ + roff;
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                double x[8];
+#pragma unroll
+                for (int r = 0; r < 8; r++) x[r] = fred(c ? a1[g][r] : a0[g][r], q, qi);
+                row_intt8(x, sr, L, tw, q, qi, big);
+#pragma unroll
+                for (int r = 0; r < 8; r++) st_d(&o0[(long)c * acs + 32 * r], x[r]);
             }
         }
         return;

@@ -25,7 +25,7 @@ CLASSES = [
     (r"k_nttf_inv_rows<\d+, false", "ntt_inv_rows"),
     (r"k_nttf_inv_cols<", "ntt_inv_cols"),
     (r"k_ntt_(fwd|inv)_(rows|cols)<", "ntt_generic"),
-    (r"k_nttf_rows_ks<\d+, \d+, (true|false), true>", "ks_rows_fin"),
+    (r"k_nttf_rows_ks<\d+, \d+, (true|false), 1>", "ks_rows_fin"),
     (r"k_nttf_rows_ks<", "ks_rows_inner"),
     (r"k_ks_inner_all<", "ks_inner"),
     (r"k_ks_inner_multi<", "ks_inner_multi"),
