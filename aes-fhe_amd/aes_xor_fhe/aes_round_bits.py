@@ -217,9 +217,10 @@ class AESRowRound:
         """SubBytes -> ShiftRows -> AddRoundKey (AES round 10: no MixColumns), depth 5."""
         return self.add_round_key(self.shift_rows(self.sub_bytes(bits)), key)
 
-    def refresh(self, bits, bs, pairs_per_call: int = 8):
+    def refresh(self, bits, bs, pairs_per_call: int = 8, in_scale: float = 1.0):
         """Bootstrap all 32 bit ciphertexts, two per refresh (bit j with bit j + 4 of a row),
-        `pairs_per_call` pairs concatenated along the batch per Bootstrapper call."""
+        `pairs_per_call` pairs concatenated along the batch per Bootstrapper call.  in_scale: the
+        bits hold in_scale * (+-1) (clean_bits' output: 2)."""
         e = self.e
         pairs = [(r, j) for r in range(4) for j in range(4)]
         out = [[None] * 8 for _ in range(4)]
@@ -228,7 +229,7 @@ class AESRowRound:
             nb = bits[0][0].batch
             a = e.concat([bits[r][j] for r, j in grp])
             b = e.concat([bits[r][j + 4] for r, j in grp])
-            ya, yb = bs.bootstrap_bits(a, b)
+            ya, yb = bs.bootstrap_bits(a, b, in_scale=in_scale)
             for k, (r, j) in enumerate(grp):
                 out[r][j] = e.slice(ya, k * nb, nb)
                 out[r][j + 4] = e.slice(yb, k * nb, nb)
@@ -244,6 +245,16 @@ class AESRowRound:
     # as a third one: its output is only decrypted (decision margin 1; measured <= 0.13).
     MAX_ROUNDS_FRESH = 3
     MAX_ROUNDS_AFTER_REFRESH = 2
+    # The last refresh is followed by two middle rounds and the final one, and its output error is
+    # its input error squared (~pi^2 e^2 / 8): after two middle rounds from the previous refresh
+    # the input is ~2.5e-2, the output ~8e-4, and the three rounds after it took the decoded
+    # slots to max | |v| - 1 | = 0.7-0.8 at N = 2^16 (round 4: tools/aes10_trace.py) with rare
+    # slots past the decision margin 1 -- a wrong block in ~1 of 7 runs of 131 072 blocks.  So
+    # the bits are cleaned first, x -> (3x - x^3) / 2 (error e -> ~1.5 e^2, two levels: x^2, then
+    # one fused product 3x - x^3 whose factor 2 the refresh's SlotToCoeff absorbs), where the
+    # level budget allows it: pick_bootstrapper prefers a previous refresh that leaves the two
+    # levels (the 3-map CoeffToSlot one before rounds 6-7 at L = 30).
+    CLEAN_LEVELS = 2
 
     def needs_refresh(self, level: int, final: bool, since: int, refreshed: bool, stc: int) -> bool:
         """Refresh before the next round?  When its depth does not fit, when a middle round would
@@ -252,21 +263,30 @@ class AESRowRound:
         limit = self.MAX_ROUNDS_AFTER_REFRESH if refreshed else self.MAX_ROUNDS_FRESH
         return level < need or (not final and (level - need < stc or since >= limit))
 
-    def refreshes_after(self, rnd: int, level: int, top: int, stc: int) -> float:
+    def can_clean(self, level: int, since: int, refreshed: bool, stc: int) -> bool:
+        """Clean before this refresh?  After MAX_ROUNDS_AFTER_REFRESH middle rounds from a refresh,
+        when CLEAN_LEVELS fit above SlotToCoeff's levels (the caller applies it to the last
+        refresh only)."""
+        return refreshed and since >= self.MAX_ROUNDS_AFTER_REFRESH and level - self.CLEAN_LEVELS >= stc
+
+    def refreshes_after(self, rnd: int, level: int, top: int, stc: int, with_clean: bool = False):
         """Refreshes that rounds rnd..10 need when they start right after a refresh at `level`,
-        later refreshes returning `top` (inf if a round would run out of levels)."""
+        later refreshes returning `top` (inf if a round would run out of levels).  with_clean:
+        (that count, 1 if the last of those refreshes cannot be preceded by clean_bits else 0)."""
         n, since, lvl = 0, 0, level
+        last_clean = True
         for r in range(rnd, 11):
             final = r == 10
             if self.needs_refresh(lvl, final, since, True, stc):
                 if since == 0:
-                    return float("inf")
+                    return (float("inf"), 1) if with_clean else float("inf")
+                last_clean = self.can_clean(lvl, since, True, stc)
                 n, since, lvl = n + 1, 0, top
             lvl -= self.FINAL_DEPTH if final else self.ROUND_DEPTH
             since += 1
             if lvl < 0:
-                return float("inf")
-        return n
+                return (float("inf"), 1) if with_clean else float("inf")
+        return (n, 0 if last_clean else 1) if with_clean else n
 
     def pick_bootstrapper(self, bss, rnd: int):
         """The first of `bss` (cheapest first) whose output level keeps the fewest refreshes for
@@ -276,8 +296,33 @@ class AESRowRound:
             return bss[0]
         stc = len(bss[0].stc_bits)
         top = max(b.bits_level for b in bss)
-        counts = [self.refreshes_after(rnd, b.bits_level, top, stc) for b in bss]
+        # fewest refreshes first, then one that leaves room to clean before the last refresh
+        counts = [self.refreshes_after(rnd, b.bits_level, top, stc, with_clean=True) for b in bss]
         return bss[counts.index(min(counts))]
+
+    def refresh_step(self, S, rnd: int, level: int, since: int, refreshed: bool, bss, pairs_per_call: int):
+        """The refresh before round rnd (state S at `level`, `since` rounds after the previous
+        refresh): pick the bootstrapper, clean the bits first when this is the last refresh and
+        can_clean allows it, bootstrap.  Returns (state, bootstrapper, cleaned)."""
+        stc = len(bss[0].stc_bits)
+        b = self.pick_bootstrapper(bss, rnd)
+        top = max(x.bits_level for x in bss)
+        clean = self.can_clean(level, since, refreshed, stc) and self.refreshes_after(rnd, b.bits_level, top, stc) == 0
+        if clean:
+            S = self.clean_bits(S)
+        return self.refresh(S, b, pairs_per_call, in_scale=2.0 if clean else 1.0), b, clean
+
+    def clean_bits(self, bits):
+        """3x - x^3 for every bit ciphertext (= 2 * (3x - x^3) / 2, the cleaning map with error
+        e -> ~1.5 e^2 near +-1, scaled by 2): x^2, then one fused product -x * x^2 + 3x
+        (Engine.multiply_fma), two levels.  The caller's refresh takes in_scale=2."""
+        e = self.e
+        out = []
+        for row in bits:
+            sq = [e.multiply(x, x, self.rlk) for x in row]
+            out.append([e.multiply_fma(e.level_down(x, y.level) if x.level > y.level else x, y, self.rlk,
+                                       alpha=-1, c=x, gamma=3.0) for x, y in zip(row, sq)])
+        return out
 
     KEY_OFFSET = 4  # a round's key product takes the SubBytes output: input level - 4
 
@@ -342,13 +387,13 @@ class AESRowRound:
             final = rnd == 10
             lvl = min(c.level for row in S for c in row)
             if self.needs_refresh(lvl, final, since, refreshes > 0, stc):
-                since = 0
                 t0 = time.perf_counter()
-                b = self.pick_bootstrapper(bss, rnd)
-                S = self.refresh(S, b, pairs_per_call)
+                S, b, clean = self.refresh_step(S, rnd, lvl, since, refreshes > 0, bss, pairs_per_call)
+                since = 0
                 refreshes += 1
                 if progress:
-                    progress(f"refresh {refreshes} before round {rnd} (CtS in {b.cts_groups} maps, output level {b.bits_level})")
+                    progress(f"refresh {refreshes} before round {rnd} (CtS in {b.cts_groups} maps, output level "
+                             f"{b.bits_level}{', bits cleaned first' if clean else ''})")
                 if timings is not None:
                     self.e.materialize(S)
                     self.e.synchronize()

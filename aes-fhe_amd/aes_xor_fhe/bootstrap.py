@@ -171,6 +171,8 @@ class Bootstrapper:
         self.cts = [self._prepare(M) for M in cts]
         self.stc = [self._prepare(M, self.stc_baby_scale) for M in stc]
         self.stc_bits = [self._prepare(M, self.stc_baby_scale) for M in stc_bits]
+        self._stc_bits_maps = stc_bits  # for the scaled-input variants (bootstrap_bits in_scale)
+        self._stc_bits_scaled: Dict[float, list] = {1.0: self.stc_bits}
         self.cts_bits = [self._prepare(M) for M in cts_bits] if bits_opt else self.cts
         # rotation keys: hoisted keys for the baby steps (one ModUp per group input), ordinary
         # keys for the giant steps
@@ -489,8 +491,19 @@ class Bootstrapper:
             y = self.linear(y, plan)
         return y
 
-    def bootstrap_bits(self, a: Ciphertext, b: Ciphertext | None = None):
+    def _stc_bits_for(self, in_scale: float):
+        """SlotToCoeff plans for inputs holding in_scale * (+-1): the last map's constant divided
+        by in_scale (plaintext constants only: no level), prepared on first use."""
+        key = float(in_scale)
+        if key not in self._stc_bits_scaled:
+            last = {d: v / key for d, v in self._stc_bits_maps[-1].items()}
+            self._stc_bits_scaled[key] = self.stc_bits[:-1] + [self._prepare(last, self.stc_baby_scale)]
+        return self._stc_bits_scaled[key]
+
+    def bootstrap_bits(self, a: Ciphertext, b: Ciphertext | None = None, in_scale: float = 1.0):
         """Refresh one or two ciphertexts whose real slots hold bits +-1 (SlotToCoeff first).
+        in_scale: the inputs hold in_scale * (+-1) instead (AESRowRound.clean_bits' 3x - x^3 =
+        2 x (3 - x^2) / 2): SlotToCoeff's last constant absorbs the factor.
 
         StC at the bottom levels puts the bits into the coefficients as +-q0/4 (a in the first
         half, b in the second); after ModRaise t/q0 = I +- 1/4 + eps, so EvalMod's
@@ -506,7 +519,7 @@ class Bootstrapper:
             raise ValueError(f"bootstrap_bits needs level >= {lv}, got {x.level}")
         if x.level > lv:
             x = e.level_down(x, lv)
-        for plan in self.stc_bits:
+        for plan in self._stc_bits_for(in_scale):
             x = self.linear(x, plan)
         x_re, x_im = self._raise_to_slots(x, bits=True)
         if b is None:

@@ -289,7 +289,16 @@ static T* upload_small(aesfhe_engine* e, const T* src, size_t count) {
     return dst;
 }
 
-static u64* dalloc(aesfhe_engine* e, size_t words) { return (u64*)e->pool.get(words * 8); }
+// AESFHE_POOL_POISON=1 (diagnostic): every pool block handed out is first filled with 0xA5 bytes on
+// the engine stream, so a read of words nobody wrote is deterministic (and loud) instead of
+// whatever the block held before
+static void* pool_get(aesfhe_engine* e, size_t bytes) {
+    static const bool poison = getenv("AESFHE_POOL_POISON") && atoi(getenv("AESFHE_POOL_POISON"));
+    void* p = e->pool.get(bytes);
+    if (poison && p) HIPC(hipMemsetAsync(p, 0xA5, bytes, e->stream));
+    return p;
+}
+static u64* dalloc(aesfhe_engine* e, size_t words) { return (u64*)pool_get(e, words * 8); }
 static void dfree(aesfhe_engine* e, u64* p, size_t words) { e->pool.put(p, words * 8); }
 
 struct Tmp {  // RAII temporary device buffer from the pool
@@ -309,7 +318,7 @@ static aesfhe_ct* ct_new(aesfhe_engine* e, int B, int np, int level) {
     c->level = level;
     c->is_zero = 0;
     c->bytes = (size_t)B * np * (level + 1) * e->N * 8;
-    c->d = (u64*)e->pool.get(c->bytes);
+    c->d = (u64*)pool_get(e, c->bytes);
     return c;
 }
 
@@ -962,7 +971,7 @@ static aesfhe_key* key_new(aesfhe_engine* e, int kind, size_t words) {
     k->galois = 0;
     k->keyseed = 0;
     k->bytes = words * 8;
-    k->d = (u64*)e->pool.get(k->bytes);
+    k->d = (u64*)pool_get(e, k->bytes);
     return k;
 }
 
@@ -1270,7 +1279,7 @@ extern "C" int aesfhe_pt_create(aesfhe_engine* e, const int64_t* co, int32_t lev
     e->refs++;
     p->level = level;
     p->bytes = (size_t)nl * N * 8;
-    p->d = (u64*)e->pool.get(p->bytes);
+    p->d = (u64*)pool_get(e, p->bytes);
     Tmp dco(e, N);
     HIPC(hipMemcpyAsync(dco.p, co, (size_t)N * 8, hipMemcpyHostToDevice, e->stream));
     hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, nl, 1), dim3(256), 0, e->stream, (const i64*)dco.p, p->d, nl, e->q, e->logN);
@@ -1291,7 +1300,7 @@ extern "C" int aesfhe_pt_create_ext(aesfhe_engine* e, const int64_t* co, int32_t
     p->level = level;
     p->ext = 1;
     p->bytes = (size_t)ne * N * 8;
-    p->d = (u64*)e->pool.get(p->bytes);
+    p->d = (u64*)pool_get(e, p->bytes);
     Tmp dco(e, N);
     HIPC(hipMemcpyAsync(dco.p, co, (size_t)N * 8, hipMemcpyHostToDevice, e->stream));
     hipLaunchKernelGGL(k_coeffs_res, dim3(N / 256, nl, 1), dim3(256), 0, e->stream, (const i64*)dco.p, p->d, nl, e->q, e->logN);

@@ -429,10 +429,16 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     el = allmax(time.perf_counter() - t0)
     timed_mallocs = eng.pool_stats()["mallocs"] - m0
     ok = None
+    wrong = None
     if args.check:
         got = R.decrypt_blocks(out, nb)
         want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
         ok = bool(np.array_equal(got, want))
+        if not ok:  # where: a few flipped bits (noise) look different from a systematic error
+            bad = np.any(got != want, axis=-1)
+            wrong = {"blocks": int(bad.sum()), "bits": int(np.unpackbits(got ^ want).sum()),
+                     "sets": sorted({int(s) for s in np.nonzero(bad)[0]})[:16],
+                     "byte_positions": sorted({int(b) for b in np.nonzero(got != want)[-1]})}
     world = int(os.environ.get("WORLD_SIZE", "1"))
     return {"metric": "AES-128 blocks/sec (10 rounds incl. bootstrapping)",
             "value": round(nb * R.n_blk * world / el, 2), "unit": "blocks/s",
@@ -440,7 +446,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
             "blocks_per_gpu": nb * R.n_blk, "refreshes": nref,
             "bootstrap_share": round(tm.get("bootstrap", 0.0) / max(el, 1e-9), 3),
             "bootstrap_ms_per_bit_ct": round(1e3 * tm.get("bootstrap", 0.0) / max(nref * 32 * nb, 1), 2),
-            "bootstrap_setup_s": round(setup_s, 2), "verified": ok,
+            "bootstrap_setup_s": round(setup_s, 2), "verified": ok, "mismatch": wrong,
             "bootstrap_cts_groups": [b.cts_groups for b in bs], "round_key_levels": klv,
             "state_level": L0,
             "block_rounds_per_s": round(10 * nb * R.n_blk * world / el, 2),

@@ -164,25 +164,29 @@ def test_refresh_schedule():
 
 def test_pick_bootstrapper():
     """Per-refresh choice among bootstrappers (AESRowRound.pick_bootstrapper): at L = 30 the
-    5-map CtS (output 17) serves the refreshes before rounds 4 and 6 (two middle rounds + StC =
-    17 levels) and the 3-map one (output 19) the refresh before rounds 8-10 (7 + 7 + 5); at L = 35
-    the cheaper one serves all three."""
+    5-map CtS (output 17) serves the refresh before round 4 (two middle rounds + StC = 17 levels),
+    the 3-map one (output 19) the refresh before round 6 -- two levels more, so the bits can be
+    cleaned (CLEAN_LEVELS) before the last refresh -- and the one before rounds 8-10 (7 + 7 + 5);
+    at L = 35 the cheaper one serves all three and leaves room to clean as well."""
     from types import SimpleNamespace as NS
     from aes_xor_fhe.aes_round_bits import AESRowRound
     R = AESRowRound.__new__(AESRowRound)
-    for L, want in ((30, [17, 17, 19]), (35, [22, 22, 22])):
+    for L, want in ((30, [17, 19, 19]), (35, [22, 22, 22])):
         bss = [NS(bits_level=L - 13, stc_bits=[0] * 3), NS(bits_level=L - 11, stc_bits=[0] * 3)]
-        lvl, since, got = L - 1, 0, []
+        lvl, since, got, cleans = L - 1, 0, [], []
         for rnd in range(1, 11):
             final = rnd == 10
             if R.needs_refresh(lvl, final, since, bool(got), 3):
                 b = R.pick_bootstrapper(bss, rnd)
+                last = R.refreshes_after(rnd, b.bits_level, L - 11, 3) == 0
+                cleans.append(last and R.can_clean(lvl, since, bool(got), 3))
                 got.append(b.bits_level)
                 lvl, since = b.bits_level, 0
             lvl -= R.FINAL_DEPTH if final else R.ROUND_DEPTH
             assert lvl >= 0
             since += 1
         assert got == want, (L, got)
+        assert cleans == [False, False, True], (L, cleans)  # the last refresh's input is cleaned
     # a single bootstrapper is always taken
     assert R.pick_bootstrapper(bss[1:], 8) is bss[1]
 
