@@ -242,7 +242,8 @@ class AESRowRound:
     # reach 1.8e-3, but a refresh leaves ~1.5e-4, after which two rounds reach 5-7e-3 and a third
     # ~0.1 -- too much for the next refresh (a fourth from a fresh encryption, which L = 35 allows
     # by levels, reached 0.12 at N = 2^17 and the run diverged).  The final round may still follow
-    # as a third one: its output is only decrypted (decision margin 1; measured <= 0.13).
+    # as a third one: its output is only decrypted (decision margin 1) -- with the last refresh's
+    # input cleaned (CLEAN_LEVELS below; without it the margin was not enough, measured 0.7-0.8).
     MAX_ROUNDS_FRESH = 3
     MAX_ROUNDS_AFTER_REFRESH = 2
     # The last refresh is followed by two middle rounds and the final one, and its output error is
