@@ -88,3 +88,23 @@ def test_aes128_ten_rounds_sliced_full_params(product_lib, gpu_available):
     assert nref == 3 and out[0][0].level == 0
     assert np.array_equal(got, want)
     assert bytes(got[0, 0]) == FIPS_C1_CT
+
+
+def test_clean_bits_oracle(oracle_lib):
+    """AESRowRound.clean_bits: 3x - x^3 (twice the cleaning map (3x - x^3) / 2) in two levels --
+    bits +-1 with a relative error e come back as +-2 with error ~3 e^2 (the refresh after it takes
+    in_scale = 2: Bootstrapper.bootstrap_bits)."""
+    from aes_xor_fhe.aes_round_bits import AESRowRound
+    from aes_xor_fhe.fhe import Engine
+    e = Engine(_lib=oracle_lib, log_n=10, max_level=6, special_primes=2, seed=3)
+    sk = e.create_secret_key()
+    R = AESRowRound(e, sk, e.create_public_key(sk), e.create_relinearization_key(sk))
+    rng = np.random.default_rng(5)
+    sgn = rng.choice([-1.0, 1.0], size=(1, e.slot_count))
+    x = sgn * (1.0 + rng.uniform(-0.05, 0.05, sgn.shape))
+    cts = [[e.encrypt(x, sk)]]
+    out = R.clean_bits(cts)
+    assert out[0][0].level == cts[0][0].level - R.CLEAN_LEVELS
+    got = np.real(np.atleast_2d(e.decrypt(out[0][0], sk)))
+    np.testing.assert_allclose(got, 3 * x - x ** 3, atol=1e-4)
+    assert np.abs(np.abs(got) - 2.0).max() < 3 * 0.05 ** 2 + 1e-3
