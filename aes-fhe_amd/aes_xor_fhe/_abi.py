@@ -164,15 +164,29 @@ class Lib:
     def __init__(self, path: str | os.PathLike):
         self.path = str(path)
         self.cdll = C.CDLL(self.path, mode=C.RTLD_LOCAL)
+        # the header revision first: a library built against an older header may lack newer
+        # symbols (aesfhe_abi_version itself included), which must read as "rebuild it", not as
+        # a ctypes "undefined symbol" from the binding loop
+        stale = "?"
+        try:
+            ver = self.cdll.aesfhe_abi_version
+            ver.restype, ver.argtypes = C.c_int, []
+            stale = ver()
+        except AttributeError:
+            pass
+        if stale != ABI_VERSION:
+            raise RuntimeError(f"{self.path}: C ABI revision {stale}, this package needs "
+                               f"{ABI_VERSION} (include/aesfhe.h AESFHE_ABI_VERSION): rebuild it")
         for name, res, args in SIGNATURES:
-            fn = getattr(self.cdll, name)
+            try:
+                fn = getattr(self.cdll, name)
+            except AttributeError:
+                raise RuntimeError(f"{self.path}: C ABI revision {ABI_VERSION} but symbol {name} is missing: "
+                                   f"rebuild it") from None
             fn.restype = res
             fn.argtypes = args
             setattr(self, name[len("aesfhe_"):], fn)
         self.backend = self.backend_name().decode()
-        if self.abi_version() != ABI_VERSION:  # a library built against another header revision
-            raise RuntimeError(f"{self.path}: C ABI revision {self.abi_version()}, this package needs "
-                               f"{ABI_VERSION} (include/aesfhe.h AESFHE_ABI_VERSION): rebuild it")
 
     def check(self, rc: int) -> None:
         if rc != 0:

@@ -372,8 +372,10 @@ class Engine:
     be checked at the call is checked there (operand levels, batch shapes, polynomial counts, the
     key's type and owning engine); an error of the evaluation itself (out of device memory, a
     device fault) surfaces at the first use of the deferred handle, as a RuntimeError naming the
-    C call.  At most ``max_pending`` products (default 256) wait unevaluated per engine: the
-    next one evaluates the waiting ones first, which bounds the operands they keep alive.
+    C call.  At most ``max_pending`` products (default 256) that no fused evaluation has taken
+    wait unevaluated per engine: the next one evaluates the waiting ones first.  A product a
+    fused sum has used no longer counts (it stays deferred; only a direct use of its handle
+    evaluates it), so the cap never re-evaluates products whose value a poly2 result holds.
 
     Randomness: without ``seed`` the engine seed, every secret key created without a seed and
     the first encryption nonce are drawn from os.urandom.  With an explicit ``seed`` everything
@@ -763,6 +765,11 @@ class Engine:
             ys.setdefault(id(p._b), p._b)
         if len(xs) > 15 or len(ys) > 15:
             return self.lincomb([p for p, _ in terms], [k for _, k in terms])
+        # the fused evaluation has used these products: they no longer count against max_pending
+        # (which bounds the products no evaluation has taken yet).  Each stays deferred: a later
+        # direct use of its handle still evaluates it.
+        for p, _ in terms:
+            self._pending.discard(p)
         xi = {k: i + 1 for i, k in enumerate(xs)}
         yi = {k: j + 1 for j, k in enumerate(ys)}
         C = np.zeros((1, len(xs) + 1, len(ys) + 1), dtype=np.complex128)

@@ -24,6 +24,7 @@
 #include "kernels_ops.h"
 #include "ntt256f.h"
 #include "ks_fused.h"
+#include "bconv_mfma.h"
 #include "arena.h"
 #include "codec_dev.h"
 
@@ -150,6 +151,10 @@ struct aesfhe_engine {
     u64* mdr_dinv = nullptr;
     double *mu_hatinvf, *md_phatinvf, *md_pinvf, *rs_invf;
     TwD *mu_hatf, *md_phatf;  // base-conversion constants {w, w/q}
+    // matrix-core base conversions (bconv_mfma.h): [set / cell][pid][8 planes][kBconvKT] signed
+    // bytes, the XOR-0x80 corrections [set / cell][pid] and (2^32 mod p) / p per prime
+    int8_t *bc_mu_tab = nullptr, *bc_md_tab = nullptr, *bc_mdr_tab = nullptr;
+    double *bc_mu_corr = nullptr, *bc_md_corr = nullptr, *bc_mdr_corr = nullptr, *bc_w32f = nullptr;
     // small-argument upload ring (device) + pinned staging
     char* ring_d = nullptr;
     char* ring_h = nullptr;
@@ -521,6 +526,42 @@ static Span span_s(u64* base, long pstride, int nl, int nq, int qpid0, int spid0
 
 // -----------------------------------------------------------------------------------------------
 // engine creation: tables
+
+// bytes of a canonical residue of prime q (0 <= y < q)
+static int res_bytes(u64 q) {
+    int b = 0;
+    for (u64 x = q - 1; x; x >>= 8) b++;
+    return b;
+}
+// The constant rows of one target prime p for a matrix-core base conversion (bconv_mfma.h):
+// tab = 8 planes x kBconvKT bytes; source slot sl's byte a (K byte 8 sl + a) holds the signed
+// balanced base-256 digits of H' = 256^a H[sl] mod p over the planes b = 0..6 (plane 7 zero), for
+// the bytes a < res_bytes(q_sl) a canonical y can have; with vc, K byte 8 ns holds those of G
+// (ModDown's -D mod p, times the in-kernel v).  Returns 128 * (sum of every H' placed) mod p:
+// the kernel feeds the bytes as u - 128 (XOR 0x80, signed MFMA operands).
+static u64 bconv_row(int8_t* tab, u64 p, int ns, const u64* srcq, const u64* H, bool vc, u64 G) {
+    u64 corr = 0;
+    auto place = [&](int k, u64 hp) {
+        int64_t x = (int64_t)hp;  // < 2^50: seven balanced digits reach 2^55
+        for (int b = 0; b < 7; b++) {
+            const int d = (int)((x + 128) & 255) - 128;
+            tab[b * kBconvKT + k] = (int8_t)d;
+            x = (x - d) / 256;
+        }
+        if (x != 0) throw_err(AESFHE_EUNSUPPORTED, "base-conversion constant beyond 7 bytes");
+        corr = (corr + h_mulmod(128 % p, hp, p)) % p;
+    };
+    for (int sl = 0; sl < ns; sl++) {
+        u64 r = 1 % p;  // 256^a mod p
+        for (int a = 0; a < res_bytes(srcq[sl]); a++) {
+            place(8 * sl + a, h_mulmod(r, H[sl] % p, p));
+            r = h_mulmod(r, 256 % p, p);
+        }
+    }
+    if (vc) place(8 * ns, G % p);
+    return corr;
+}
+
 static void build_tables(aesfhe_engine* e) {
     const int N = e->N, np = e->np, L = e->L, K = e->K, Lp1 = e->Lp1;
     const auto& Q = e->chain.q;
@@ -617,6 +658,29 @@ static void build_tables(aesfhe_engine* e) {
     up(hhatinvf, &e->mu_hatinvf);
     up(hhat, &e->mu_hat);
     up(hhatf, &e->mu_hatf);
+    {  // matrix-core ModUp rows: [set][pid] (the digit's own pids are never targets)
+        const size_t row = 8 * (size_t)kBconvKT;
+        std::vector<int8_t> tab(mu_sets * np * row, 0);
+        std::vector<double> corr(mu_sets * np, 0.0), w32f(np);
+        for (int j = 0; j < e->dnum; j++)
+            for (int a = 1; a <= A; a++) {
+                const int lo = j * A;
+                if (lo + a > Lp1 || a > 16) continue;
+                const size_t set = (size_t)j * A + (a - 1);
+                for (int pid = 0; pid < np; pid++) {
+                    std::vector<u64> H(a);
+                    for (int i = 0; i < a; i++) H[i] = hhat[(set * A + i) * np + pid];
+                    corr[set * np + pid] = (double)bconv_row(&tab[(set * np + pid) * row], Q[pid], a, &Q[lo], H.data(), false, 0);
+                }
+            }
+        for (int pid = 0; pid < np; pid++) {
+            const u64 p = Q[pid], w = h_mulmod((1ULL << 32) % p, 1, p);
+            w32f[pid] = (double)w / (double)p;
+        }
+        up(tab, &e->bc_mu_tab);
+        up(corr, &e->bc_mu_corr);
+        up(w32f, &e->bc_w32f);
+    }
 
     // ModDown tables
     std::vector<u64> hphatinv(K), hphat((size_t)K * Lp1), hpinv(Lp1), hpmod(np, 0);
@@ -643,6 +707,24 @@ static void build_tables(aesfhe_engine* e) {
         hpinv[i] = h_invmod(P, qi);
         hpinvf[i] = (double)hpinv[i] / (double)qi;
     }
+    {  // matrix-core ModDown rows, r = 0: sources p_0..p_{K-1}, targets q_i, v slot G = -P mod q_i
+        const size_t row = 8 * (size_t)kBconvKT;
+        std::vector<int8_t> tab((size_t)Lp1 * row, 0);
+        std::vector<double> corr(Lp1, 0.0);
+        if (K + 1 <= 16)
+            for (int i = 0; i < Lp1; i++) {
+                const u64 qi = Q[i];
+                std::vector<u64> H(K);
+                u64 P = 1;
+                for (int k = 0; k < K; k++) {
+                    H[k] = hphat[(size_t)k * Lp1 + i];
+                    P = h_mulmod(P, Q[Lp1 + k] % qi, qi);
+                }
+                corr[i] = (double)bconv_row(&tab[(size_t)i * row], qi, K, &Q[Lp1], H.data(), true, (qi - P) % qi);
+            }
+        up(tab, &e->bc_md_tab);
+        up(corr, &e->bc_md_corr);
+    }
     up(hphatinv, &e->md_phatinv);
     up(hphatinvf, &e->md_phatinvf);
     up(hphat, &e->md_phat);
@@ -668,12 +750,18 @@ static void build_tables(aesfhe_engine* e) {
         std::vector<TwD> hhatf(cells * kMdrMaxE * Lp1, TwD{0, 0});
         std::vector<u64> hdinv(cells * Lp1, 0);
         std::vector<double> heinv(cells * kMdrMaxE, 0.0), hdmodf(cells * Lp1, 0.0);
+        // matrix-core rows [cell][target i][8][kBconvKT] (bconv_mfma.h), v slot G = -D mod q_i
+        const size_t brow = 8 * (size_t)kBconvKT;
+        std::vector<int8_t> btab(cells * Lp1 * brow, 0);
+        std::vector<double> bcorr(cells * Lp1, 0.0);
         for (int r = 1; r <= kMdrMaxR && K + r <= kMdrMaxE; r++)
             for (int l = r; l <= L; l++) {
                 const size_t cell = (size_t)(r - 1) * Lp1 + l;
                 std::vector<int> E;
                 for (int j = 0; j < r; j++) E.push_back(l - r + 1 + j);
                 for (int j = 0; j < K; j++) E.push_back(Lp1 + j);
+                std::vector<u64> Hc((size_t)(l - r + 1) * E.size()), Eq(E.size());
+                for (size_t j = 0; j < E.size(); j++) Eq[j] = Q[E[j]];
                 for (size_t j = 0; j < E.size(); j++) {
                     const u64 ej = Q[E[j]];
                     u64 prod = 1;
@@ -687,6 +775,7 @@ static void build_tables(aesfhe_engine* e) {
                         for (size_t j2 = 0; j2 < E.size(); j2++)
                             if (j2 != j) h = h_mulmod(h, Q[E[j2]] % qi, qi);
                         hhatf[(cell * Lp1 + i) * kMdrMaxE + j] = TwD{(double)h, (double)h / (double)qi};  // [cell][target i][source j]
+                        Hc[(size_t)i * E.size() + j] = h;
                     }
                 }
                 for (int i = 0; i <= l - r; i++) {
@@ -697,8 +786,13 @@ static void build_tables(aesfhe_engine* e) {
                     hdinv[cell * Lp1 + i] = di;
                     hdmodf[cell * Lp1 + i] = (double)D / (double)qi;
                     hdinvf[cell * Lp1 + i] = (double)di / (double)qi;
+                    if ((int)E.size() + 1 <= 16)
+                        bcorr[cell * Lp1 + i] = (double)bconv_row(&btab[(cell * Lp1 + i) * brow], qi, (int)E.size(), Eq.data(),
+                                                                  &Hc[(size_t)i * E.size()], true, (qi - D) % qi);
                 }
             }
+        up(btab, &e->bc_mdr_tab);
+        up(bcorr, &e->bc_mdr_corr);
         up(hinvf, &e->mdr_invf);
         up(hhatf, &e->mdr_hatf);
         up(hdinv, &e->mdr_dinv);
@@ -798,7 +892,9 @@ static void engine_teardown(aesfhe_engine* e) {
                     e->mu_hatinv, e->mu_hat, e->md_phatinv, e->md_phat, e->md_pinv, e->rs_inv,
                     e->rs_mod, e->pmod, e->mu_hatinvf, e->mu_hatf, e->md_phatinvf, e->md_phatf,
                     e->md_pinvf, e->rs_invf, e->ring_d, e->tw, e->itw, e->mdr_invf, e->mdr_hatf,
-                    e->mdr_dinv, e->mdr_dinvf, e->pmodf, e->mdr_einv, e->mdr_dmodf, e->md_einv};
+                    e->mdr_dinv, e->mdr_dinvf, e->pmodf, e->mdr_einv, e->mdr_dmodf, e->md_einv,
+                    e->bc_mu_tab, e->bc_md_tab, e->bc_mdr_tab, e->bc_mu_corr, e->bc_md_corr, e->bc_mdr_corr,
+                    e->bc_w32f};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto& kv : e->poly2_tabs) hipFree(kv.second);
@@ -1925,6 +2021,37 @@ static unsigned bconv_groups(int N, int P, int ntarget) {
     return (unsigned)std::max(1L, std::min(g, (long)ntarget));
 }
 
+// Base conversions on the matrix cores (bconv_mfma.h), the default; AESFHE_BCONV_VALU=1 selects the
+// exact-fp64 VALU kernels (k_modup / k_moddown) for A/B runs.  Same residues either way.
+static bool bconv_mfma_on() {
+    static const bool on = !(getenv("AESFHE_BCONV_VALU") && atoi(getenv("AESFHE_BCONV_VALU")));
+    return on;
+}
+// nslots = source slots (+ 1 for ModDown's v): ceil(nslots / 4) K-steps of 32 bytes (<= 4)
+static void launch_bconv(aesfhe_engine* e, BconvArgs a, int nz, int nslots, bool vc) {
+    const int N = e->N, nstep = (nslots + 3) / 4, ntile = (a.nt + 3) / 4;
+    if (nstep < 1 || nstep > 4 || ntile < 1) throw_err(AESFHE_EUNSUPPORTED, "matrix-core base conversion of %d slots", nslots);
+    // target groups: >= ~1024 workgroups of 256 threads when the batch alone does not fill the chip
+    const long wg = (long)(N / 256) * nz;
+    const long groups0 = std::max(1L, std::min((long)ntile, (1024 + wg - 1) / wg));
+    a.tiles_per_group = (int)((ntile + groups0 - 1) / groups0);
+    const unsigned groups = (unsigned)((ntile + a.tiles_per_group - 1) / a.tiles_per_group);
+    const dim3 g(N / 256, groups, nz);
+#define BCV(S, V) hipLaunchKernelGGL((k_bconv_mfma<S, V>), g, dim3(256), 0, e->stream, a, e->logN)
+    switch (nstep * 2 + (vc ? 1 : 0)) {
+        case 2: BCV(1, false); break;
+        case 3: BCV(1, true); break;
+        case 4: BCV(2, false); break;
+        case 5: BCV(2, true); break;
+        case 6: BCV(3, false); break;
+        case 7: BCV(3, true); break;
+        case 8: BCV(4, false); break;
+        default: BCV(4, true); break;
+    }
+#undef BCV
+    HIPC(hipGetLastError());
+}
+
 static int ks_beta(const aesfhe_engine* e, int l) {
     const int beta = (l + 1 + e->A - 1) / e->A;
     if (beta > 12) throw_err(AESFHE_EUNSUPPORTED, "more than 12 key-switch digits");
@@ -1960,13 +2087,15 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
     // extension of extra memory, not one per digit (with the ModDown conv pass out of place as
     // well: round +0.8 %, A/B/A/B/A on one box, profiles/r04/ab/oop/)
     const bool oop = cols_only;
-    std::unique_ptr<Tmp> mu;
-    if (oop) mu.reset(new Tmp(e, (size_t)B * neN));
+    std::unique_ptr<Tmp> mu;  // only when some digit runs k_modup (alpha > 1)
+    bool any_wide = false;
+    for (int j = 0; j < beta; j++) any_wide |= std::min((j + 1) * e->A, l + 1) - j * e->A > 1;
+    if (oop && any_wide) mu.reset(new Tmp(e, (size_t)B * neN));
     for (int j = 0; j < beta; j++) {
         const int A = e->A, lo = j * A, hi = std::min(lo + A, l + 1), alpha = hi - lo;
         const size_t set = (size_t)j * A + (alpha - 1);
         u64* exj = ext + (size_t)j * B * neN;
-        u64* muj = oop ? mu->p : exj;  // where ModUp writes
+        u64* muj = mu ? mu->p : exj;  // where ModUp writes (mu absent: every digit is one limb)
         if (cols_only && alpha == 1) {
             // one-limb digit: the conversion is x mod p_t (hat = hatinv = 1), formed in the column
             // pass's copy-in from the digit limb itself (no k_modup<1> write + read-back)
@@ -1985,6 +2114,29 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         {
             ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne, "modup");
             if (alpha < 1 || alpha > 16) throw_err(AESFHE_EUNSUPPORTED, "ModUp digit width outside 1..16");
+            if (bconv_mfma_on()) {
+                BconvArgs a{};
+                a.src = (const u64*)dc.p + (long)lo * N;
+                a.sbs = lN;
+                a.dst = muj;
+                a.dbs = neN;
+                a.nc = 1;
+                a.ns = alpha;
+                a.s_nq = alpha;
+                a.s_q0 = lo;
+                a.sinvf = e->mu_hatinvf + set * A;
+                a.nt = ne - alpha;
+                a.skip0 = lo;
+                a.skipn = alpha;
+                a.tl_l = l;
+                a.Lp1 = e->Lp1;
+                a.tab = e->bc_mu_tab + set * e->np * 8 * kBconvKT;
+                a.corr = e->bc_mu_corr + set * e->np;
+                a.w32f = e->bc_w32f;
+                a.qall = e->q;
+                a.qinvall = e->qinv;
+                launch_bconv(e, a, B, alpha, false);
+            } else
             AESFHE_DISPATCH16(alpha, launch_modup, dim3(N / 256, bconv_groups(N, B, ne), B), e->stream, (const u64*)dc.p, lN, muj, neN, lo, l, ne,
                               (const double*)(e->mu_hatinvf + set * A), (const TwD*)(e->mu_hatf + set * A * e->np),
                               A, e->q, e->qinv, e->Lp1, e->logN);
@@ -2026,7 +2178,7 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
         const int nown = std::min(l + 1, beta * e->A);
         const double opw = pb ? (4.0 + (pc && pc->ptr ? 2.0 : 0.0)) * (l + 1)
                               : (double)nown + (pmod && addend.ptr ? (double)addend.np * (l + 1) : 0.0);
-        ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown + opw) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))), "ks_rows_inner");
+        ProfScope ps(e, FAM_KS, 8.0 * N * ((double)B * (beta * ne - nown + opw) + (double)ne * (2.0 * beta + 2.0 * B * (accum ? 2 : 1))), pb ? "ks_rows_acc.prod" : "ks_rows_acc.ks");
         const int R = N / 256, blocks = 8 * B * (ne * (R / 8) / 8);
         const Opnd none{nullptr, 0, 0, 0};
         auto kern = pb ? (R == 256 ? k_nttf_rows_ks<1, 256, true> : k_nttf_rows_ks<1, 512, true>)
@@ -2048,15 +2200,20 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
 // ([B][2][lk+1][N], coefficient form).  Returns D^{-1} mod q_i (as w / q) for the finish.
 // rows_done (fused_ntt engines): the dropped limbs already hold their inverse row pass (raw
 // doubles, k_nttf_rows_ks EPI 2), so only the inverse column pass runs.
-static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int r, u64* conv, bool rows_done = false) {
+// abs_ / acs: acc's batch and component strides (default: the full [B][2][l+1+K][N] layout; a
+// caller that holds only the dropped limbs passes its own, with acc offset so that limb t is at
+// acc + t N as before).
+static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int r, u64* conv, bool rows_done = false,
+                                  long abs_ = 0, long acs = 0) {
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long neN = (long)ne * N;
+    if (!acs) acs = neN, abs_ = 2 * neN;
     if (r < 0 || r > kMdrMaxR || K + r > kMdrMaxE || l - r < 0) throw_err(AESFHE_EARG, "bad combined rescale depth %d", r);
     const int lk = l - r;  // output level
     const long kN = (long)(lk + 1) * N;
     // 4. ModDown: INTT the dropped limbs (top r Q limbs + the special limbs) of both accumulators
     {
-        Span ssp = span_s(acc + (long)(lk + 1) * N, neN, K + r, r, lk + 1, e->Lp1);
+        Span ssp = span_s(acc + (long)(lk + 1) * N, acs, K + r, r, lk + 1, e->Lp1);
         const int total = B * 2 * (K + r);
         if (rows_done) {
             ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_inv_cols");
@@ -2074,7 +2231,34 @@ static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int 
     {
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1), "moddown");
         if (K + r < 1 || K + r > 16) throw_err(AESFHE_EUNSUPPORTED, "ModDown source width outside 1..16");
-        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, bconv_groups(N, B * 2, lk + 1), B * 2), e->stream, (const u64*)acc, 2 * neN, neN, l, r, conv, 2 * kN, kN,
+        if (bconv_mfma_on() && K + r + 1 <= 16) {
+            BconvArgs a{};
+            a.src = acc + (long)(lk + 1) * N;
+            a.sbs = abs_;
+            a.scs = acs;
+            a.dst = conv;
+            a.dbs = 2 * kN;
+            a.dcs = kN;
+            a.nc = 2;
+            a.ns = K + r;
+            a.s_nq = r;
+            a.s_q0 = lk + 1;
+            a.s_p0 = e->Lp1;
+            a.sinvf = invf;
+            a.einv = r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv;
+            a.nt = lk + 1;
+            a.skip0 = lk + 1;
+            a.skipn = 0;
+            a.tl_l = lk;
+            a.Lp1 = e->Lp1;
+            a.tab = r ? e->bc_mdr_tab + cell * e->Lp1 * 8 * kBconvKT : e->bc_md_tab;
+            a.corr = r ? e->bc_mdr_corr + cell * e->Lp1 : e->bc_md_corr;
+            a.w32f = e->bc_w32f;
+            a.qall = e->q;
+            a.qinvall = e->qinv;
+            launch_bconv(e, a, B * 2, K + r + 1, true);
+        } else
+        AESFHE_DISPATCH16(K + r, launch_moddown, dim3(N / 512, bconv_groups(N, B * 2, lk + 1), B * 2), e->stream, (const u64*)acc, abs_, acs, l, r, conv, 2 * kN, kN,
                            invf, hatf, r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv,
                            r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN, hs);
     }
@@ -2156,36 +2340,47 @@ static void ks_finish_fused(aesfhe_engine* e, const u64* d, long dbs, const u64*
                             (accum ? 2.0 * nt : 0.0);  // accum: the earlier sums read
         return 8.0 * N * ((double)B * ((double)beta * nt - nq + opw + outw) + 2.0 * beta * nt);
     };
-    auto launch = [&](int t0, int nt, bool fin, u64* acc, const KsFin& kf) {
+    auto launch = [&](int t0, int nt, bool fin, u64* acc, long abs_, long acs, const KsFin& kf) {
         const int blocks = 8 * B * (nt * (R / 8) / 8 + ((nt * (R / 8)) % 8 ? 1 : 0));
         const int nq = std::max(0, std::min(t0 + nt, l + 1) - t0);
-        ProfScope ps(e, FAM_KS, bytes(nt, nq, fin), fin ? "ks_rows_fin" : "ks_rows_inner");
+        // one label per kernel instantiation (PROD or not): a class average over launches of very
+        // different sizes is not comparable with a rocprof per-symbol average
+        ProfScope ps(e, FAM_KS, bytes(nt, nq, fin),
+                     fin ? (pb ? "ks_rows_fin.prod" : "ks_rows_fin.ks") : (pb ? "ks_rows_inner.prod" : "ks_rows_inner.ks"));
         // the dropped limbs leave with their inverse row pass done (EPI 2), the kept ones finished (EPI 1)
         auto kern = R == 256 ? (pb ? (fin ? k_nttf_rows_ks<1, 256, true, 1> : k_nttf_rows_ks<1, 256, true, 2>)
                                    : (fin ? k_nttf_rows_ks<1, 256, false, 1> : k_nttf_rows_ks<1, 256, false, 2>))
                              : (pb ? (fin ? k_nttf_rows_ks<1, 512, true, 1> : k_nttf_rows_ks<1, 512, true, 2>)
                                    : (fin ? k_nttf_rows_ks<1, 512, false, 1> : k_nttf_rows_ks<1, 512, false, 2>));
         hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d,
-                           2L * e->np * N, (long)e->np * N, acc, 2 * neN, neN, B, beta, e->A, l, ne, e->tabs(), addend, pm,
+                           2L * e->np * N, (long)e->np * N, acc, abs_, acs, B, beta, e->A, l, ne, e->tabs(), addend, pm,
                            (int)accum, pb ? *pb : none, fac, pc ? *pc : none, t0, nt, kf);
         HIPC(hipGetLastError());
     };
-    std::unique_ptr<Tmp> own;  // only the dropped limbs lk + 1 .. ne - 1 are written
-    if (!acc_in) own.reset(new Tmp(e, (size_t)B * 2 * neN));
-    u64* acc = acc_in ? acc_in : own->p;
-    launch(lk + 1, ne - (lk + 1), false, acc, KsFin{});
-    Tmp conv(e, (size_t)B * 2 * kN);
-    const double* dinvf = moddown_conv(e, acc, B, l, r, conv.p, true);
+    // only the dropped limbs lk + 1 .. ne - 1 are written: an own accumulator holds just those
+    // ([B][2][nd][N], nd = ne - lk - 1; ADVICE r4: the full [B][2][ne][N] block was ~1 GB per key
+    // switch at B = 32, l = 30 of memory never touched), addressed through a base pointer offset by
+    // lk + 1 limbs so that limb t still sits at acc + t N; the FIN launch does not read acc then
+    const int nd = ne - (lk + 1);
+    std::unique_ptr<Tmp> own;
+    if (!acc_in) own.reset(new Tmp(e, (size_t)B * 2 * nd * N));
+    u64* acc = acc_in ? acc_in : own->p - (long)(lk + 1) * N;
+    const long abs_ = acc_in ? 2 * neN : 2L * nd * N, acs = acc_in ? neN : (long)nd * N;
+    launch(lk + 1, nd, false, acc, abs_, acs, KsFin{});
+    std::unique_ptr<Tmp> conv(new Tmp(e, (size_t)B * 2 * kN));
+    const double* dinvf = moddown_conv(e, acc, B, l, r, conv->p, true, abs_, acs);
+    if (own) own.reset();  // the dropped limbs are converted: stream-ordered reuse from here on
     Tmp conv2(e, (size_t)B * 2 * kN);
     {
         const int total = B * 2 * (lk + 1);
         ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
-        ntt_fwd_cols(e, span_s(conv.p, kN, lk + 1, lk + 1, 0, e->Lp1), span_s(conv2.p, kN, lk + 1, lk + 1, 0, e->Lp1), total);
+        ntt_fwd_cols(e, span_s(conv->p, kN, lk + 1, lk + 1, 0, e->Lp1), span_s(conv2.p, kN, lk + 1, lk + 1, 0, e->Lp1), total);
     }
+    conv.reset();  // conv's coefficient form is read only by the column pass
     HIPC(hipGetLastError());
     const KsFin kf{conv2.p, 2 * kN, kN, o->d, 2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf,
                    Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}};
-    launch(0, lk + 1, true, acc, kf);
+    launch(0, lk + 1, true, acc, abs_, acs, kf);
 }
 
 // Key switch, second half: inner product of ext (ks_modup of d) with key k, ModDown (fused with

@@ -50,6 +50,22 @@ def test_abi_version(product_cdll, oracle_lib):
     assert product_cdll.abi_version() == want and oracle_lib.abi_version() == want
 
 
+@pytest.mark.parametrize("body", ["", "int aesfhe_abi_version(void) { return 1; }",
+                                  "int aesfhe_abi_version(void) { return %d; }"],
+                         ids=["no-version-symbol", "old-revision", "missing-symbol"])
+def test_stale_library_reads_as_rebuild(tmp_path, body):
+    """A library built against an older header -- without aesfhe_abi_version, with an older
+    revision, or with the current revision but a symbol missing -- is refused with a "rebuild it"
+    RuntimeError before anything else is bound, not a ctypes AttributeError."""
+    from aes_xor_fhe._abi import ABI_VERSION, Lib
+    src = tmp_path / "stale.c"
+    src.write_text((body % ABI_VERSION if "%d" in body else body) + "\nint aesfhe_unrelated(void) { return 0; }\n")
+    so = tmp_path / "libstale.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    with pytest.raises(RuntimeError, match="rebuild it"):
+        Lib(so)
+
+
 @pytest.mark.parametrize("log_n", [10, 12, 16])
 def test_host_codec_bit_identical(product_cdll, oracle_lib, log_n):
     n = 1 << (log_n - 1)

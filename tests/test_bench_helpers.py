@@ -89,3 +89,37 @@ def test_dominant_roofline_picks_the_largest_share():
     r = bench.dominant_roofline(bench.kernel_table(_FakeEngine(raw), {}, 2), 2, {})
     assert r["traffic"] is None and r["traffic_head"] is None
     assert bench.dominant_roofline(None, 2, {})["frac"] is None
+
+
+def test_dominant_class_over_two_instantiations():
+    """ks_rows_fin launches two instantiations of one kernel template (228 product
+    launches of ~0.94 ms and 4 plain ones of ~6.8 ms per step).  The table keeps them apart
+    (each compares with its own rocprof symbol average); the headline class figure is the sum of
+    bytes over the sum of time, and lists every instantiation's own figures."""
+    steps = 2
+    raw = {"ks_rows_fin.prod": [2 * 228, 2 * 228 * 0.9366, 2 * 228 * 5.0e9, 2 * 228],
+           "ks_rows_fin.ks": [2 * 4, 2 * 4 * 6.848, 2 * 4 * 3.6e10, 2 * 4],
+           "ntt_fwd_cols": [2 * 1328, 2 * 1328 * 0.1739, 2 * 1328 * 4.457e8, 2 * 1328]}
+    pmc = {"head": "h", "csrc_sha16": "0" * 16,
+           "per_kernel": {"ks_rows_fin.prod": {"launches": 228, "hbm_bytes_per_launch": 5.4e9},
+                          "ks_rows_fin.ks": {"launches": 4, "hbm_bytes_per_launch": 3.8e10}}}
+    t = bench.kernel_table(_FakeEngine(raw), pmc, steps)
+    assert t["ks_rows_fin.prod"]["class"] == "ks_rows_fin"
+    assert t["ks_rows_fin.prod"]["avg_us"] == pytest.approx(936.6)
+    assert t["ks_rows_fin.ks"]["avg_us"] == pytest.approx(6848.0)
+    assert t["ks_rows_fin.prod"]["frac"] == pytest.approx(5.0e9 / 936.6e-6 / 8e12, rel=1e-3)
+    r = bench.dominant_roofline(t, steps, pmc)
+    assert r["kernel"].startswith("ks_rows_fin:")
+    ms = 228 * 0.9366 + 4 * 6.848
+    by = 228 * 5.0e9 + 4 * 3.6e10
+    assert r["avg_launch_us"] == pytest.approx(ms / 232 * 1e3, rel=1e-4)
+    assert r["achieved"] == pytest.approx(by / (ms * 1e-3) / 1e9, rel=1e-3)
+    assert r["frac"] == pytest.approx(by / (ms * 1e-3) / 8e12, rel=1e-3)
+    assert r["launches"] == 2 * 232
+    assert set(r["instantiations"]) == {"ks_rows_fin.prod", "ks_rows_fin.ks"}
+    assert r["instantiations"]["ks_rows_fin.ks"]["avg_us"] == pytest.approx(6848.0)
+    assert r["traffic"] == pytest.approx((228 * 5.4e9 + 4 * 3.8e10) / 232, rel=1e-6)
+    # one instantiation without a PMC figure: no class traffic (never a partial sum)
+    del pmc["per_kernel"]["ks_rows_fin.ks"]
+    r = bench.dominant_roofline(bench.kernel_table(_FakeEngine(raw), pmc, steps), steps, pmc)
+    assert r["traffic"] is None

@@ -138,3 +138,31 @@ def test_deferred_conjugations_batched_residue_exact(oracle_lib):
         np.testing.assert_allclose(e.decrypt(cj[1], sk), np.conj(z[2]), atol=1e-4)
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
+
+
+def test_fused_products_leave_the_pending_cap(oracle_lib):
+    """products a fused sum (aesfhe_poly2) has used no longer count against
+    max_pending, so building more than max_pending products in fused groups never falls back
+    to an eager aesfhe_mul per product -- and the fused results decode correctly."""
+    e = Engine(_lib=oracle_lib, max_pending=4, **KW)
+    sk = e.create_secret_key(3)
+    pk, rlk = e.create_public_key(sk), e.create_relinearization_key(sk)
+    z = np.random.default_rng(7).uniform(-1, 1, (3, e.slot_count))
+    a, b, c = (e.encrypt(v, pk, level=6) for v in z)
+    calls = []
+    real = e._lib.mul
+    e._lib.mul = lambda *args: (calls.append(1), real(*args))[1]
+    try:
+        outs = []
+        for g in range(4):  # 4 groups x 3 products = 12 > max_pending
+            k = 0.25 * (g + 1)
+            s = e.add(e.add(e.multiply(e.multiply(a, b, rlk), k), e.multiply(e.multiply(a, c, rlk), -k)),
+                      e.multiply(e.multiply(b, c, rlk), 0.5))
+            outs.append((k, e.decrypt(s, sk)))  # materialised: one poly2 of the group
+        assert not calls, f"{len(calls)} eager aesfhe_mul calls"
+        assert len(e._pending) == 0
+    finally:
+        e._lib.mul = real
+    for k, got in outs:
+        want = k * z[0] * z[1] - k * z[0] * z[2] + 0.5 * z[1] * z[2]
+        np.testing.assert_allclose(got.real, want, atol=1e-3)

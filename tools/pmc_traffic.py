@@ -25,8 +25,12 @@ CLASSES = [
     (r"k_nttf_inv_rows<\d+, false", "ntt_inv_rows"),
     (r"k_nttf_inv_cols<", "ntt_inv_cols"),
     (r"k_ntt_(fwd|inv)_(rows|cols)<", "ntt_generic"),
-    (r"k_nttf_rows_ks<\d+, \d+, (true|false), 1>", "ks_rows_fin"),
-    (r"k_nttf_rows_ks<", "ks_rows_inner"),
+    (r"k_nttf_rows_ks<\d+, \d+, true, 1>", "ks_rows_fin.prod"),
+    (r"k_nttf_rows_ks<\d+, \d+, false, 1>", "ks_rows_fin.ks"),
+    (r"k_nttf_rows_ks<\d+, \d+, true, 2>", "ks_rows_inner.prod"),
+    (r"k_nttf_rows_ks<\d+, \d+, false, 2>", "ks_rows_inner.ks"),
+    (r"k_nttf_rows_ks<\d+, \d+, true", "ks_rows_acc.prod"),
+    (r"k_nttf_rows_ks<", "ks_rows_acc.ks"),
     (r"k_ks_inner_all<", "ks_inner"),
     (r"k_ks_inner_multi<", "ks_inner_multi"),
     (r"k_modup<", "modup"),
