@@ -301,17 +301,37 @@ class AESRowRound:
         counts = [self.refreshes_after(rnd, b.bits_level, top, stc, with_clean=True) for b in bss]
         return bss[counts.index(min(counts))]
 
-    def refresh_step(self, S, rnd: int, level: int, since: int, refreshed: bool, bss, pairs_per_call: int):
+    def refresh_step(self, S, rnd: int, level: int, since: int, refreshed: bool, bss, pairs_per_call: int,
+                     probe=None):
         """The refresh before round rnd (state S at `level`, `since` rounds after the previous
         refresh): pick the bootstrapper, clean the bits first when this is the last refresh and
-        can_clean allows it, bootstrap.  Returns (state, bootstrapper, cleaned)."""
+        can_clean allows it, bootstrap.  Returns (state, bootstrapper, cleaned).  probe: optional
+        callable(rnd, state, in_scale) shown the state the bootstrap takes (after the cleaning)."""
         stc = len(bss[0].stc_bits)
         b = self.pick_bootstrapper(bss, rnd)
         top = max(x.bits_level for x in bss)
         clean = self.can_clean(level, since, refreshed, stc) and self.refreshes_after(rnd, b.bits_level, top, stc) == 0
         if clean:
             S = self.clean_bits(S)
+        if probe is not None:
+            probe(rnd, S, 2.0 if clean else 1.0)
         return self.refresh(S, b, pairs_per_call, in_scale=2.0 if clean else 1.0), b, clean
+
+    def bit_margin(self, bits, scale: float = 1.0) -> float:
+        """max over every slot of every bit ciphertext of | |v| / scale - 1 |: how far the +-1 bit
+        values have drifted (a bit decodes wrongly past 1).  Decrypted on the device when the
+        engine is the HIP one (the reduction too), else on the host."""
+        worst = 0.0
+        for row in bits:
+            for c in row:
+                if self.e.on_device:
+                    v = self.e.decrypt_device(c, self.sk).real
+                    d = float((v.abs() / scale - 1.0).abs().max())
+                else:
+                    v = np.real(np.atleast_2d(self.e.decrypt(c, self.sk)))
+                    d = float(np.abs(np.abs(v) / scale - 1.0).max())
+                worst = max(worst, d)
+        return worst
 
     def clean_bits(self, bits):
         """3x - x^3 for every bit ciphertext (= 2 * (3x - x^3) / 2, the cleaning map with error
@@ -364,7 +384,7 @@ class AESRowRound:
         return [L] + [lvl - self.KEY_OFFSET for _, lvl, _ in self.schedule(L, bss)]
 
     def encrypt_aes128(self, bits, keys, bs, timings: dict | None = None, pairs_per_call: int = 8,
-                       progress=None, consume: bool = False):
+                       progress=None, consume: bool = False, probe=None):
         """AES-128 encryption of the bit state under the 11 encrypted round keys `keys`
         (FIPS-197 section 5.1), bootstrapping with `bs` (a bootstrap.Bootstrapper, or a list of them
         cheapest first: each refresh takes the first whose output level costs no extra refresh,
@@ -372,7 +392,8 @@ class AESRowRound:
         Returns the state and the number of refreshes.  progress: optional callable(str) told
         after each step.  consume: empty the rows of `bits` after AddRoundKey(k_0), so that the
         input state (the largest one, at the top level) is freed if the caller holds it only
-        through that list."""
+        through that list.  probe: optional callable(rnd, state, in_scale) shown every refresh's
+        input (refresh_step)."""
         import time
         bss = list(bs) if isinstance(bs, (list, tuple)) else [bs]
         stc = len(bss[0].stc_bits)
@@ -389,7 +410,7 @@ class AESRowRound:
             lvl = min(c.level for row in S for c in row)
             if self.needs_refresh(lvl, final, since, refreshes > 0, stc):
                 t0 = time.perf_counter()
-                S, b, clean = self.refresh_step(S, rnd, lvl, since, refreshes > 0, bss, pairs_per_call)
+                S, b, clean = self.refresh_step(S, rnd, lvl, since, refreshes > 0, bss, pairs_per_call, probe)
                 since = 0
                 refreshes += 1
                 if progress:

@@ -117,25 +117,41 @@ __global__ __launch_bounds__(256) void k_bconv_mfma(BconvArgs a, int logN) {
         }
     }
     // ---- target tiles ------------------------------------------------------------------------
+    // software-pipelined: tile + 1's A fragments and epilogue constants are requested before tile's
+    // epilogue runs (every load branch-free: absent targets read pid 0 and are not stored), so the
+    // L2 round trips of a tile hide behind the previous one's VALU work
     const int row = lane & 31;  // this lane's A row: target 2 ((row >> 2) & 1) + (row >> 4), plane b
     const int ta = 2 * ((row >> 2) & 1) + (row >> 4), pb = 4 * ((row >> 3) & 1) + (row & 3);
     u64* dst = a.dst + (long)zb * a.dbs + (long)zc * a.dcs;
     const int tile0 = blockIdx.y * a.tiles_per_group;
     const int ntile = (a.nt + 3) >> 2;
-    for (int tile = tile0; tile < tile0 + a.tiles_per_group && tile < ntile; tile++) {
-        bc_v4i af[NSTEP];
-        {
-            const int tau = 4 * tile + ta;
-            const int tl = tau < a.skip0 ? tau : tau + a.skipn;
-            const int pid = tl <= a.tl_l ? tl : a.Lp1 + tl - a.tl_l - 1;
-            const bool ok = tau < a.nt;
-            const bc_v4i* ap = (const bc_v4i*)(a.tab + ((long)(ok ? pid : 0) * 8 + pb) * kBconvKT + 16 * h);
+    const int tile1 = min(tile0 + a.tiles_per_group, ntile);
+    auto limb_of = [&](int tau) { return tau < a.skip0 ? tau : tau + a.skipn; };
+    auto pid_of = [&](int tl) { return tl <= a.tl_l ? tl : a.Lp1 + tl - a.tl_l - 1; };
+    // (a target past nt reads pid 0's row: its D rows are computed and never stored -- a row of D
+    // depends on that row of A only -- so no load result is ever selected or waited for early)
+    bc_v4i af[NSTEP];
+    u64 cq[2];
+    double cqi[2], ccr[2], cf32[2];
+    auto fetch = [&](int tile) {
+        const int tau = 4 * tile + ta;
+        const bc_v4i* ap =
+            (const bc_v4i*)(a.tab + ((long)(tau < a.nt ? pid_of(limb_of(tau)) : 0) * 8 + pb) * kBconvKT + 16 * h);
 #pragma unroll
-            for (int s = 0; s < NSTEP; s++) {
-                const bc_v4i x = ap[2 * s];  // bytes 32 s + 16 h .. + 15 of the row
-                af[s] = ok ? x : bc_v4i{0, 0, 0, 0};
-            }
+        for (int s = 0; s < NSTEP; s++) af[s] = ap[2 * s];  // bytes 32 s + 16 h .. + 15 of the row
+#pragma unroll
+        for (int t2 = 0; t2 < 2; t2++) {
+            const int tt = 4 * tile + 2 * h + t2;
+            const int pid = tt < a.nt ? pid_of(limb_of(tt)) : 0;
+            cq[t2] = a.qall[pid];
+            cqi[t2] = a.qinvall[pid];
+            ccr[t2] = a.corr[pid];
+            cf32[t2] = a.w32f[pid];
         }
+    };
+    if (tile0 < tile1) fetch(tile0);
+#pragma unroll 1
+    for (int tile = tile0; tile < tile1; tile++) {
         bc_v16i acc[2];
 #pragma unroll
         for (int g = 0; g < 2; g++) {
@@ -143,21 +159,21 @@ __global__ __launch_bounds__(256) void k_bconv_mfma(BconvArgs a, int logN) {
 #pragma unroll
             for (int s = 0; s < NSTEP; s++) acc[g] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bf[g][s], acc[g], 0, 0, 0);
         }
+        const u64 q0 = cq[0], q1 = cq[1];
+        const double qi0 = cqi[0], qi1 = cqi[1], cr0 = ccr[0], cr1 = ccr[1], f0 = cf32[0], f1 = cf32[1];
+        if (tile + 1 < tile1) fetch(tile + 1);
         // epilogue: this lane holds targets 4 tile + 2 h + t2 (t2 = 0, 1), planes b in registers
         // 4 (2 t2 + (b >> 2)) + (b & 3), of coefficient kb + 32 g + c
 #pragma unroll
         for (int t2 = 0; t2 < 2; t2++) {
             const int tau = 4 * tile + 2 * h + t2;
-            if (tau >= a.nt) continue;
-            const int tl = tau < a.skip0 ? tau : tau + a.skipn;
-            const int pid = tl <= a.tl_l ? tl : a.Lp1 + tl - a.tl_l - 1;
-            const double q = (double)a.qall[pid], qi = a.qinvall[pid];
-            const double cr = a.corr[pid], f32 = a.w32f[pid], w32 = tw_w(f32, q);
-            u64* op = dst + ((long)tl << logN) + kb + c;
+            const double q = (double)(t2 ? q1 : q0), qi = t2 ? qi1 : qi0, cr = t2 ? cr1 : cr0, f32 = t2 ? f1 : f0;
+            const double w32 = tw_w(f32, q);
+            u64* op = dst + ((long)limb_of(tau) << logN) + kb + c;
 #pragma unroll
             for (int g = 0; g < 2; g++) {
                 const int r0 = 8 * t2;
-                // |S_b| <= 128 * 128 * 32 NSTEP < 2^21: every partial sum below is an exact integer
+                // |S_b| <= 128 * 128 * (7 * 16 + 1) < 2^21: every partial sum below is an exact integer
                 double lo = (double)acc[g][r0 + 3];
                 lo = __builtin_fma(lo, 256.0, (double)acc[g][r0 + 2]);
                 lo = __builtin_fma(lo, 256.0, (double)acc[g][r0 + 1]);
@@ -168,7 +184,7 @@ __global__ __launch_bounds__(256) void k_bconv_mfma(BconvArgs a, int logN) {
                 hi = __builtin_fma(hi, 256.0, (double)acc[g][r0 + 4]);
                 // |lo|, |hi| < 2^46; (2^32 hi mod p) in (-p, p); + corr < p: below 2^52
                 const double v = lo + fmul_rem(hi, w32, f32, q) + cr;
-                __builtin_nontemporal_store(fcanon(v, q, qi), &op[32 * g]);  // streaming, as k_modup
+                if (tau < a.nt) __builtin_nontemporal_store(fcanon(v, q, qi), &op[32 * g]);  // streaming
             }
         }
     }

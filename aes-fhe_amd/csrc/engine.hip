@@ -2052,6 +2052,12 @@ static void launch_bconv(aesfhe_engine* e, BconvArgs a, int nz, int nslots, bool
     HIPC(hipGetLastError());
 }
 
+// AESFHE_KS_PIPE=1: the LDS-DMA pipelined key-switch row kernels (ks_fused.h k_nttf_rows_ks_p), A/B
+static bool ks_pipe_on() {
+    static const bool on = getenv("AESFHE_KS_PIPE") && atoi(getenv("AESFHE_KS_PIPE"));
+    return on;
+}
+
 static int ks_beta(const aesfhe_engine* e, int l) {
     const int beta = (l + 1 + e->A - 1) / e->A;
     if (beta > 12) throw_err(AESFHE_EUNSUPPORTED, "more than 12 key-switch digits");
@@ -2352,6 +2358,11 @@ static void ks_finish_fused(aesfhe_engine* e, const u64* d, long dbs, const u64*
                                    : (fin ? k_nttf_rows_ks<1, 256, false, 1> : k_nttf_rows_ks<1, 256, false, 2>))
                              : (pb ? (fin ? k_nttf_rows_ks<1, 512, true, 1> : k_nttf_rows_ks<1, 512, true, 2>)
                                    : (fin ? k_nttf_rows_ks<1, 512, false, 1> : k_nttf_rows_ks<1, 512, false, 2>));
+        if (ks_pipe_on())
+            kern = R == 256 ? (pb ? (fin ? k_nttf_rows_ks_p<256, true, 1> : k_nttf_rows_ks_p<256, true, 2>)
+                                  : (fin ? k_nttf_rows_ks_p<256, false, 1> : k_nttf_rows_ks_p<256, false, 2>))
+                            : (pb ? (fin ? k_nttf_rows_ks_p<512, true, 1> : k_nttf_rows_ks_p<512, true, 2>)
+                                  : (fin ? k_nttf_rows_ks_p<512, false, 1> : k_nttf_rows_ks_p<512, false, 2>));
         hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, e->stream, d, dbs, ext, neN, (long)B * neN, (const u64*)k->d,
                            2L * e->np * N, (long)e->np * N, acc, abs_, acs, B, beta, e->A, l, ne, e->tabs(), addend, pm,
                            (int)accum, pb ? *pb : none, fac, pc ? *pc : none, t0, nt, kf);

@@ -213,6 +213,50 @@ __device__ __forceinline__ void row_intt8(double (&x)[8], double* sr, int L, con
 // done, raw doubles, fin.conv[b][c][t]) get their row pass here -- same prime, same row, so the
 // staged twiddles serve them -- and out[b][c][t] = (acc_c - conv_c) D^{-1} (+ fin.add_c) is
 // written canonical; the dropped limbs (t > lk) ran through the non-FIN launch first, into acc.
+// The PROD prologue (see k_nttf_rows_ks below): d0 = a0 b0, d1 = a0 b1 + a1 b0 times P and the own
+// digit's d2 = a1 b1 times its key words, for the lane's 8 elements of (limb t, row).  FMA (the
+// multiply-add of aesfhe_mul_fma, fac != nullptr) is a template argument: with a runtime `if (fac)`
+// inside the element loop every element's 6 operand loads sat behind their own branch and wait
+// (the ISA showed vmcnt(5)..(0) per element), so the prologue's 48 loads were serialised 8 times.
+template <bool FMA>
+__device__ __forceinline__ void ks_prod_prologue(double (&a0)[8], double (&a1)[8], const u64* kp, long kcomp,
+                                                 const u64* xa, long aps, const u64* xb, long bps, const u64* xc,
+                                                 long cps, bool has_c, double wv, double f, double fal, double fC,
+                                                 double fK, double q, double qi, bool big) {
+    double x0[8], x1[8], y0[8], y1[8], kb[8], ka[8];
+#pragma unroll
+    for (int r = 0; r < 8; r++) {  // every operand word requested before the first product
+        x0[r] = u2d(xa[32 * r]);
+        x1[r] = u2d(xa[aps + 32 * r]);
+        y0[r] = u2d(xb[32 * r]);
+        y1[r] = u2d(xb[bps + 32 * r]);
+        kb[r] = u2d(kp[32 * r]);
+        ka[r] = u2d(kp[32 * r + kcomp]);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        const double y0q = y0[r] * qi, y1q = y1[r] * qi;
+        double p0 = fmul_rem(x0[r], y0[r], y0q, q);
+        double p1 = fmul_rem(x0[r], y1[r], y1q, q) + fmul_rem(x1[r], y0[r], y0q, q);
+        double p2 = fmul_rem(x1[r], y1[r], y1q, q);
+        if constexpr (FMA) {  // multiply-add: alpha (a (x) b) + C (c0, c1, 0) + (K, 0, 0)
+            p0 = fmul_rem(p0, fal, fal * qi, q) + fK;
+            p1 = fmul_rem(p1, fal, fal * qi, q);
+            p2 = fmul_rem(p2, fal, fal * qi, q);
+            if (has_c) {
+                p0 += fmul_rem(u2d(xc[32 * r]), fC, fC * qi, q);
+                p1 += fmul_rem(u2d(xc[cps + 32 * r]), fC, fC * qi, q);
+            }
+        }
+        a0[r] = fmul_rem(p0, wv, f, q) + fmul_rem(p2, kb[r], kb[r] * qi, q);
+        a1[r] = fmul_rem(p1, wv, f, q) + fmul_rem(p2, ka[r], ka[r] * qi, q);
+        if (big) {
+            a0[r] = fred(a0[r], q, qi);
+            a1[r] = fred(a1[r], q, qi);
+        }
+    }
+}
+
 struct KsFin {
     const u64* conv;
     long cbs, cps;
@@ -435,6 +479,229 @@ __global__ __launch_bounds__(256, G == 1 ? 4 : 2) void k_nttf_rows_ks(const u64*
             __builtin_nontemporal_store(fcanon(a0[g][r], q, qi), &o0[32 * r]);  // streaming
             __builtin_nontemporal_store(fcanon(a1[g][r], q, qi), &o0[acs + 32 * r]);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pipelined variant (G = 1): the extension row of the NEXT digit (and, in
+// the FIN epilogue, the next conv row) is fetched by LDS-DMA (global_load_lds_dwordx4: no VGPR
+// destination) into a per-wave staging buffer while the current digit's row NTT runs, so the ext
+// latency that k_nttf_rows_ks exposes once per digit (the load is issued, then waited for by the
+// NTT's first butterflies) overlaps the NTT instead.  The own digit of a plain key switch (d rows,
+// already NTT form) joins the prologue.  16 KB more LDS (51.2 KB: 3 workgroups per CU) and no
+// more registers for the staging.  A row pair of a wave is 4 KB contiguous in HBM and lands
+// linearly in the wave's 4 KB of the buffer (4 x 1 KB wave-instructions); the wave that issues a
+// DMA is the one that reads it (after its own vmcnt), so no workgroup barrier is needed.
+typedef __attribute__((address_space(3))) void ks_lds_void;
+__device__ __forceinline__ void ks_dma_rows(const u64* g, double* lds_wave, int lane) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        __builtin_amdgcn_global_load_lds((const void*)(g + 128 * k + 2 * lane), (ks_lds_void*)(lds_wave + 128 * k), 16, 0, 0);
+}
+// every DMA of this wave landed (and, being the issuing wave, its LDS reads see the bytes)
+__device__ __forceinline__ void ks_dma_wait() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+// this wave's LDS reads are complete before a new DMA may overwrite the buffer
+__device__ __forceinline__ void ks_lds_reads_done() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int R = 256, bool PROD = false, int EPI = 0>
+__global__ __launch_bounds__(256, 3) void k_nttf_rows_ks_p(const u64* __restrict__ d, long dbs,
+                                                      const u64* __restrict__ ext, long exs, long exj,
+                                                      const u64* __restrict__ key, long kdig, long kcomp,
+                                                      u64* __restrict__ acc, long abs_, long acs, int B,
+                                                      int beta, int K, int l, int ne, Tabs T, Opnd addend,
+                                                      const double* __restrict__ pmodf, int accum, Opnd pb,
+                                                      const u64* __restrict__ fac, Opnd pc, int t0, int nt,
+                                                      KsFin fin) {
+    constexpr bool FIN = EPI == 1, INV = EPI == 2;
+    // sr (row transposes) | tw (the 8 rows' twiddles) | eb (DMA staging, 2 rows per wave)
+    __shared__ double s[8 * 288 + 8 * 256 + 8 * 256];
+    const int id = blockIdx.x, x8 = id & 7, rest = id >> 3;
+    const int bb = rest % B, pair = (rest / B) * 8 + x8;
+    constexpr int RB = R / 8;
+    constexpr int LOGN = R == 256 ? 16 : 17;
+    const int tq = pair / RB, rb = pair - tq * RB;
+    if (tq >= nt) return;
+    const int t = t0 + tq;
+    const int pid = t <= l ? t : T.Lp1 + (t - l - 1);
+    const int own = t <= l ? t / K : -1;
+    const int tid = threadIdx.x, L = tid & 31, rl = tid >> 5, lane = tid & 63, w = tid >> 6;
+    const int row = rb * 8 + rl;
+    const double q = (double)T.q[pid], qi = T.qinv[pid];
+    const bool big = q >= kBigPrime;
+    const double* W = T.psif + ((long)pid << LOGN);
+    double* sr = s + rl * 288;
+    double* tw = s + 8 * 288 + rl * 256;
+    double* ebw = s + 8 * 288 + 8 * 256 + w * 512;  // the wave's 2 rows
+    const double* er = ebw + (rl & 1) * 256;         // this lane's row in it
+    const long woff = ((long)t << LOGN) + (long)(rb * 8 + 2 * w) * 256;  // the wave's first row
+    // the first ext digit is requested before anything else: it lands while the prologue works
+    auto next_digit = [&](int j) {
+        for (j++; j < beta && j == own; j++) {
+        }
+        return j;
+    };
+    int jn = next_digit(-1);
+    if (jn < beta) ks_dma_rows(ext + (long)jn * exj + (long)bb * exs + woff, ebw, lane);
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+        const int e = L + 32 * m;
+        if (e > 0) {
+            const int ml = 1 << (31 - __clz(e));
+            tw[e] = W[(long)ml * (R + row) + (e - ml)];
+        }
+    }
+    const long roff = ((long)t << LOGN) + (long)row * 256 + L;
+    double a0[8], a1[8];
+#pragma unroll
+    for (int r = 0; r < 8; r++) a0[r] = a1[r] = 0.0;
+    if (PROD && t <= l) {
+        const double f = pmodf[t], wv = tw_w(f, q);
+        const u64* kp = key + (long)own * kdig + ((long)pid << LOGN) + (long)row * 256 + L;
+        const u64* xa = addend.ptr + (long)(bb & addend.bmask) * addend.bs + roff;
+        const u64* xb = pb.ptr + (long)(bb & pb.bmask) * pb.bs + roff;
+        const u64* xc = pc.ptr ? pc.ptr + (long)(bb & pc.bmask) * pc.bs + roff : xb;
+        if (fac)
+            ks_prod_prologue<true>(a0, a1, kp, kcomp, xa, addend.ps, xb, pb.ps, xc, pc.ps, pc.ptr != nullptr, wv, f,
+                                   (double)fac[3 * t], (double)fac[3 * t + 1], (double)fac[3 * t + 2], q, qi, big);
+        else
+            ks_prod_prologue<false>(a0, a1, kp, kcomp, xa, addend.ps, xb, pb.ps, xc, pc.ps, false, wv, f, 0.0, 0.0, 0.0,
+                                    q, qi, big);
+    } else if (!PROD) {
+        if (pmodf && t <= l && addend.ptr) {
+            const double f = pmodf[t], wv = tw_w(f, q);
+            const u64* xa = addend.ptr + (long)bb * addend.bs + roff;
+            if (addend.np > 0) {
+#pragma unroll
+                for (int r = 0; r < 8; r++) a0[r] = fmul_rem(u2d(xa[32 * r]), wv, f, q);
+            }
+            if (addend.np > 1) {
+#pragma unroll
+                for (int r = 0; r < 8; r++) a1[r] = fmul_rem(u2d(xa[addend.ps + 32 * r]), wv, f, q);
+            }
+        }
+        if (own >= 0 && own < beta) {  // the own digit's limbs: d itself, already in NTT form
+            const u64* kp = key + (long)own * kdig + ((long)pid << LOGN) + (long)row * 256 + L;
+            const u64* dp = d + (long)bb * dbs + roff;
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const double v = u2d(dp[32 * r]), kb = u2d(kp[32 * r]), ka = u2d(kp[32 * r + kcomp]);
+                a0[r] += fmul_rem(v, kb, kb * qi, q);
+                a1[r] += fmul_rem(v, ka, ka * qi, q);
+            }
+        }
+    }
+    if (accum) {
+        const u64* o0 = acc + (long)bb * abs_ + roff;
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            a0[r] = fred(a0[r] + u2d(o0[32 * r]), q, qi);
+            a1[r] = fred(a1[r] + u2d(o0[acs + 32 * r]), q, qi);
+        }
+    } else if (big) {
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            a0[r] = fred(a0[r], q, qi);
+            a1[r] = fred(a1[r], q, qi);
+        }
+    }
+    wave_lds_sync();  // the row's twiddles (written by its own 32 lanes) before use
+    int nsum = 0;
+    const long coff = ((long)t << LOGN) + (long)(rb * 8 + 2 * w) * 256;
+#pragma unroll 1
+    while (jn < beta) {
+        const int j = jn;
+        ks_dma_wait();  // ext_j is in this wave's staging rows
+        double v[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) v[r] = er[L + 32 * r];
+        ks_lds_reads_done();
+        jn = next_digit(j);
+        // the next digit's row (or the FIN epilogue's first conv row) streams in during this NTT
+        if (jn < beta) ks_dma_rows(ext + (long)jn * exj + (long)bb * exs + woff, ebw, lane);
+        else if (FIN) ks_dma_rows(fin.conv + (long)bb * fin.cbs + coff, ebw, lane);
+        const u64* kp = key + (long)j * kdig + ((long)pid << LOGN) + (long)row * 256 + L;
+        u64 kbw[8], kaw[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            kbw[r] = kp[32 * r];
+            kaw[r] = kp[32 * r + kcomp];
+        }
+        row_ntt8_stages(v, sr, L, 1, tw, q, qi, big);
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const double kb = u2d(kbw[r]), ka = u2d(kaw[r]);
+            a0[r] += fmul_rem(v[r], kb, kb * qi, q);
+            a1[r] += fmul_rem(v[r], ka, ka * qi, q);
+        }
+        if (big && (++nsum & 3) == 0) {
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                a0[r] = fred(a0[r], q, qi);
+                a1[r] = fred(a1[r], q, qi);
+            }
+        }
+    }
+    if constexpr (FIN) {
+        const double f = fin.dinvf[t], wv = tw_w(f, q);
+        if (beta == 0 || next_digit(-1) >= beta)  // no ext digit: conv row 0 not requested yet
+            ks_dma_rows(fin.conv + (long)bb * fin.cbs + coff, ebw, lane);
+#pragma unroll 1
+        for (int c = 0; c < 2; c++) {
+            ks_dma_wait();
+            double cv[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) cv[r] = er[L + 32 * r];
+            ks_lds_reads_done();
+            if (c == 0) ks_dma_rows(fin.conv + (long)bb * fin.cbs + fin.cps + coff, ebw, lane);
+            row_ntt8_stages(cv, sr, L, 1, tw, q, qi, big);
+            const u64* ap = fin.add.ptr && c < fin.add.np ? fin.add.ptr + (long)bb * fin.add.bs + (long)c * fin.add.ps + roff
+                                                          : nullptr;
+            u64* op = fin.out + (long)bb * fin.obs + (long)c * fin.ops + roff;
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                double a = c ? a1[r] : a0[r];
+                if (big) a = fred(a, q, qi);
+                double v = fmul_rem(a - cv[r], wv, f, q);
+                if (ap) v += u2d(ap[32 * r]);
+                __builtin_nontemporal_store(fcanon(v, q, qi), &op[32 * r]);
+            }
+        }
+        return;
+    }
+    if constexpr (INV) {
+        const double* IW = T.ipsif + ((long)pid << LOGN);
+#pragma unroll
+        for (int m = 0; m < 8; m++) {
+            const int e = L + 32 * m;
+            if (e > 0) {
+                const int ml = 1 << (31 - __clz(e));
+                tw[e] = IW[(long)ml * (R + row) + (e - ml)];
+            }
+        }
+        wave_lds_sync();
+        u64* o0 = acc + (long)bb * abs_ + roff;
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            double x[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) x[r] = fred(c ? a1[r] : a0[r], q, qi);
+            row_intt8(x, sr, L, tw, q, qi, big);
+#pragma unroll
+            for (int r = 0; r < 8; r++) st_d(&o0[(long)c * acs + 32 * r], x[r]);
+        }
+        return;
+    }
+    u64* o0 = acc + (long)bb * abs_ + roff;
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        __builtin_nontemporal_store(fcanon(a0[r], q, qi), &o0[32 * r]);
+        __builtin_nontemporal_store(fcanon(a1[r], q, qi), &o0[acs + 32 * r]);
     }
 }
 

@@ -472,8 +472,17 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
         ps = eng.pool_stats()
         log(f"aes10: {msg} (pool held {ps['held'] / 1e9:.1f} GB live {ps['live'] / 1e9:.1f} GB "
             f"mallocs {ps['mallocs']} trims {ps['trims']})")
-    warm = R.encrypt_aes128(R.encrypt_blocks(rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8), level=L0),
-                            keys, bs, pairs_per_call=ppc, progress=prog, consume=True)
+    # the warm-up (untimed, same shape, other blocks) also records the decision margin of every
+    # refresh's input: max | |v| / s - 1 | over all slots (s = 2 for a cleaned state, which the
+    # refresh takes at in_scale 2); a bit decodes wrongly past 1 (DESIGN.md 6, round 4's wrong block)
+    refresh_in = []
+
+    def probe(rnd, S, sc):
+        refresh_in.append({"before_round": rnd, "max_abs_dev": round(R.bit_margin(S, sc), 5),
+                           "cleaned": sc != 1.0})
+    warm, _ = R.encrypt_aes128(R.encrypt_blocks(rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8), level=L0),
+                               keys, bs, pairs_per_call=ppc, progress=prog, consume=True, probe=probe)
+    warm_final = R.bit_margin(warm)
     del warm
     blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
     st = R.encrypt_blocks(blocks, level=L0)
@@ -491,6 +500,10 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     timed_mallocs = eng.pool_stats()["mallocs"] - m0
     ok = None
     wrong = None
+    margin = {"final_max_abs_dev": round(R.bit_margin(out), 5), "warmup_final_max_abs_dev": round(warm_final, 5),
+              "refresh_inputs": refresh_in, "worst_refresh_input": max((r["max_abs_dev"] for r in refresh_in), default=None),
+              "note": "max over every slot of | |v| / s - 1 | (a bit flips past 1); final = the timed run's output "
+                      "(decrypted after the clock stopped), refresh inputs from the untimed warm-up of the same shape"}
     if args.check:
         got = R.decrypt_blocks(out, nb)
         want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
@@ -507,7 +520,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
             "blocks_per_gpu": nb * R.n_blk, "refreshes": nref,
             "bootstrap_share": round(tm.get("bootstrap", 0.0) / max(el, 1e-9), 3),
             "bootstrap_ms_per_bit_ct": round(1e3 * tm.get("bootstrap", 0.0) / max(nref * 32 * nb, 1), 2),
-            "bootstrap_setup_s": round(setup_s, 2), "verified": ok, "mismatch": wrong,
+            "bootstrap_setup_s": round(setup_s, 2), "verified": ok, "mismatch": wrong, "margin": margin,
             "bootstrap_cts_groups": [b.cts_groups for b in bs], "round_key_levels": klv,
             "state_level": L0,
             "block_rounds_per_s": round(10 * nb * R.n_blk * world / el, 2),

@@ -118,7 +118,7 @@ int main() {
     if (a.held != 0 || !a.chunks_.empty() || !a.free_addr_.empty() || !a.free_size_.empty())
         return fail("trim left chunks behind", steps);
     if (cnt.allocs != cnt.frees) return fail("allocator calls unbalanced", steps);
-    // growth cap: an arena holding more than 1.2 x its peak live set grows by the request alone
+    // growth cap: an arena holding more than grow_cap x its peak live set grows by the request alone
     {
         Arena b;
         b.A = a.A;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5 A/B on one box: the i8 MFMA layout probe, the GPU suite (or a subset: PYTEST_K), then
-# round-only bench runs alternating the two arms (ARM_A / ARM_B env assignments, default: the
+# round-only bench runs alternating the arms (ARMS="A B C", ARM_<x> = env assignments, default: the
 # VALU base conversions vs the matrix-core ones).  Stops at the first crash or time limit.
 set -o pipefail
 mkdir -p gpurun_out
@@ -18,8 +18,13 @@ if [ -z "$NO_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu ${PYTEST_K:+-k "$PYTEST_K"} --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?
   tail -15 gpurun_out/${TAG}_pytest.log; fatal $rc pytest
 fi
+if [ -n "$EXTRA_TEST_ENV" ]; then  # the parity subset again under another switch (e.g. AESFHE_KS_PIPE=1)
+  env $EXTRA_TEST_ENV timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_aes128_full.py tests/test_bootstrap.py -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest_extra.log 2>&1; rc=$?
+  tail -5 gpurun_out/${TAG}_pytest_extra.log; fatal $rc pytest_extra
+fi
+ARMS=${ARMS:-A B}
 for i in $(seq 1 $REPS); do
-  for arm in A B; do
+  for arm in $ARMS; do
     eval "ARMV=\$ARM_$arm"
     env $ARMV timeout -k 10 600 python -u bench.py $BENCH_ARGS > gpurun_out/${TAG}_${arm}${i}.json 2> gpurun_out/${TAG}_${arm}${i}.err; rc=$?
     fatal $rc "bench $arm$i"
