@@ -36,9 +36,9 @@ struct Arena {
     // growth cap: once the arena holds more than grow_cap x the largest live set seen, a new
     // chunk is sized to its request alone -- fragmentation then grows the arena by what it needs,
     // not by 8 GiB steps (round 3: 211.5 GB held for a 159.4 GB peak in the bench round; round 4
-    // at cap 1.2: 1.29 x).  Round 5: 1.0 -- whole chunks only while the arena holds less than its
-    // largest live set (the first growth of a workload), then exactly the shortfall.  0 disables.
-    double grow_cap = 1.0;
+    // at cap 1.2: 1.29 x; cap 1.0 measured the same, 1.35 x: the excess is fragmentation, which the
+    // engine now keeps down with a second arena for temporaries).  0 disables.
+    double grow_cap = 1.2;
     std::map<char*, size_t> chunks_;                  // base -> size
     std::map<char*, size_t> free_addr_;               // free block -> size (address order)
     std::multimap<size_t, char*> free_size_;          // size -> free block (best fit)

@@ -43,7 +43,7 @@ struct BconvArgs {
     int nt, skip0, skipn, tl_l, Lp1;
     const int8_t* tab;     // [pid][8 planes][128 bytes of K]: signed bytes of H' per (slot, byte)
     const double* corr;    // [pid] 128 sum H' mod p (exact double)
-    const double* w32f;    // [pid] (2^32 mod p) / p
+    const double* pc;      // [pid][4] {p, 1/p, 2^32 mod p, (2^32 mod p) / p} as doubles (epilogue constants)
     const u64* qall;
     const double* qinvall;
     int tiles_per_group;   // target tiles (4 targets) per blockIdx.y
@@ -54,7 +54,7 @@ constexpr int kBconvKT = 128;  // K bytes per table row (up to 4 MFMA steps of 3
 // 32-column groups) into every target of its group.  NSTEP MFMA K-steps of 32 bytes = 4 u64
 // slots: lane half h of step s holds slots 4 s + 2 h, 4 s + 2 h + 1.  VC: slot ns carries v.
 template <int NSTEP, bool VC>
-__global__ __launch_bounds__(256) void k_bconv_mfma(BconvArgs a, int logN) {
+__global__ __launch_bounds__(256, 3) void k_bconv_mfma(BconvArgs a, int logN) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 31, h = lane >> 5;
     const int z = blockIdx.z, zb = z / a.nc, zc = z - zb * a.nc;
@@ -117,75 +117,92 @@ __global__ __launch_bounds__(256) void k_bconv_mfma(BconvArgs a, int logN) {
         }
     }
     // ---- target tiles ------------------------------------------------------------------------
-    // software-pipelined: tile + 1's A fragments and epilogue constants are requested before tile's
-    // epilogue runs (every load branch-free: absent targets read pid 0 and are not stored), so the
-    // L2 round trips of a tile hide behind the previous one's VALU work
+    // Two tiles in flight: tile + 1's MFMAs are issued before tile's epilogue, so the matrix
+    // pipe runs beside the VALU epilogue, and tile + 2's A fragments and constants are requested
+    // before it as well (ping-pong register sets, the loop unrolled by two; every load
+    // branch-free: a target past nt reads pid 0's row, its D rows -- which depend on that A row
+    // only -- are computed and never stored).
     const int row = lane & 31;  // this lane's A row: target 2 ((row >> 2) & 1) + (row >> 4), plane b
     const int ta = 2 * ((row >> 2) & 1) + (row >> 4), pb = 4 * ((row >> 3) & 1) + (row & 3);
-    u64* dst = a.dst + (long)zb * a.dbs + (long)zc * a.dcs;
+    u64* dst = a.dst + (long)zb * a.dbs + (long)zc * a.dcs + kb + c;
     const int tile0 = blockIdx.y * a.tiles_per_group;
     const int ntile = (a.nt + 3) >> 2;
     const int tile1 = min(tile0 + a.tiles_per_group, ntile);
     auto limb_of = [&](int tau) { return tau < a.skip0 ? tau : tau + a.skipn; };
     auto pid_of = [&](int tl) { return tl <= a.tl_l ? tl : a.Lp1 + tl - a.tl_l - 1; };
-    // (a target past nt reads pid 0's row: its D rows are computed and never stored -- a row of D
-    // depends on that row of A only -- so no load result is ever selected or waited for early)
-    bc_v4i af[NSTEP];
-    u64 cq[2];
-    double cqi[2], ccr[2], cf32[2];
-    auto fetch = [&](int tile) {
+    // A fragments of a tile (the epilogue constants are requested after the tile's successor's
+    // MFMAs are issued: their L1 round trip overlaps the matrix pipe)
+    auto fetch = [&](bc_v4i (&af)[NSTEP], int tile) {
         const int tau = 4 * tile + ta;
         const bc_v4i* ap =
             (const bc_v4i*)(a.tab + ((long)(tau < a.nt ? pid_of(limb_of(tau)) : 0) * 8 + pb) * kBconvKT + 16 * h);
 #pragma unroll
         for (int s = 0; s < NSTEP; s++) af[s] = ap[2 * s];  // bytes 32 s + 16 h .. + 15 of the row
-#pragma unroll
-        for (int t2 = 0; t2 < 2; t2++) {
-            const int tt = 4 * tile + 2 * h + t2;
-            const int pid = tt < a.nt ? pid_of(limb_of(tt)) : 0;
-            cq[t2] = a.qall[pid];
-            cqi[t2] = a.qinvall[pid];
-            ccr[t2] = a.corr[pid];
-            cf32[t2] = a.w32f[pid];
-        }
     };
-    if (tile0 < tile1) fetch(tile0);
-#pragma unroll 1
-    for (int tile = tile0; tile < tile1; tile++) {
-        bc_v16i acc[2];
+    auto mma = [&](bc_v16i (&acc)[2], const bc_v4i (&af)[NSTEP]) {
 #pragma unroll
         for (int g = 0; g < 2; g++) {
             acc[g] = bc_v16i{};
 #pragma unroll
             for (int s = 0; s < NSTEP; s++) acc[g] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bf[g][s], acc[g], 0, 0, 0);
         }
-        const u64 q0 = cq[0], q1 = cq[1];
-        const double qi0 = cqi[0], qi1 = cqi[1], cr0 = ccr[0], cr1 = ccr[1], f0 = cf32[0], f1 = cf32[1];
-        if (tile + 1 < tile1) fetch(tile + 1);
-        // epilogue: this lane holds targets 4 tile + 2 h + t2 (t2 = 0, 1), planes b in registers
-        // 4 (2 t2 + (b >> 2)) + (b & 3), of coefficient kb + 32 g + c
+    };
+    // this lane holds targets 4 tile + 2 h + t2 (t2 = 0, 1), plane b of t2 in register
+    // 8 t2 + 4 (b >> 2) + (b & 3), of coefficients kb + 32 g + c
+    auto epilogue = [&](const bc_v16i (&acc)[2], int tile) {
+        double qv[2], qiv[2], crv[2], wv[2], fv[2];
+#pragma unroll
+        for (int t2 = 0; t2 < 2; t2++) {
+            const int tt = 4 * tile + 2 * h + t2;
+            const int pid = tt < a.nt ? pid_of(limb_of(tt)) : 0;
+            const double* pc = a.pc + 4 * pid;
+            qv[t2] = pc[0];
+            qiv[t2] = pc[1];
+            wv[t2] = pc[2];
+            fv[t2] = pc[3];
+            crv[t2] = a.corr[pid];
+        }
 #pragma unroll
         for (int t2 = 0; t2 < 2; t2++) {
             const int tau = 4 * tile + 2 * h + t2;
-            const double q = (double)(t2 ? q1 : q0), qi = t2 ? qi1 : qi0, cr = t2 ? cr1 : cr0, f32 = t2 ? f1 : f0;
-            const double w32 = tw_w(f32, q);
-            u64* op = dst + ((long)limb_of(tau) << logN) + kb + c;
+            const double q = qv[t2], qi = qiv[t2], cr = crv[t2], w32 = wv[t2], f32 = fv[t2];
+            u64* op = dst + ((long)limb_of(tau) << logN);
 #pragma unroll
             for (int g = 0; g < 2; g++) {
                 const int r0 = 8 * t2;
-                // |S_b| <= 128 * 128 * (7 * 16 + 1) < 2^21: every partial sum below is an exact integer
-                double lo = (double)acc[g][r0 + 3];
-                lo = __builtin_fma(lo, 256.0, (double)acc[g][r0 + 2]);
-                lo = __builtin_fma(lo, 256.0, (double)acc[g][r0 + 1]);
-                lo = __builtin_fma(lo, 256.0, (double)acc[g][r0 + 0]);
-                double hi = (double)acc[g][r0 + 7];
-                hi = __builtin_fma(hi, 256.0, (double)acc[g][r0 + 6]);
-                hi = __builtin_fma(hi, 256.0, (double)acc[g][r0 + 5]);
-                hi = __builtin_fma(hi, 256.0, (double)acc[g][r0 + 4]);
-                // |lo|, |hi| < 2^46; (2^32 hi mod p) in (-p, p); + corr < p: below 2^52
+                // |S_b| <= 128 * 128 * (7 * 16 + 1) < 2^21: byte pairs combine exactly in i32
+                // (|S + 256 S'| < 2^30), then |lo|, |hi| < 2^46 in fp64
+                const int p01 = acc[g][r0 + 0] + acc[g][r0 + 1] * 256, p23 = acc[g][r0 + 2] + acc[g][r0 + 3] * 256;
+                const int p45 = acc[g][r0 + 4] + acc[g][r0 + 5] * 256, p67 = acc[g][r0 + 6] + acc[g][r0 + 7] * 256;
+                const double lo = __builtin_fma((double)p23, 65536.0, (double)p01);
+                const double hi = __builtin_fma((double)p67, 65536.0, (double)p45);
+                // (2^32 hi mod p) in (-p, p); + corr < p: below 2^52
                 const double v = lo + fmul_rem(hi, w32, f32, q) + cr;
                 if (tau < a.nt) __builtin_nontemporal_store(fcanon(v, q, qi), &op[32 * g]);  // streaming
             }
+        }
+    };
+    if (tile0 < tile1) {
+        bc_v4i af0[NSTEP], af1[NSTEP];
+        bc_v16i acc0[2], acc1[2];
+        fetch(af0, tile0);
+        mma(acc0, af0);
+        if (tile0 + 1 < tile1) fetch(af1, tile0 + 1);
+#pragma unroll 1
+        for (int tile = tile0; tile < tile1; tile += 2) {
+            // acc0 = tile (issued), af1 = tile + 1 (requested)
+            if (tile + 1 < tile1) {
+                mma(acc1, af1);
+                if (tile + 2 < tile1) fetch(af0, tile + 2);
+            }
+            epilogue(acc0, tile);
+            if (tile + 1 >= tile1) break;
+            // acc1 = tile + 1 (issued), af0 = tile + 2 (requested)
+            if (tile + 2 < tile1) {
+                mma(acc0, af0);
+                if (tile + 3 < tile1) fetch(af1, tile + 3);
+            }
+            epilogue(acc1, tile + 1);
         }
     }
 }

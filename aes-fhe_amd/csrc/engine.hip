@@ -134,7 +134,12 @@ struct aesfhe_engine {
     ChaKey ck;  // ChaCha20 key of every random stream
     Chain chain;
     hipStream_t stream;
-    Pool pool;
+    // two arenas (round 5): `pool` for what outlives a call (ciphertexts, plaintexts, keys),
+    // `tpool` for the per-call temporaries (Tmp: extensions, accumulators, conversions).  In one
+    // arena the short-lived blocks landed between long-lived ones and left holes (round 4: 1.29-1.35x
+    // the peak live set held, 51 GB of fragmentation in the bench round).
+    Pool pool, tpool;
+    size_t peak_total = 0;  // largest pool.live + tpool.live seen
     // device tables
     u64 *q, *psi, *ipsi, *ninv;
     double *qinv, *psif, *ipsif, *ninvf;
@@ -154,7 +159,7 @@ struct aesfhe_engine {
     // matrix-core base conversions (bconv_mfma.h): [set / cell][pid][8 planes][kBconvKT] signed
     // bytes, the XOR-0x80 corrections [set / cell][pid] and (2^32 mod p) / p per prime
     int8_t *bc_mu_tab = nullptr, *bc_md_tab = nullptr, *bc_mdr_tab = nullptr;
-    double *bc_mu_corr = nullptr, *bc_md_corr = nullptr, *bc_mdr_corr = nullptr, *bc_w32f = nullptr;
+    double *bc_mu_corr = nullptr, *bc_md_corr = nullptr, *bc_mdr_corr = nullptr, *bc_pc = nullptr;
     // small-argument upload ring (device) + pinned staging
     char* ring_d = nullptr;
     char* ring_h = nullptr;
@@ -297,14 +302,15 @@ static T* upload_small(aesfhe_engine* e, const T* src, size_t count) {
 // AESFHE_POOL_POISON=1 (diagnostic): every pool block handed out is first filled with 0xA5 bytes on
 // the engine stream, so a read of words nobody wrote is deterministic (and loud) instead of
 // whatever the block held before
-static void* pool_get(aesfhe_engine* e, size_t bytes) {
+static void* pool_get(aesfhe_engine* e, size_t bytes, bool tmp = false) {
     static const bool poison = getenv("AESFHE_POOL_POISON") && atoi(getenv("AESFHE_POOL_POISON"));
-    void* p = e->pool.get(bytes);
+    void* p = (tmp ? e->tpool : e->pool).get(bytes);
+    e->peak_total = std::max(e->peak_total, e->pool.live + e->tpool.live);
     if (poison && p) HIPC(hipMemsetAsync(p, 0xA5, bytes, e->stream));
     return p;
 }
-static u64* dalloc(aesfhe_engine* e, size_t words) { return (u64*)pool_get(e, words * 8); }
-static void dfree(aesfhe_engine* e, u64* p, size_t words) { e->pool.put(p, words * 8); }
+static u64* dalloc(aesfhe_engine* e, size_t words) { return (u64*)pool_get(e, words * 8, true); }
+static void dfree(aesfhe_engine* e, u64* p, size_t words) { e->tpool.put(p, words * 8); }
 
 struct Tmp {  // RAII temporary device buffer from the pool
     aesfhe_engine* e;
@@ -661,7 +667,7 @@ static void build_tables(aesfhe_engine* e) {
     {  // matrix-core ModUp rows: [set][pid] (the digit's own pids are never targets)
         const size_t row = 8 * (size_t)kBconvKT;
         std::vector<int8_t> tab(mu_sets * np * row, 0);
-        std::vector<double> corr(mu_sets * np, 0.0), w32f(np);
+        std::vector<double> corr(mu_sets * np, 0.0), pc(4 * (size_t)np);
         for (int j = 0; j < e->dnum; j++)
             for (int a = 1; a <= A; a++) {
                 const int lo = j * A;
@@ -673,13 +679,16 @@ static void build_tables(aesfhe_engine* e) {
                     corr[set * np + pid] = (double)bconv_row(&tab[(set * np + pid) * row], Q[pid], a, &Q[lo], H.data(), false, 0);
                 }
             }
-        for (int pid = 0; pid < np; pid++) {
-            const u64 p = Q[pid], w = h_mulmod((1ULL << 32) % p, 1, p);
-            w32f[pid] = (double)w / (double)p;
+        for (int pid = 0; pid < np; pid++) {  // {p, 1/p, 2^32 mod p, (2^32 mod p) / p}
+            const u64 p = Q[pid], w = (1ULL << 32) % p;
+            pc[4 * pid] = (double)p;
+            pc[4 * pid + 1] = 1.0 / (double)p;
+            pc[4 * pid + 2] = (double)w;
+            pc[4 * pid + 3] = (double)w / (double)p;
         }
         up(tab, &e->bc_mu_tab);
         up(corr, &e->bc_mu_corr);
-        up(w32f, &e->bc_w32f);
+        up(pc, &e->bc_pc);
     }
 
     // ModDown tables
@@ -858,6 +867,7 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
         const long mb = atol(cm);
         if (mb > 0) e->pool.chunk_bytes = (size_t)mb << 20;
     }
+    e->tpool.chunk_bytes = e->pool.chunk_bytes;
     HIPC(hipMalloc(&e->ring_d, e->ring_size));
     HIPC(hipHostMalloc((void**)&e->ring_h, e->ring_size, hipHostMallocDefault));
     *out = e.release();
@@ -888,13 +898,14 @@ static void engine_teardown(aesfhe_engine* e) {
     }
     for (auto ev : e->spare) hipEventDestroy(ev);
     e->pool.release_all();
+    e->tpool.release_all();
     void* ptrs[] = {e->q, e->psi, e->ipsi, e->ninv, e->qinv, e->psif, e->ipsif, e->ninvf, e->rtwf, e->irtwf,
                     e->mu_hatinv, e->mu_hat, e->md_phatinv, e->md_phat, e->md_pinv, e->rs_inv,
                     e->rs_mod, e->pmod, e->mu_hatinvf, e->mu_hatf, e->md_phatinvf, e->md_phatf,
                     e->md_pinvf, e->rs_invf, e->ring_d, e->tw, e->itw, e->mdr_invf, e->mdr_hatf,
                     e->mdr_dinv, e->mdr_dinvf, e->pmodf, e->mdr_einv, e->mdr_dmodf, e->md_einv,
                     e->bc_mu_tab, e->bc_md_tab, e->bc_mdr_tab, e->bc_mu_corr, e->bc_md_corr, e->bc_mdr_corr,
-                    e->bc_w32f};
+                    e->bc_pc};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto& kv : e->poly2_tabs) hipFree(kv.second);
@@ -980,23 +991,26 @@ extern "C" int aesfhe_engine_profile_kernels(aesfhe_engine* e, char* buf, int64_
     }
     API_END
 }
-extern "C" int64_t aesfhe_engine_device_bytes(const aesfhe_engine* e) { return (int64_t)e->pool.held; }
+extern "C" int64_t aesfhe_engine_device_bytes(const aesfhe_engine* e) { return (int64_t)(e->pool.held + e->tpool.held); }
 extern "C" int aesfhe_engine_pool_trim(aesfhe_engine* e) {
     API_BEGIN
     HIPC(hipSetDevice(e->device));
     HIPC(hipStreamSynchronize(e->stream));
     e->pool.trim();
+    e->tpool.trim();
     API_END
 }
+// both arenas together: held, live, hipMallocs, trims, larger-block reuses, the largest combined
+// live set, fragmentation
 extern "C" int aesfhe_engine_pool_stats(const aesfhe_engine* e, int64_t* out) {
     if (!e || !out) return set_err(AESFHE_EARG, "null argument");
-    out[0] = (int64_t)e->pool.held;
-    out[1] = (int64_t)e->pool.live;
-    out[2] = e->pool.mallocs;
-    out[3] = e->pool.trims;
-    out[4] = e->pool.reuse_larger;
-    out[5] = (int64_t)e->pool.peak_live;
-    out[6] = (int64_t)e->pool.fragmentation();
+    out[0] = (int64_t)(e->pool.held + e->tpool.held);
+    out[1] = (int64_t)(e->pool.live + e->tpool.live);
+    out[2] = e->pool.mallocs + e->tpool.mallocs;
+    out[3] = e->pool.trims + e->tpool.trims;
+    out[4] = e->pool.reuse_larger + e->tpool.reuse_larger;
+    out[5] = (int64_t)e->peak_total;
+    out[6] = (int64_t)(e->pool.fragmentation() + e->tpool.fragmentation());
     return AESFHE_OK;
 }
 
@@ -2052,6 +2066,12 @@ static void launch_bconv(aesfhe_engine* e, BconvArgs a, int nz, int nslots, bool
     HIPC(hipGetLastError());
 }
 
+// AESFHE_BSGS_UNFUSED=1: the lazy-ModDown BSGS map with its babies written (k_ks_inner_multi +
+// k_dot_pt_ext_multi) instead of formed inside the term sums (k_bsgs_terms), for A/B runs
+static bool bsgs_fused_on() {
+    static const bool on = !(getenv("AESFHE_BSGS_UNFUSED") && atoi(getenv("AESFHE_BSGS_UNFUSED")));
+    return on;
+}
 // AESFHE_KS_PIPE=1: the LDS-DMA pipelined key-switch row kernels (ks_fused.h k_nttf_rows_ks_p), A/B
 static bool ks_pipe_on() {
     static const bool on = getenv("AESFHE_KS_PIPE") && atoi(getenv("AESFHE_KS_PIPE"));
@@ -2138,7 +2158,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
                 a.Lp1 = e->Lp1;
                 a.tab = e->bc_mu_tab + set * e->np * 8 * kBconvKT;
                 a.corr = e->bc_mu_corr + set * e->np;
-                a.w32f = e->bc_w32f;
+                a.pc = e->bc_pc;
                 a.qall = e->q;
                 a.qinvall = e->qinv;
                 launch_bconv(e, a, B, alpha, false);
@@ -2259,7 +2279,7 @@ static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int 
             a.Lp1 = e->Lp1;
             a.tab = r ? e->bc_mdr_tab + cell * e->Lp1 * 8 * kBconvKT : e->bc_md_tab;
             a.corr = r ? e->bc_mdr_corr + cell * e->Lp1 : e->bc_md_corr;
-            a.w32f = e->bc_w32f;
+            a.pc = e->bc_pc;
             a.qall = e->q;
             a.qinvall = e->qinv;
             launch_bconv(e, a, B * 2, K + r + 1, true);
@@ -2696,7 +2716,15 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
     std::vector<std::unique_ptr<Tmp>> E;
     bool any_key = false;
     for (int i = 0; i < nb; i++) any_key |= bkeys[i] != nullptr;
-    {
+    // fused (the default): the babies are formed inside the term sums (k_bsgs_terms) from the
+    // extension and the keys, never written; AESFHE_BSGS_UNFUSED=1 keeps the three-kernel form
+    const bool fused_terms = bsgs_fused_on();
+    std::unique_ptr<Tmp> ext_keep;
+    if (fused_terms && any_key) {
+        ext_keep.reset(new Tmp(e, (size_t)ks_beta(e, l) * B * neN));
+        ks_modup(e, c1, cv.bs, B, l, ext_keep->p);
+    }
+    if (!fused_terms) {
         std::unique_ptr<Tmp> ext;
         if (any_key) {
             ext.reset(new Tmp(e, (size_t)ks_beta(e, l) * B * neN));
@@ -2737,7 +2765,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
         std::vector<const u64*> ep(nb);
         std::vector<u64> gal(nb, 0);
         for (int i = 0; i < nb; i++) {
-            ep[i] = E[i]->p;
+            ep[i] = fused_terms ? (bkeys[i] ? (const u64*)bkeys[i]->d : nullptr) : E[i]->p;  // fused: the baby's key
             gal[i] = bkeys[i] ? bkeys[i]->galois : 0;
         }
         auto dep = upload_small(e, ep.data(), ep.size());
@@ -2759,7 +2787,20 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             }
             auto dpt = upload_small(e, pt.data(), pt.size());
             auto dso = upload_small(e, so.data(), so.size());
-            {
+            if (fused_terms) {
+                // bytes: the extension (beta words per (b, t, k), read once; the permuted re-reads of
+                // the other babies hit cache), c0 / c1, the keys (2 beta words per baby, once per
+                // call: shared by the batch) and the plaintexts once, the sums written
+                const int beta = ks_beta(e, l);
+                ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * (beta + 2 + 2.0 * gn) + 2.0 * beta * nb + terms),
+                              "bsgs_terms");
+                const u64* ex = ext_keep ? (const u64*)ext_keep->p : (const u64*)c->d;  // no keyed baby: never read
+                auto kern = beta <= 4 ? k_bsgs_terms<kGM, 4> : beta <= 8 ? k_bsgs_terms<kGM, 8> : k_bsgs_terms<kGM, 12>;
+                hipLaunchKernelGGL(kern, dim3((ne * (N / 256) + 7) / 8 * 8 * B), dim3(256), 0, e->stream, (const u64*)c->d, cv.bs, c1,
+                                   cv.bs, ex, neN, (long)B * neN, (const u64* const*)dep, (const u64*)dgal, 2L * e->np * N,
+                                   (long)e->np * N, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, beta, e->A, e->q,
+                                   e->qinv, (const double*)e->pmodf, e->Lp1, e->logN, B);
+            } else {
                 ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (nb + gn) + terms), "dot_pt_ext_multi");
                 // two (b, c) polynomials per workgroup (four measured the same: 153.7 vs 153.3 ms per
                 // B = 16 bit bootstrap, 162.7 with one)
@@ -2772,6 +2813,7 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
             }
         }
         E.clear();
+        ext_keep.reset();
         // 3. giants: key switches of sigma_j(part_j) summed in Q_{l-1} u P, one ModDown
         const int l2 = l - 1, ne2 = l2 + 1 + K;
         const long ne2N = (long)ne2 * N, l2N = (long)(l2 + 1) * N;

@@ -710,6 +710,9 @@ def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
     per_rank = 4 if drv.layout == "sliced" else 1
     nsets = per_rank * world + (per_rank if world > 1 else 0)
     blocks = np.random.default_rng(77).integers(0, 256, (nsets, drv.n_blk, 16), dtype=np.uint8)
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.reset_peak_memory_stats()
     cts = drv.cts(drv.encrypt(blocks)) if rank == 0 else [None] * (2 if drv.layout == "bytes" else 32)
     cts_batch = nsets if drv.layout != "sliced" else 4 * drv.R.slabs(nsets)
     key = drv.key(rk)
@@ -734,7 +737,13 @@ def scatter_gather_leg(args, eng, drv, rank, world, barrier, allmax):
     ok = None
     if rank == 0 and args.check:
         ok = bool(np.array_equal(drv.decrypt(drv.from_cts(full), nsets), T.aes_round(blocks, rk)))
-    return {"sets": nsets, "granule": gran, "batch_per_rank": [shard_range(cts_batch, world, r, gran)
+    # this rank's device memory during the leg: the engine's pool (ciphertexts; cumulative peak of
+    # the engine) and torch's staging tensors of the collectives (peak over the leg)
+    ps = eng.pool_stats()
+    mem = {"pool_held_gb": round(ps["held"] / 1e9, 2), "pool_live_gb": round(ps["live"] / 1e9, 2),
+           "pool_peak_live_gb": round(ps["peak_live"] / 1e9, 2),
+           "torch_staging_peak_gb": round(torch.cuda.max_memory_allocated() / 1e9, 3) if torch.cuda.is_available() else None}
+    return {"sets": nsets, "granule": gran, "rank_memory": mem, "batch_per_rank": [shard_range(cts_batch, world, r, gran)
                                                                 for r in range(world)],
             "bytes_per_rank_in": bytes_in, "scatter_ms": round(t_sc * 1e3, 2),
             "gather_ms": round(t_ga * 1e3, 2),
