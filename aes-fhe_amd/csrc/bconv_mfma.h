@@ -12,10 +12,9 @@
 // The MFMA takes signed bytes: u XOR 0x80 = u - 128, and the host folds 128 sum_{(i,a)} H' mod p_t
 // into a per-target correction.  A (32 x K, the constants) has the rows (target, byte plane b);
 // B (K x 32) the columns = coefficients, one u64 y per 8 bytes of K (no packing: the u64 IS the
-// operand).  The 32 x 32 i32 result puts, in each lane, the 8 planes of 2 targets of one
-// coefficient (D row r: lane half (r >> 2) & 1, register (r & 3) + 4 (r >> 3)), so the epilogue
-// is per lane: V = sum_b 256^b S_b, out = (lo + (2^32 mod p) hi + corr) mod p, ~28 VALU ops per
-// output against ~78 (tools/mfma_i8_probe.hip pins the operand / result maps).
+// operand).  The 32 x 32 i32 result (D row r: lane half (r >> 2) & 1, register (r & 3) + 4 (r >> 3))
+// holds half of the byte planes of 4 targets per lane; V = sum_b 256^b S_b, out = (lo + (2^32 mod p)
+// hi + corr) mod p (tools/mfma_i8_probe.hip pins the operand / result maps).
 // ModDown's exact conversion: v = rint(sum_j y_j (1/e_j)) (fp64, j in order, as the
 // oracle) rides in one more byte slot of K whose constant column is -D mod q_i.
 #pragma once
@@ -49,6 +48,16 @@ struct BconvArgs {
     int tiles_per_group;   // target tiles (4 targets) per blockIdx.y
 };
 constexpr int kBconvKT = 128;  // K bytes per table row (up to 4 MFMA steps of 32)
+
+// (x, y) -> (x with lanes 32..63 taken from y's lanes 0..31, y with lanes 0..31 taken from x's
+// lanes 32..63): v_permlane32_swap on both dwords of the doubles
+__device__ __forceinline__ void swap_halves(double x, double y, double& xo, double& yo) {
+    const u64 a = (u64)__double_as_longlong(x), b = (u64)__double_as_longlong(y);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)a, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(a >> 32), (unsigned)(b >> 32), false, false);
+    xo = __longlong_as_double((long long)(((u64)(unsigned)hi[0] << 32) | (unsigned)lo[0]));
+    yo = __longlong_as_double((long long)(((u64)(unsigned)hi[1] << 32) | (unsigned)lo[1]));
+}
 
 // grid (N / 256, target groups, batch * nc), 256 threads: each wave converts 64 coefficients (two
 // 32-column groups) into every target of its group.  NSTEP MFMA K-steps of 32 bytes = 4 u64
@@ -117,21 +126,25 @@ __global__ __launch_bounds__(256, 3) void k_bconv_mfma(BconvArgs a, int logN) {
         }
     }
     // ---- target tiles ------------------------------------------------------------------------
-    // Two tiles in flight: tile + 1's MFMAs are issued before tile's epilogue, so the matrix
-    // pipe runs beside the VALU epilogue, and tile + 2's A fragments and constants are requested
-    // before it as well (ping-pong register sets, the loop unrolled by two; every load
-    // branch-free: a target past nt reads pid 0's row, its D rows -- which depend on that A row
-    // only -- are computed and never stored).
-    const int row = lane & 31;  // this lane's A row: target 2 ((row >> 2) & 1) + (row >> 4), plane b
-    const int ta = 2 * ((row >> 2) & 1) + (row >> 4), pb = 4 * ((row >> 3) & 1) + (row & 3);
-    u64* dst = a.dst + (long)zb * a.dbs + (long)zc * a.dcs + kb + c;
+    // A rows: row r = (target r >> 3 of the tile, byte plane (r & 3) + 4 ((r >> 2) & 1)), so that
+    // lane half h holds, in registers 4 m .. 4 m + 3, planes 4 h .. 4 h + 3 of the tile's target m
+    // (all four targets, both column groups).  Each half folds its 4 planes into one exact double
+    // (lo for h = 0, hi for h = 1); one cross-half exchange of 4 doubles then gives half 0 the whole
+    // of column group 0 and half 1 the whole of group 1, so every lane finishes the tile's 4
+    // targets for one coefficient: the targets -- and their constants -- are wave-uniform (scalar
+    // loads), and each store writes 64 consecutive coefficients of one limb (512 B).
+    // Two tiles in flight: tile + 1's MFMAs are issued before tile's epilogue (the matrix pipe
+    // runs beside the VALU epilogue) and tile + 2's A fragments are requested before it (ping-pong
+    // register sets, the loop unrolled by two).  A target past nt reads pid 0's row: its D rows --
+    // which depend on that A row only -- are computed and never stored.
+    const int row = lane & 31;
+    const int ta = row >> 3, pb = (row & 3) + 4 * ((row >> 2) & 1);
+    u64* dst = a.dst + (long)zb * a.dbs + (long)zc * a.dcs + kb + 32 * h + c;
     const int tile0 = blockIdx.y * a.tiles_per_group;
     const int ntile = (a.nt + 3) >> 2;
     const int tile1 = min(tile0 + a.tiles_per_group, ntile);
     auto limb_of = [&](int tau) { return tau < a.skip0 ? tau : tau + a.skipn; };
     auto pid_of = [&](int tl) { return tl <= a.tl_l ? tl : a.Lp1 + tl - a.tl_l - 1; };
-    // A fragments of a tile (the epilogue constants are requested after the tile's successor's
-    // MFMAs are issued: their L1 round trip overlaps the matrix pipe)
     auto fetch = [&](bc_v4i (&af)[NSTEP], int tile) {
         const int tau = 4 * tile + ta;
         const bc_v4i* ap =
@@ -147,39 +160,32 @@ __global__ __launch_bounds__(256, 3) void k_bconv_mfma(BconvArgs a, int logN) {
             for (int s = 0; s < NSTEP; s++) acc[g] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bf[g][s], acc[g], 0, 0, 0);
         }
     };
-    // this lane holds targets 4 tile + 2 h + t2 (t2 = 0, 1), plane b of t2 in register
-    // 8 t2 + 4 (b >> 2) + (b & 3), of coefficients kb + 32 g + c
     auto epilogue = [&](const bc_v16i (&acc)[2], int tile) {
-        double qv[2], qiv[2], crv[2], wv[2], fv[2];
+        // this half's 4 planes of target m, group g: |S| < 2^21, byte pairs exact in i32 (< 2^30),
+        // then |part| < 2^46 in fp64
+        double part[2][4];
 #pragma unroll
-        for (int t2 = 0; t2 < 2; t2++) {
-            const int tt = 4 * tile + 2 * h + t2;
-            const int pid = tt < a.nt ? pid_of(limb_of(tt)) : 0;
-            const double* pc = a.pc + 4 * pid;
-            qv[t2] = pc[0];
-            qiv[t2] = pc[1];
-            wv[t2] = pc[2];
-            fv[t2] = pc[3];
-            crv[t2] = a.corr[pid];
-        }
+        for (int g = 0; g < 2; g++)
 #pragma unroll
-        for (int t2 = 0; t2 < 2; t2++) {
-            const int tau = 4 * tile + 2 * h + t2;
-            const double q = qv[t2], qi = qiv[t2], cr = crv[t2], w32 = wv[t2], f32 = fv[t2];
-            u64* op = dst + ((long)limb_of(tau) << logN);
-#pragma unroll
-            for (int g = 0; g < 2; g++) {
-                const int r0 = 8 * t2;
-                // |S_b| <= 128 * 128 * (7 * 16 + 1) < 2^21: byte pairs combine exactly in i32
-                // (|S + 256 S'| < 2^30), then |lo|, |hi| < 2^46 in fp64
-                const int p01 = acc[g][r0 + 0] + acc[g][r0 + 1] * 256, p23 = acc[g][r0 + 2] + acc[g][r0 + 3] * 256;
-                const int p45 = acc[g][r0 + 4] + acc[g][r0 + 5] * 256, p67 = acc[g][r0 + 6] + acc[g][r0 + 7] * 256;
-                const double lo = __builtin_fma((double)p23, 65536.0, (double)p01);
-                const double hi = __builtin_fma((double)p67, 65536.0, (double)p45);
-                // (2^32 hi mod p) in (-p, p); + corr < p: below 2^52
-                const double v = lo + fmul_rem(hi, w32, f32, q) + cr;
-                if (tau < a.nt) __builtin_nontemporal_store(fcanon(v, q, qi), &op[32 * g]);  // streaming
+            for (int m = 0; m < 4; m++) {
+                const int p01 = acc[g][4 * m] + acc[g][4 * m + 1] * 256, p23 = acc[g][4 * m + 2] + acc[g][4 * m + 3] * 256;
+                part[g][m] = __builtin_fma((double)p23, 65536.0, (double)p01);
             }
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const int tau = 4 * tile + m;  // wave-uniform
+            if (tau >= a.nt) break;
+            // v_permlane32_swap: lanes 32..63 of the first operand <-> lanes 0..31 of the second
+            // (tools/mfma_i8_probe.hip checks it): (part[0], part[1]) become (lo of group h, hi of
+            // group h) in every lane, no select
+            double lo, hi;
+            swap_halves(part[0][m], part[1][m], lo, hi);
+            const int tl = limb_of(tau), pid = pid_of(tl);
+            const double* pc = a.pc + 4 * pid;
+            const double q = pc[0], qi = pc[1], w32 = pc[2], f32 = pc[3], cr = a.corr[pid];
+            // (2^32 hi mod p) in (-p, p); + corr < p: below 2^52
+            const double v = lo + fmul_rem(hi, w32, f32, q) + cr;
+            __builtin_nontemporal_store(fcanon(v, q, qi), dst + ((long)tl << logN));  // streaming
         }
     };
     if (tile0 < tile1) {

@@ -2035,8 +2035,9 @@ static unsigned bconv_groups(int N, int P, int ntarget) {
     return (unsigned)std::max(1L, std::min(g, (long)ntarget));
 }
 
-// Base conversions on the matrix cores (bconv_mfma.h), the default; AESFHE_BCONV_VALU=1 selects the
-// exact-fp64 VALU kernels (k_modup / k_moddown) for A/B runs.  Same residues either way.
+// Base conversions on the matrix cores (bconv_mfma.h), the default (round 5: ModUp 214 -> 190 us,
+// ModDown 453 -> 403 us per call, round +3.2 %, profiles/r05/ab/bconv_mfma/); AESFHE_BCONV_VALU=1
+// selects the exact-fp64 VALU kernels (k_modup / k_moddown) for A/B runs.  Same residues either way.
 static bool bconv_mfma_on() {
     static const bool on = !(getenv("AESFHE_BCONV_VALU") && atoi(getenv("AESFHE_BCONV_VALU")));
     return on;
@@ -2066,15 +2067,20 @@ static void launch_bconv(aesfhe_engine* e, BconvArgs a, int nz, int nslots, bool
     HIPC(hipGetLastError());
 }
 
-// AESFHE_BSGS_UNFUSED=1: the lazy-ModDown BSGS map with its babies written (k_ks_inner_multi +
-// k_dot_pt_ext_multi) instead of formed inside the term sums (k_bsgs_terms), for A/B runs
+// AESFHE_BSGS_FUSED=1: the lazy-ModDown BSGS map with its babies formed inside the term sums
+// (k_bsgs_terms) instead of written (k_ks_inner_multi + k_dot_pt_ext_multi).  Off by default: it
+// measured 3.63 against 3.27 ms per refreshed bit ciphertext (ten rounds 16.3 k vs 17.5 k blocks/s,
+// profiles/r05/ab/bsgs_fused/) -- every batch element re-reads its babies' keys, which the unfused
+// inner product reads once for the whole batch.
 static bool bsgs_fused_on() {
-    static const bool on = !(getenv("AESFHE_BSGS_UNFUSED") && atoi(getenv("AESFHE_BSGS_UNFUSED")));
+    static const bool on = getenv("AESFHE_BSGS_FUSED") && atoi(getenv("AESFHE_BSGS_FUSED"));
     return on;
 }
-// AESFHE_KS_PIPE=1: the LDS-DMA pipelined key-switch row kernels (ks_fused.h k_nttf_rows_ks_p), A/B
+// The LDS-DMA pipelined key-switch row kernels (ks_fused.h k_nttf_rows_ks_p) are the default
+// (round 5: round +1.0 %, A/B/A/B on one box, profiles/r05/ab/ks_pipe/); AESFHE_KS_PIPE=0 selects
+// k_nttf_rows_ks for A/B runs
 static bool ks_pipe_on() {
-    static const bool on = getenv("AESFHE_KS_PIPE") && atoi(getenv("AESFHE_KS_PIPE"));
+    static const bool on = !(getenv("AESFHE_KS_PIPE") && !atoi(getenv("AESFHE_KS_PIPE")));
     return on;
 }
 
@@ -2716,8 +2722,8 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
     std::vector<std::unique_ptr<Tmp>> E;
     bool any_key = false;
     for (int i = 0; i < nb; i++) any_key |= bkeys[i] != nullptr;
-    // fused (the default): the babies are formed inside the term sums (k_bsgs_terms) from the
-    // extension and the keys, never written; AESFHE_BSGS_UNFUSED=1 keeps the three-kernel form
+    // fused (AESFHE_BSGS_FUSED=1, bsgs_fused_on): the babies are formed inside the term sums
+    // (k_bsgs_terms) from the extension and the keys, never written
     const bool fused_terms = bsgs_fused_on();
     std::unique_ptr<Tmp> ext_keep;
     if (fused_terms && any_key) {

@@ -33,6 +33,15 @@ __global__ void k_probe(const int8_t* A, const int8_t* B, int* D) {
     for (int r = 0; r < 16; r++) D[l * 16 + r] = c[r];
 }
 
+// v_permlane32_swap semantics used by bconv_mfma.h swap_halves: (x, y) -> (x with lanes 32..63
+// from y's lanes 0..31, y with lanes 0..31 from x's lanes 32..63)
+__global__ void k_swap(unsigned* out) {
+    const unsigned l = threadIdx.x;
+    const auto r = __builtin_amdgcn_permlane32_swap(1000u + l, 2000u + l, false, false);
+    out[l] = r[0];
+    out[64 + l] = r[1];
+}
+
 __global__ void k_rate(int iters, int* out) {
     v4i a = {(int)threadIdx.x, 1, 2, 3}, b = {3, 2, 1, (int)threadIdx.x};
     v16i c0 = {}, c1 = {}, c2 = {}, c3 = {};
@@ -78,6 +87,21 @@ int main() {
             if (D[lane * 16 + reg] != want) bad++;
         }
     printf("mfma_i32_32x32x32_i8 layout hypothesis: %s (%d of 1024 wrong)\n", bad ? "WRONG" : "confirmed", bad);
+    {
+        unsigned* dS;
+        hipMalloc(&dS, 128 * 4);
+        hipLaunchKernelGGL(k_swap, dim3(1), dim3(64), 0, 0, dS);
+        std::vector<unsigned> S(128);
+        hipMemcpy(S.data(), dS, 128 * 4, hipMemcpyDeviceToHost);
+        int sb = 0;
+        for (unsigned l = 0; l < 64; l++) {
+            const unsigned want0 = l < 32 ? 1000 + l : 2000 + (l - 32), want1 = l < 32 ? 1000 + l + 32 : 2000 + l;
+            sb += (S[l] != want0) + (S[64 + l] != want1);
+        }
+        printf("permlane32_swap (x, y) -> (x[0..31] | y[0..31], x[32..63] | y[32..63]): %s (%d wrong; lane 0/32: %u %u / %u %u)\n",
+               sb ? "WRONG" : "confirmed", sb, S[0], S[32], S[64], S[96]);
+        bad += sb;
+    }
     // rate: 1 wave per SIMD on every CU, 4 independent accumulators
     int* dO;
     const int blocks = 256 * 4, iters = 4096;
