@@ -2067,13 +2067,15 @@ static void launch_bconv(aesfhe_engine* e, BconvArgs a, int nz, int nslots, bool
     HIPC(hipGetLastError());
 }
 
-// AESFHE_BSGS_FUSED=1: the lazy-ModDown BSGS map with its babies formed inside the term sums
-// (k_bsgs_terms) instead of written (k_ks_inner_multi + k_dot_pt_ext_multi).  Off by default: it
-// measured 3.63 against 3.27 ms per refreshed bit ciphertext (ten rounds 16.3 k vs 17.5 k blocks/s,
-// profiles/r05/ab/bsgs_fused/) -- every batch element re-reads its babies' keys, which the unfused
-// inner product reads once for the whole batch.
+// The lazy-ModDown BSGS map with its babies formed inside the term sums (k_bsgs_terms) instead
+// of written (k_ks_inner_multi + k_dot_pt_ext_multi) is the default; AESFHE_BSGS_FUSED=0 selects
+// the unfused pair for A/B runs.  Its first form (one batch element per thread, every element
+// re-reading its babies' keys) lost: 3.63 against 3.27 ms per refreshed bit ciphertext.  With
+// the key and plaintext words of each baby serving BB = 2..4 elements per thread it gains:
+// 3.15 against 3.23 ms, ten rounds 17.99 k / 17.89 k against 17.63 k / 17.66 k blocks/s
+// (A/B/A/B on one box, profiles/r05/ab/bsgs_fused/).
 static bool bsgs_fused_on() {
-    static const bool on = getenv("AESFHE_BSGS_FUSED") && atoi(getenv("AESFHE_BSGS_FUSED"));
+    static const bool on = !(getenv("AESFHE_BSGS_FUSED") && !atoi(getenv("AESFHE_BSGS_FUSED")));
     return on;
 }
 // The LDS-DMA pipelined key-switch row kernels (ks_fused.h k_nttf_rows_ks_p) are the default
@@ -2801,8 +2803,13 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
                 ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * (beta + 2 + 2.0 * gn) + 2.0 * beta * nb + terms),
                               "bsgs_terms");
                 const u64* ex = ext_keep ? (const u64*)ext_keep->p : (const u64*)c->d;  // no keyed baby: never read
-                auto kern = beta <= 4 ? k_bsgs_terms<kGM, 4> : beta <= 8 ? k_bsgs_terms<kGM, 8> : k_bsgs_terms<kGM, 12>;
-                hipLaunchKernelGGL(kern, dim3((ne * (N / 256) + 7) / 8 * 8 * B), dim3(256), 0, e->stream, (const u64*)c->d, cv.bs, c1,
+                // accumulator pairs GM >= gn and batch block BB: registers 2 BB GM doubles
+                // (beta > 4 only above the bootstrap's levels: one element per thread there)
+                auto kern = gn <= 2 ? (beta <= 4 ? k_bsgs_terms<2, 4, 4> : k_bsgs_terms<2, 12, 1>)
+                          : gn <= 4 ? (beta <= 4 ? k_bsgs_terms<4, 4, 4> : k_bsgs_terms<4, 12, 1>)
+                                    : (beta <= 4 ? k_bsgs_terms<8, 4, 2> : k_bsgs_terms<8, 12, 1>);
+                const int BBv = beta > 4 ? 1 : gn <= 4 ? 4 : 2;
+                hipLaunchKernelGGL(kern, dim3((ne * (N / 256) + 7) / 8 * 8 * ((B + BBv - 1) / BBv)), dim3(256), 0, e->stream, (const u64*)c->d, cv.bs, c1,
                                    cv.bs, ex, neN, (long)B * neN, (const u64* const*)dep, (const u64*)dgal, 2L * e->np * N,
                                    (long)e->np * N, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, beta, e->A, e->q,
                                    e->qinv, (const double*)e->pmodf, e->Lp1, e->logN, B);

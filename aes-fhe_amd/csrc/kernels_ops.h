@@ -1289,17 +1289,20 @@ __global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64*
 // and plaintexts are shared by the batch through L2 (the XCD-local grid of k_dot_pt_ext_multi).
 // grid: 1-D, (pair = (limb t, 256-slot k-block)) x B, block id -> (x = id & 7, w = id >> 3):
 // pair = (w / B) * 8 + x, b = w % B.  GM >= ng accumulator pairs in registers; BM >= beta.
-template <int GM, int BM>
-__global__ void k_bsgs_terms(const u64* __restrict__ c0p, long c0bs, const u64* __restrict__ c1p, long c1bs,
+template <int GM, int BM, int BB>
+__global__ __launch_bounds__(256) void k_bsgs_terms(const u64* __restrict__ c0p, long c0bs, const u64* __restrict__ c1p, long c1bs,
                              const u64* __restrict__ ext, long exs, long exj,
                              const u64* const* __restrict__ keys, const u64* __restrict__ gal, long kdig, long kcomp,
                              const u64* const* __restrict__ pt, int nb, int ng, u64* const* __restrict__ outs,
                              int l, int ne, int beta, int A, const u64* __restrict__ qall,
                              const double* __restrict__ qinvall, const double* __restrict__ pmodf, int Lp1, int logN,
                              int B) {
-    const int kbits = logN - 8;
+    // BB batch elements per thread: every key and plaintext word loaded serves BB of them (the
+    // first form, one element per thread, re-read each baby's 2 beta key words per element from
+    // L2 and lost to the unfused kernels)
+    const int kbits = logN - 8, nbb = (B + BB - 1) / BB;
     const int x8 = blockIdx.x & 7, w = blockIdx.x >> 3;
-    const int pair = (w / B) * 8 + x8, b = w % B;
+    const int pair = (w / nbb) * 8 + x8, b0 = (w % nbb) * BB;
     if (pair >= (ne << kbits)) return;
     const int t = pair >> kbits, k = ((pair & ((1 << kbits) - 1)) << 8) + threadIdx.x;
     const int pid = ext_pid(t, l, Lp1);
@@ -1308,80 +1311,106 @@ __global__ void k_bsgs_terms(const u64* __restrict__ c0p, long c0bs, const u64* 
     const double q = (double)qall[pid], qi = qinvall[pid];
     const double pf = isq ? pmodf[t] : 0.0, pw = isq ? tw_w(pf, q) : 0.0;
     const long po = ((long)t << logN) + k;
-    const u64* c0r = c0p + (long)b * c0bs + ((long)t << logN);  // this limb's rows (Q limbs only)
-    const u64* c1r = c1p + (long)b * c1bs + ((long)t << logN);
-    const u64* er = ext + (long)b * exs + ((long)t << logN);
     const u64 M = 2ULL << logN;
     const u64 ek = 2 * (u64)(__brev((unsigned)k) >> (32 - logN)) + 1;
-    double acc0[GM], acc1[GM];
+    const u64* c0r[BB];
+    const u64* c1r[BB];
+    const u64* er[BB];
 #pragma unroll
-    for (int j = 0; j < GM; j++) acc0[j] = acc1[j] = 0.0;
+    for (int u = 0; u < BB; u++) {  // elements past B alias the last one (computed, not stored)
+        const int b = min(b0 + u, B - 1);
+        c0r[u] = c0p + (long)b * c0bs + ((long)t << logN);
+        c1r[u] = c1p + (long)b * c1bs + ((long)t << logN);
+        er[u] = ext + (long)b * exs + ((long)t << logN);
+    }
+    double acc0[BB][GM], acc1[BB][GM];
+#pragma unroll
+    for (int u = 0; u < BB; u++)
+#pragma unroll
+        for (int j = 0; j < GM; j++) acc0[u][j] = acc1[u][j] = 0.0;
     for (int i = 0; i < nb; i++) {
         const u64 g = gal[i];
         long src = k;
         if (g > 1) src = __brev((unsigned)((((g * ek) & (M - 1)) - 1) >> 1)) >> (32 - logN);
         const u64* kp = keys[i];
-        double e0, e1;
-        if (!kp) {  // identity baby: (P c0, P c1) on the Q limbs
-            e0 = isq ? fmul_rem(u2d(c0r[src]), pw, pf, q) : 0.0;
-            e1 = isq ? fmul_rem(u2d(c1r[src]), pw, pf, q) : 0.0;
-        } else {
-            double x[BM], kb[BM], ka[BM];
-#pragma unroll
-            for (int d = 0; d < BM; d++) {  // every word requested before the first product
-                if (d < beta) {
-                    const u64* xp = d == own ? c1r + src : er + (long)d * exj + src;
-                    const u64* kk = kp + (long)d * kdig + ((long)pid << logN) + src;
-                    x[d] = u2d(*xp);
-                    kb[d] = u2d(kk[0]);
-                    ka[d] = u2d(kk[kcomp]);
-                }
-            }
-            e0 = isq ? fmul_rem(u2d(c0r[src]), pw, pf, q) : 0.0;
-            e1 = 0.0;
-#pragma unroll
-            for (int d = 0; d < BM; d++) {
-                if (d < beta) {
-                    e0 += fmul_rem(x[d], kb[d], kb[d] * qi, q);
-                    e1 += fmul_rem(x[d], ka[d], ka[d] * qi, q);
-                    if ((d & 3) == 3) {
-                        e0 = fred(e0, q, qi);
-                        e1 = fred(e1, q, qi);
-                    }
-                }
-            }
-        }
-        e0 = fred(e0, q, qi);  // |e| <= q/2 + 1: fmul_rem's input bound for every prime size
-        e1 = fred(e1, q, qi);
         const u64* pj[GM];
         double wv[GM];
 #pragma unroll
         for (int j = 0; j < GM; j++) pj[j] = j < ng ? pt[j * nb + i] : nullptr;
 #pragma unroll
         for (int j = 0; j < GM; j++) wv[j] = pj[j] ? u2d(pj[j][po]) : 0.0;
+        double e0[BB], e1[BB];
+        if (!kp) {  // identity baby: (P c0, P c1) on the Q limbs
 #pragma unroll
-        for (int j = 0; j < GM; j++) {
-            if (pj[j]) {
-                const double wq = wv[j] * qi;
-                acc0[j] += fmul_rem(e0, wv[j], wq, q);
-                acc1[j] += fmul_rem(e1, wv[j], wq, q);
+            for (int u = 0; u < BB; u++) {
+                e0[u] = isq ? fmul_rem(u2d(c0r[u][src]), pw, pf, q) : 0.0;
+                e1[u] = isq ? fmul_rem(u2d(c1r[u][src]), pw, pf, q) : 0.0;
+            }
+        } else {
+            double kb[BM], ka[BM];
+#pragma unroll
+            for (int d = 0; d < BM; d++) {  // the baby's key words: once for the BB elements
+                if (d < beta) {
+                    const u64* kk = kp + (long)d * kdig + ((long)pid << logN) + src;
+                    kb[d] = u2d(kk[0]);
+                    ka[d] = u2d(kk[kcomp]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < BB; u++) {
+                double x[BM];
+#pragma unroll
+                for (int d = 0; d < BM; d++)
+                    if (d < beta) x[d] = u2d(d == own ? c1r[u][src] : er[u][(long)d * exj + src]);
+                double a0 = isq ? fmul_rem(u2d(c0r[u][src]), pw, pf, q) : 0.0, a1 = 0.0;
+#pragma unroll
+                for (int d = 0; d < BM; d++) {
+                    if (d < beta) {
+                        a0 += fmul_rem(x[d], kb[d], kb[d] * qi, q);
+                        a1 += fmul_rem(x[d], ka[d], ka[d] * qi, q);
+                        if ((d & 3) == 3) {
+                            a0 = fred(a0, q, qi);
+                            a1 = fred(a1, q, qi);
+                        }
+                    }
+                }
+                e0[u] = a0;
+                e1[u] = a1;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < BB; u++) {
+            const double f0 = fred(e0[u], q, qi), f1 = fred(e1[u], q, qi);  // |e| <= q/2 + 1
+#pragma unroll
+            for (int j = 0; j < GM; j++) {
+                if (pj[j]) {
+                    const double wq = wv[j] * qi;
+                    acc0[u][j] += fmul_rem(f0, wv[j], wq, q);
+                    acc1[u][j] += fmul_rem(f1, wv[j], wq, q);
+                }
             }
         }
         if ((i & 3) == 3) {
 #pragma unroll
-            for (int j = 0; j < GM; j++) {
-                acc0[j] = fred(acc0[j], q, qi);
-                acc1[j] = fred(acc1[j], q, qi);
-            }
+            for (int u = 0; u < BB; u++)
+#pragma unroll
+                for (int j = 0; j < GM; j++) {
+                    acc0[u][j] = fred(acc0[u][j], q, qi);
+                    acc1[u][j] = fred(acc1[u][j], q, qi);
+                }
         }
     }
 #pragma unroll
-    for (int j = 0; j < GM; j++)
-        if (j < ng) {
-            u64* o = outs[j] + (((long)(2 * b) * ne + t) << logN) + k;
-            o[0] = fcanon(acc0[j], q, qi);
-            o[(long)ne << logN] = fcanon(acc1[j], q, qi);
-        }
+    for (int u = 0; u < BB; u++) {
+        if (b0 + u >= B) break;
+#pragma unroll
+        for (int j = 0; j < GM; j++)
+            if (j < ng) {
+                u64* o = outs[j] + (((long)(2 * (b0 + u)) * ne + t) << logN) + k;
+                o[0] = fcanon(acc0[u][j], q, qi);
+                o[(long)ne << logN] = fcanon(acc1[u][j], q, qi);
+            }
+    }
 }
 
 }  // namespace aesfhe

@@ -15,6 +15,11 @@ if [ -n "$TESTS" ]; then
   tail -6 gpurun_out/${TAG}_pytest.log; fatal $rc pytest
   [ $rc -ne 0 ] && [ -n "$STOP_ON_FAIL" ] && exit 1
 fi
+if [ -n "$EXTRA_TESTS" ]; then  # the same selection again under an opt-in env (EXTRA_TEST_ENV)
+  env $EXTRA_TEST_ENV timeout -k 10 900 python -u -m pytest $EXTRA_TESTS -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest_extra.log 2>&1; rc=$?
+  tail -6 gpurun_out/${TAG}_pytest_extra.log; fatal $rc pytest_extra
+  [ $rc -ne 0 ] && [ -n "$STOP_ON_FAIL" ] && exit 1
+fi
 ROUND="--steps 5 --warmup 1 --no-configs --no-harness --client-batch 0 --aes10-batch 0 --no-cpu-baseline --config5 off"
 AES10="--steps 1 --warmup 0 --profile-steps 0 --no-configs --no-harness --client-batch 0 --no-cpu-baseline --config5 off"
 while IFS='|' read -r name envs args; do
