@@ -2074,6 +2074,45 @@ static void launch_bconv(aesfhe_engine* e, BconvArgs a, int nz, int nslots, bool
 // the key and plaintext words of each baby serving BB = 2..4 elements per thread it gains:
 // 3.15 against 3.23 ms, ten rounds 17.99 k / 17.89 k against 17.63 k / 17.66 k blocks/s
 // (A/B/A/B on one box, profiles/r05/ab/bsgs_fused/).
+// The order k_bsgs_terms walks the 256-slot k-blocks of a limb in: along the orbits of pi, the
+// block map of the first keyed baby's Galois element g (slot k = 256 kb + j reads slot
+// sigma_g(k) = brv(((g (2 brv(k) + 1)) mod 2N - 1) / 2), whose block depends on kb alone), when
+// every keyed baby i is g^i (the BSGS babies: rotations by i x stride); otherwise 0, 1, 2, ...
+// Either order is a permutation of the blocks, so results do not depend on it.
+static std::vector<unsigned short> bsgs_block_order(int logN, const std::vector<u64>& gal) {
+    const int nblk = logN >= 8 ? 1 << (logN - 8) : 1;
+    const u64 M = 2ULL << logN;
+    std::vector<unsigned short> ord(nblk);
+    for (int i = 0; i < nblk; i++) ord[i] = (unsigned short)i;
+    u64 g1 = 0;
+    int i1 = -1;
+    for (int i = 0; i < (int)gal.size(); i++)
+        if (gal[i] > 1) {
+            g1 = gal[i], i1 = i;
+            break;
+        }
+    if (!g1) return ord;
+    u64 gp = 1;  // keyed babies must be g1^(i - i1 + 1), identity babies anywhere
+    for (int i = i1; i < (int)gal.size(); i++) {
+        gp = (gp * g1) & (M - 1);
+        if (gal[i] != 0 && gal[i] != gp) return ord;
+    }
+    auto brv = [&](u64 x) { return (u64)(__builtin_bitreverse32((unsigned)x) >> (32 - logN)); };
+    auto pi = [&](int kb) {
+        const u64 k = (u64)kb << 8, ek = 2 * brv(k) + 1;
+        return (int)(brv((((g1 * ek) & (M - 1)) - 1) >> 1) >> 8);
+    };
+    std::vector<char> seen(nblk, 0);
+    int n = 0;
+    for (int s = 0; s < nblk; s++)
+        for (int kb = s; !seen[kb]; kb = pi(kb)) {
+            seen[kb] = 1;
+            ord[n++] = (unsigned short)kb;
+        }
+    if (n != nblk) throw_err(AESFHE_EUNSUPPORTED, "bsgs block order is not a permutation");
+    return ord;
+}
+
 static bool bsgs_fused_on() {
     static const bool on = !(getenv("AESFHE_BSGS_FUSED") && !atoi(getenv("AESFHE_BSGS_FUSED")));
     return on;
@@ -2726,7 +2765,9 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
     for (int i = 0; i < nb; i++) any_key |= bkeys[i] != nullptr;
     // fused (AESFHE_BSGS_FUSED=1, bsgs_fused_on): the babies are formed inside the term sums
     // (k_bsgs_terms) from the extension and the keys, never written
-    const bool fused_terms = bsgs_fused_on();
+    bool only_first_keyless = true;  // k_bsgs_terms peels a key-less (identity) baby at index 0 only
+    for (int i = 1; i < nb; i++) only_first_keyless &= bkeys[i] != nullptr;
+    const bool fused_terms = bsgs_fused_on() && only_first_keyless;
     std::unique_ptr<Tmp> ext_keep;
     if (fused_terms && any_key) {
         ext_keep.reset(new Tmp(e, (size_t)ks_beta(e, l) * B * neN));
@@ -2778,6 +2819,8 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
         }
         auto dep = upload_small(e, ep.data(), ep.size());
         auto dgal = upload_small(e, gal.data(), gal.size());
+        const std::vector<unsigned short> kord = bsgs_block_order(e->logN, gal);
+        auto dkord = upload_small(e, kord.data(), kord.size());
         for (int j0 = 0; j0 < ng; j0 += kGM) {
             const int gn = std::min(kGM, ng - j0);
             std::vector<const u64*> pt((size_t)gn * nb, nullptr);
@@ -2803,16 +2846,23 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
                 ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * (beta + 2 + 2.0 * gn) + 2.0 * beta * nb + terms),
                               "bsgs_terms");
                 const u64* ex = ext_keep ? (const u64*)ext_keep->p : (const u64*)c->d;  // no keyed baby: never read
-                // accumulator pairs GM >= gn and batch block BB: registers 2 BB GM doubles
-                // (beta > 4 only above the bootstrap's levels: one element per thread there)
-                auto kern = gn <= 2 ? (beta <= 4 ? k_bsgs_terms<2, 4, 4> : k_bsgs_terms<2, 12, 1>)
-                          : gn <= 4 ? (beta <= 4 ? k_bsgs_terms<4, 4, 4> : k_bsgs_terms<4, 12, 1>)
-                                    : (beta <= 4 ? k_bsgs_terms<8, 4, 2> : k_bsgs_terms<8, 12, 1>);
+                // accumulator pairs GM >= gn, digit words BM = beta exactly, batch block BB (registers
+                // 2 BB GM doubles), PB babies' loads in flight together: tools/bsgs_bench.hip timed
+                // <2, 3, 4, 2> at 3.07 ms against 3.75 (PB 1), 3.32 (BB 8), 4.00 (PB 3); <4, 3, 4, 2>
+                // 4.95 ms against 5.08 (PB 1).  beta > 4 only above the bootstrap's levels.
+                using KF = decltype(&k_bsgs_terms<2, 2, 4, 2>);
+                auto pick = [&](auto gm) -> KF {
+                    constexpr int G = decltype(gm)::value, BBc = G <= 4 ? 4 : 2, PBc = G <= 4 ? 2 : 1;
+                    return beta <= 2 ? k_bsgs_terms<G, 2, BBc, PBc> : beta == 3 ? k_bsgs_terms<G, 3, BBc, PBc>
+                         : beta == 4 ? k_bsgs_terms<G, 4, BBc, PBc> : k_bsgs_terms<G, 12, 1, 1>;
+                };
+                KF kern = gn <= 2 ? pick(std::integral_constant<int, 2>{}) : gn <= 4 ? pick(std::integral_constant<int, 4>{})
+                                  : pick(std::integral_constant<int, 8>{});
                 const int BBv = beta > 4 ? 1 : gn <= 4 ? 4 : 2;
                 hipLaunchKernelGGL(kern, dim3((ne * (N / 256) + 7) / 8 * 8 * ((B + BBv - 1) / BBv)), dim3(256), 0, e->stream, (const u64*)c->d, cv.bs, c1,
                                    cv.bs, ex, neN, (long)B * neN, (const u64* const*)dep, (const u64*)dgal, 2L * e->np * N,
                                    (long)e->np * N, (const u64* const*)dpt, nb, gn, (u64* const*)dso, l, ne, beta, e->A, e->q,
-                                   e->qinv, (const double*)e->pmodf, e->Lp1, e->logN, B);
+                                   e->qinv, (const double*)e->pmodf, e->Lp1, e->logN, B, (const unsigned short*)dkord);
             } else {
                 ProfScope ps_(e, FAM_EW, 8.0 * N * ne * ((double)B * 2 * (nb + gn) + terms), "dot_pt_ext_multi");
                 // two (b, c) polynomials per workgroup (four measured the same: 153.7 vs 153.3 ms per

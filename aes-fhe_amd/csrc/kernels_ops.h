@@ -1287,24 +1287,42 @@ __global__ void k_dot_pt_ext_multi(const u64* const* __restrict__ ep, const u64*
 // from ~4 nb + beta ceil(nk / KC) to the beta extension words (their permuted re-reads for the
 // other babies hit the 2 KB row already cached) and the sums written.  Keys (2 beta words per baby)
 // and plaintexts are shared by the batch through L2 (the XCD-local grid of k_dot_pt_ext_multi).
-// grid: 1-D, (pair = (limb t, 256-slot k-block)) x B, block id -> (x = id & 7, w = id >> 3):
-// pair = (w / B) * 8 + x, b = w % B.  GM >= ng accumulator pairs in registers; BM >= beta.
-template <int GM, int BM, int BB>
-__global__ __launch_bounds__(256) void k_bsgs_terms(const u64* __restrict__ c0p, long c0bs, const u64* __restrict__ c1p, long c1bs,
+// The 256-slot k-blocks are walked in the order kord (host, bsgs_block_order): a block's slots
+// all read ONE source block per baby (sigma_g maps the top 8 bits of k by the top 8 bits alone),
+// and with babies g_i = g_1^i the blocks block k reads are the orbit window pi^i(kb), i < nb, of
+// the block map pi of g_1 -- so walking kb along pi's orbits, each XCD taking one contiguous
+// eighth of the walk, gives consecutive workgroups nb - 1 of nb source blocks in common (ext, c0,
+// c1 and keys reused from the XCD's L2).  Identity order when the babies are not powers of one
+// element.  grid: 1-D, block id -> (x = id & 7, w = id >> 3): r = w / ceil(B / BB) runs over
+// (limb t, position in x's eighth of the walk), batch block w % ceil(B / BB) fastest (the keys
+// of one k-block shared by the whole batch from L2).  GM >= ng accumulator pairs; BM >= beta.
+// PB: babies whose loads are issued together; OCC: launch-bounds wave target (tools/bsgs_bench.hip)
+template <int GM, int BM, int BB, int PB = 1, int OCC = 1>
+__global__ __launch_bounds__(256, OCC) void k_bsgs_terms(const u64* __restrict__ c0p, long c0bs, const u64* __restrict__ c1p, long c1bs,
                              const u64* __restrict__ ext, long exs, long exj,
                              const u64* const* __restrict__ keys, const u64* __restrict__ gal, long kdig, long kcomp,
                              const u64* const* __restrict__ pt, int nb, int ng, u64* const* __restrict__ outs,
                              int l, int ne, int beta, int A, const u64* __restrict__ qall,
                              const double* __restrict__ qinvall, const double* __restrict__ pmodf, int Lp1, int logN,
-                             int B) {
+                             int B, const unsigned short* __restrict__ kord) {
     // BB batch elements per thread: every key and plaintext word loaded serves BB of them (the
     // first form, one element per thread, re-read each baby's 2 beta key words per element from
     // L2 and lost to the unfused kernels)
-    const int kbits = logN - 8, nbb = (B + BB - 1) / BB;
+    const int nblk = 1 << (logN - 8), nbb = (B + BB - 1) / BB;
     const int x8 = blockIdx.x & 7, w = blockIdx.x >> 3;
-    const int pair = (w / nbb) * 8 + x8, b0 = (w % nbb) * BB;
-    if (pair >= (ne << kbits)) return;
-    const int t = pair >> kbits, k = ((pair & ((1 << kbits) - 1)) << 8) + threadIdx.x;
+    const int r = w / nbb, b0 = (w % nbb) * BB;
+    int t, m;
+    if (nblk >= 8) {  // XCD x8 walks positions [x8 seg, x8 seg + seg) of every limb
+        const int seg = nblk >> 3;
+        t = r / seg;
+        m = x8 * seg + r - t * seg;
+    } else {  // fewer blocks than XCDs (N < 2^11): positions dealt round robin
+        const int pos = r * 8 + x8;
+        t = pos / nblk;
+        m = pos - t * nblk;
+    }
+    if (t >= ne) return;
+    const int k = ((int)kord[m] << 8) + threadIdx.x;
     const int pid = ext_pid(t, l, Lp1);
     const bool isq = t <= l;
     const int own = isq ? t / A : -1;
@@ -1328,46 +1346,75 @@ __global__ __launch_bounds__(256) void k_bsgs_terms(const u64* __restrict__ c0p,
     for (int u = 0; u < BB; u++)
 #pragma unroll
         for (int j = 0; j < GM; j++) acc0[u][j] = acc1[u][j] = 0.0;
-    for (int i = 0; i < nb; i++) {
-        const u64 g = gal[i];
-        long src = k;
-        if (g > 1) src = __brev((unsigned)((((g * ek) & (M - 1)) - 1) >> 1)) >> (32 - logN);
-        const u64* kp = keys[i];
-        const u64* pj[GM];
-        double wv[GM];
+    // absent plaintexts (a giant without a term on this baby) read the zero word: w = 0 adds 0
+    auto pt_word = [&](int j, int i) {
+        const u64* pp = j < ng ? pt[j * nb + i] : nullptr;
+        return u2d(*(pp ? pp + po : &kZeroWord));
+    };
+    auto add_terms = [&](const double (&e0)[BB], const double (&e1)[BB], const double (&wv)[GM]) {
 #pragma unroll
-        for (int j = 0; j < GM; j++) pj[j] = j < ng ? pt[j * nb + i] : nullptr;
+        for (int u = 0; u < BB; u++) {
+            const double f0 = fred(e0[u], q, qi), f1 = fred(e1[u], q, qi);  // |e| <= q/2 + 1
 #pragma unroll
-        for (int j = 0; j < GM; j++) wv[j] = pj[j] ? u2d(pj[j][po]) : 0.0;
-        double e0[BB], e1[BB];
-        if (!kp) {  // identity baby: (P c0, P c1) on the Q limbs
-#pragma unroll
-            for (int u = 0; u < BB; u++) {
-                e0[u] = isq ? fmul_rem(u2d(c0r[u][src]), pw, pf, q) : 0.0;
-                e1[u] = isq ? fmul_rem(u2d(c1r[u][src]), pw, pf, q) : 0.0;
+            for (int j = 0; j < GM; j++) {
+                const double wq = wv[j] * qi;
+                acc0[u][j] += fmul_rem(f0, wv[j], wq, q);
+                acc1[u][j] += fmul_rem(f1, wv[j], wq, q);
             }
-        } else {
-            double kb[BM], ka[BM];
+        }
+    };
+    int i = 0;
+    if (!keys[0]) {  // the identity baby (rotation 0, the host puts it first): (P c0, P c1) on the Q limbs
+        double wv[GM], e0[BB], e1[BB];
+#pragma unroll
+        for (int j = 0; j < GM; j++) wv[j] = pt_word(j, 0);
+#pragma unroll
+        for (int u = 0; u < BB; u++) {
+            e0[u] = isq ? fmul_rem(u2d(c0r[u][k]), pw, pf, q) : 0.0;
+            e1[u] = isq ? fmul_rem(u2d(c1r[u][k]), pw, pf, q) : 0.0;
+        }
+        add_terms(e0, e1, wv);
+        i = 1;
+    }
+    // keyed babies, PB per iteration with every load of the PB issued before any arithmetic (a
+    // past-the-end slot of the last iteration re-reads baby nb - 1 and adds nothing)
+    int nsum = 1;
+#pragma unroll 1
+    for (; i < nb; i += PB) {
+        double kb[PB][BM], ka[PB][BM], x[PB][BB][BM], c0v[PB][BB], wv[PB][GM];
+#pragma unroll
+        for (int p = 0; p < PB; p++) {
+            const int ii = min(i + p, nb - 1);
+            const bool live = i + p < nb;
+            const u64 g = gal[ii];
+            const long src = __brev((unsigned)((((g * ek) & (M - 1)) - 1) >> 1)) >> (32 - logN);
+            const u64* kp = keys[ii];
 #pragma unroll
             for (int d = 0; d < BM; d++) {  // the baby's key words: once for the BB elements
-                if (d < beta) {
-                    const u64* kk = kp + (long)d * kdig + ((long)pid << logN) + src;
-                    kb[d] = u2d(kk[0]);
-                    ka[d] = u2d(kk[kcomp]);
-                }
+                const u64* kk = kp + (long)min(d, beta - 1) * kdig + ((long)pid << logN) + src;
+                kb[p][d] = u2d(kk[0]);
+                ka[p][d] = u2d(kk[kcomp]);
             }
 #pragma unroll
-            for (int u = 0; u < BB; u++) {
-                double x[BM];
+            for (int j = 0; j < GM; j++) wv[p][j] = live ? pt_word(j, ii) : 0.0;
 #pragma unroll
-                for (int d = 0; d < BM; d++)
-                    if (d < beta) x[d] = u2d(d == own ? c1r[u][src] : er[u][(long)d * exj + src]);
-                double a0 = isq ? fmul_rem(u2d(c0r[u][src]), pw, pf, q) : 0.0, a1 = 0.0;
+            for (int u = 0; u < BB; u++) {
+#pragma unroll
+                for (int d = 0; d < BM; d++) x[p][u][d] = u2d(d == own ? c1r[u][src] : er[u][(long)min(d, beta - 1) * exj + src]);
+                c0v[p][u] = u2d(c0r[u][src]);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < PB; p++) {
+            double e0[BB], e1[BB];
+#pragma unroll
+            for (int u = 0; u < BB; u++) {
+                double a0 = isq ? fmul_rem(c0v[p][u], pw, pf, q) : 0.0, a1 = 0.0;
 #pragma unroll
                 for (int d = 0; d < BM; d++) {
                     if (d < beta) {
-                        a0 += fmul_rem(x[d], kb[d], kb[d] * qi, q);
-                        a1 += fmul_rem(x[d], ka[d], ka[d] * qi, q);
+                        a0 += fmul_rem(x[p][u][d], kb[p][d], kb[p][d] * qi, q);
+                        a1 += fmul_rem(x[p][u][d], ka[p][d], ka[p][d] * qi, q);
                         if ((d & 3) == 3) {
                             a0 = fred(a0, q, qi);
                             a1 = fred(a1, q, qi);
@@ -1377,20 +1424,11 @@ __global__ __launch_bounds__(256) void k_bsgs_terms(const u64* __restrict__ c0p,
                 e0[u] = a0;
                 e1[u] = a1;
             }
+            add_terms(e0, e1, wv[p]);
         }
-#pragma unroll
-        for (int u = 0; u < BB; u++) {
-            const double f0 = fred(e0[u], q, qi), f1 = fred(e1[u], q, qi);  // |e| <= q/2 + 1
-#pragma unroll
-            for (int j = 0; j < GM; j++) {
-                if (pj[j]) {
-                    const double wq = wv[j] * qi;
-                    acc0[u][j] += fmul_rem(f0, wv[j], wq, q);
-                    acc1[u][j] += fmul_rem(f1, wv[j], wq, q);
-                }
-            }
-        }
-        if ((i & 3) == 3) {
+        nsum += PB;
+        if (nsum >= 4) {  // accumulators: <= 4 + PB - 1 terms of < 1.5 q between folds
+            nsum = 0;
 #pragma unroll
             for (int u = 0; u < BB; u++)
 #pragma unroll
