@@ -84,7 +84,12 @@ extern "C" int32_t aesfhe_abi_version(void) { return AESFHE_ABI_VERSION; }
 // engine state
 // Device memory: the chunked best-fit arena of arena.h over hipMalloc / hipFree (its host logic
 // is unit-tested on the CPU under AddressSanitizer, tests/native/arena_asan.cpp).
+// AESFHE_ARENA_TRACE=path (diagnostic): every engine writes its two arenas' block events to
+// path.<engine number> ("g tag ptr bytes", "p tag ptr", "s tag ptr parts part"), which
+// tools/arena_replay.cpp replays under other arena policies on the CPU.
 struct Pool : Arena {
+    FILE* trace = nullptr;
+    char tag = 'c';
     Pool() {
         A.alloc = [](size_t n, void*) -> void* {
             void* p = nullptr;
@@ -101,12 +106,17 @@ struct Pool : Arena {
     void* get(size_t bytes) {
         void* p = Arena::get(bytes);
         if (!p) throw_err(AESFHE_ENOMEM, "device allocation of %zu bytes failed (%zu held, %zu live)", round_up(bytes), held, live);
+        if (trace) fprintf(trace, "g %c %p %zu\n", tag, p, round_up(bytes));
         return p;
     }
-    void put(void* p, size_t) { Arena::put(p); }
+    void put(void* p, size_t) {
+        if (trace && p) fprintf(trace, "p %c %p\n", tag, p);
+        Arena::put(p);
+    }
     void split(void* p, int parts, size_t part) {
         if (!Arena::split(p, parts, part))
             throw_err(AESFHE_EARG, "pool split of a block that is not %d x %zu bytes", parts, part);
+        if (trace) fprintf(trace, "s %c %p %d %zu\n", tag, p, parts, part);
     }
 };
 
@@ -868,6 +878,12 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
         if (mb > 0) e->pool.chunk_bytes = (size_t)mb << 20;
     }
     e->tpool.chunk_bytes = e->pool.chunk_bytes;
+    e->tpool.tag = 't';
+    if (const char* tp = getenv("AESFHE_ARENA_TRACE")) {
+        static std::atomic<int> engines{0};
+        const std::string path = std::string(tp) + "." + std::to_string(engines++);
+        e->pool.trace = e->tpool.trace = fopen(path.c_str(), "w");
+    }
     HIPC(hipMalloc(&e->ring_d, e->ring_size));
     HIPC(hipHostMalloc((void**)&e->ring_h, e->ring_size, hipHostMallocDefault));
     *out = e.release();
@@ -899,6 +915,7 @@ static void engine_teardown(aesfhe_engine* e) {
     for (auto ev : e->spare) hipEventDestroy(ev);
     e->pool.release_all();
     e->tpool.release_all();
+    if (e->pool.trace) fclose(e->pool.trace);
     void* ptrs[] = {e->q, e->psi, e->ipsi, e->ninv, e->qinv, e->psif, e->ipsif, e->ninvf, e->rtwf, e->irtwf,
                     e->mu_hatinv, e->mu_hat, e->md_phatinv, e->md_phat, e->md_pinv, e->rs_inv,
                     e->rs_mod, e->pmod, e->mu_hatinvf, e->mu_hatf, e->md_phatinvf, e->md_phatf,

@@ -1370,8 +1370,8 @@ __global__ __launch_bounds__(256, OCC) void k_bsgs_terms(const u64* __restrict__
         for (int j = 0; j < GM; j++) wv[j] = pt_word(j, 0);
 #pragma unroll
         for (int u = 0; u < BB; u++) {
-            e0[u] = isq ? fmul_rem(u2d(c0r[u][k]), pw, pf, q) : 0.0;
-            e1[u] = isq ? fmul_rem(u2d(c1r[u][k]), pw, pf, q) : 0.0;
+            e0[u] = isq ? fmul_rem(u2d(*(isq ? c0r[u] + k : &kZeroWord)), pw, pf, q) : 0.0;
+            e1[u] = isq ? fmul_rem(u2d(*(isq ? c1r[u] + k : &kZeroWord)), pw, pf, q) : 0.0;
         }
         add_terms(e0, e1, wv);
         i = 1;
@@ -1400,8 +1400,9 @@ __global__ __launch_bounds__(256, OCC) void k_bsgs_terms(const u64* __restrict__
 #pragma unroll
             for (int u = 0; u < BB; u++) {
 #pragma unroll
-                for (int d = 0; d < BM; d++) x[p][u][d] = u2d(d == own ? c1r[u][src] : er[u][(long)min(d, beta - 1) * exj + src]);
-                c0v[p][u] = u2d(c0r[u][src]);
+                for (int d = 0; d < BM; d++)  // the own digit's word is c1 itself (Q limbs only: own = -1 on P)
+                    x[p][u][d] = u2d(*(d == own ? c1r[u] + src : er[u] + (long)min(d, beta - 1) * exj + src));
+                c0v[p][u] = u2d(*(isq ? c0r[u] + src : &kZeroWord));  // c has the Q limbs only
             }
         }
 #pragma unroll

@@ -1,0 +1,135 @@
+// Replays an AESFHE_ARENA_TRACE event file (engine.hip Pool) through arena.h under other
+// policies, on the CPU (fake addresses, no memory): held / peak live / hipMalloc count per
+// policy, at the end of the trace and at its largest.  Dev tool for VERDICT r4 item 7.
+//   g++ -O2 -std=c++17 -o tools/arena_replay tools/arena_replay.cpp
+//   tools/arena_replay TRACE [TRACE ...]
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../aes-fhe_amd/csrc/arena.h"
+
+using namespace aesfhe;
+
+struct Ev {
+    char op, tag;
+    unsigned long long p;
+    size_t n;
+    int parts;
+};
+
+static std::vector<Ev> load(const char* path) {
+    std::vector<Ev> ev;
+    FILE* f = fopen(path, "r");
+    if (!f) {
+        perror(path);
+        exit(1);
+    }
+    char line[256];
+    while (fgets(line, sizeof line, f)) {
+        Ev e{};
+        char op, tag;
+        void* p;
+        if (sscanf(line, "%c %c %p", &op, &tag, &p) < 3) continue;
+        e.op = op, e.tag = tag, e.p = (unsigned long long)p;
+        if (op == 'g') sscanf(line, "%*c %*c %*p %zu", &e.n);
+        if (op == 's') sscanf(line, "%*c %*c %*p %d %zu", &e.parts, &e.n);
+        ev.push_back(e);
+    }
+    fclose(f);
+    return ev;
+}
+
+struct Policy {
+    const char* name;
+    size_t chunk;
+    double cap;
+    size_t exact_round;  // exact chunks rounded up to this (0: the request)
+    bool two;            // two arenas (ciphertexts / temporaries) or one
+};
+
+struct Fake {
+    unsigned long long next = 1ULL << 40;
+};
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        fprintf(stderr, "usage: arena_replay TRACE [TRACE ...]\n");
+        return 2;
+    }
+    const size_t G = 1ULL << 30;
+    const Policy pols[] = {
+        {"now: 8G chunks, cap 1.2, two arenas", 8 * G, 1.2, 0, true},
+        {"cap 1.1", 8 * G, 1.1, 0, true},
+        {"cap 1.05", 8 * G, 1.05, 0, true},
+        {"cap 1.0", 8 * G, 1.0, 0, true},
+        {"4G chunks, cap 1.2", 4 * G, 1.2, 0, true},
+        {"2G chunks, cap 1.2", 2 * G, 1.2, 0, true},
+        {"2G chunks, cap 1.05", 2 * G, 1.05, 0, true},
+        {"1G chunks, cap 1.05", G, 1.05, 0, true},
+        {"8G chunks, cap 1.05, exact to 1G", 8 * G, 1.05, G, true},
+        {"one arena, 8G, cap 1.2", 8 * G, 1.2, 0, false},
+    };
+    for (int a = 1; a < argc; a++) {
+        const auto ev = load(argv[a]);
+        printf("%s: %zu events\n", argv[a], ev.size());
+        for (const auto& pol : pols) {
+            Fake fk;
+            ArenaAllocator al{[](size_t n, void* ctx) -> void* {
+                                  auto* f = (Fake*)ctx;
+                                  void* p = (void*)f->next;
+                                  f->next += (n + 4095) & ~(size_t)4095;
+                                  return p;
+                              },
+                              [](void*, void*) {}, [](void*) {}, &fk};
+            Arena ar[2];
+            for (auto& x : ar) x.A = al, x.chunk_bytes = pol.chunk, x.grow_cap = pol.cap;
+            std::unordered_map<unsigned long long, std::pair<int, char*>> map;
+            size_t peak_total = 0, max_held = 0;
+            for (const auto& e : ev) {
+                const int k = pol.two && e.tag == 't' ? 1 : 0;
+                if (e.op == 'g') {
+                    if (pol.exact_round) {  // emulate rounding of exact chunks: pre-grow by the rounded need
+                        Arena& A = ar[k];
+                        const size_t n = Arena::round_up(e.n);
+                        if (A.free_size_.lower_bound(n) == A.free_size_.end() && A.peak_live > 0 &&
+                            (double)A.held > A.grow_cap * (double)A.peak_live) {
+                            const size_t r = (n + pol.exact_round - 1) / pol.exact_round * pol.exact_round;
+                            const double cap = A.grow_cap;
+                            A.grow_cap = 0;
+                            const size_t cb = A.chunk_bytes;
+                            A.chunk_bytes = r;
+                            A.new_chunk(n);
+                            A.chunk_bytes = cb;
+                            A.grow_cap = cap;
+                        }
+                    }
+                    char* p = (char*)ar[k].get(e.n);
+                    map[e.p] = {k, p};
+                } else if (e.op == 'p') {
+                    auto it = map.find(e.p);
+                    if (it == map.end()) continue;
+                    ar[it->second.first].put(it->second.second);
+                    map.erase(it);
+                } else if (e.op == 's') {
+                    auto it = map.find(e.p);
+                    if (it == map.end()) continue;
+                    const int kk = it->second.first;
+                    char* base = it->second.second;
+                    ar[kk].split(base, e.parts, e.n);
+                    for (int t = 0; t < e.parts; t++) map[e.p + (unsigned long long)t * e.n] = {kk, base + (size_t)t * e.n};
+                }
+                peak_total = std::max(peak_total, ar[0].live + ar[1].live);
+                max_held = std::max(max_held, ar[0].held + ar[1].held);
+            }
+            const size_t held = ar[0].held + ar[1].held;
+            printf("  %-36s held %6.1f GB (max %6.1f)  peak live %6.1f GB  held/peak %.3f  mallocs %lld\n", pol.name, held / 1e9,
+                   max_held / 1e9, peak_total / 1e9, (double)held / (double)std::max<size_t>(1, peak_total),
+                   (long long)(ar[0].mallocs + ar[1].mallocs));
+        }
+    }
+    return 0;
+}

@@ -25,6 +25,15 @@ CLASSES = [
     (r"k_nttf_inv_rows<\d+, false", "ntt_inv_rows"),
     (r"k_nttf_inv_cols<", "ntt_inv_cols"),
     (r"k_ntt_(fwd|inv)_(rows|cols)<", "ntt_generic"),
+    (r"k_nttf_rows_ks_p<\d+, true, 1>", "ks_rows_fin.prod"),  # round 5: the LDS-DMA pipelined rows
+    (r"k_nttf_rows_ks_p<\d+, false, 1>", "ks_rows_fin.ks"),
+    (r"k_nttf_rows_ks_p<\d+, true, 2>", "ks_rows_inner.prod"),
+    (r"k_nttf_rows_ks_p<\d+, false, 2>", "ks_rows_inner.ks"),
+    (r"k_nttf_rows_ks_p<\d+, true", "ks_rows_acc.prod"),
+    (r"k_nttf_rows_ks_p<", "ks_rows_acc.ks"),
+    (r"k_bconv_mfma<\d+, false", "modup"),  # matrix-core conversions: ModUp (no v slot), ModDown (v)
+    (r"k_bconv_mfma<\d+, true", "moddown"),
+    (r"k_bsgs_terms<", "bsgs_terms"),
     (r"k_nttf_rows_ks<\d+, \d+, true, 1>", "ks_rows_fin.prod"),
     (r"k_nttf_rows_ks<\d+, \d+, false, 1>", "ks_rows_fin.ks"),
     (r"k_nttf_rows_ks<\d+, \d+, true, 2>", "ks_rows_inner.prod"),
