@@ -109,14 +109,23 @@ class Bootstrapper:
     def __init__(self, engine: Engine, sk, rlk, cjk=None, *, hw: int = 32, K: float = 12.0,
                  r: int = 3, deg: int = 31, groups: int = 3, seed: int = 7,
                  bits_deg: int | None = None, bits_r: int | None = None, lazy: bool = True, baby_scale: int = 2,
-                 bits_opt: bool = True, cts_groups: int | None = None, stc_baby_scale: float | None = None):
+                 bits_opt: bool = True, cts_groups: int | None = None, stc_baby_scale: float | None = None,
+                 share: "Bootstrapper | None" = None):
         # cts_groups: CoeffToSlot's stages merged into this many maps (default `groups`, which
         # StC keeps): more groups = more levels, far fewer diagonals per map
+        # share: a bootstrapper of the same engine and secret key whose key material this one
+        # reuses -- the conjugation and sparse-secret keys, every rotation key of the same
+        # rotation, and the SlotToCoeff plans (plaintext diagonals) when their parameters match.
+        # The AES drivers run a 5-map and a 3-map CoeffToSlot bootstrapper side by side: their
+        # StC maps are the same, and each held its own copy (config 5: 116 rotation keys of
+        # 0.3 GB live at the N = 2^17 peak).
         cts_groups = groups if cts_groups is None else cts_groups
         self.groups, self.cts_groups = groups, cts_groups
         e = self.e = engine
         self.rlk = rlk
-        self.cjk = cjk if cjk is not None else e.create_conjugation_key(sk)
+        if share is not None and share.e is not engine:
+            raise ValueError("Bootstrapper(share=...) needs a bootstrapper of the same engine")
+        self.cjk = cjk if cjk is not None else share.cjk if share is not None else e.create_conjugation_key(sk)
         self.N = 1 << e.log_coeff_count
         self.n = self.N // 2
         self.L = e.max_level
@@ -140,9 +149,13 @@ class Bootstrapper:
         # write and read back, so its split may take fewer babies (stc_baby_scale)
         self.stc_baby_scale = self.baby_scale if stc_baby_scale is None or not lazy else stc_baby_scale
         # sparse-secret encapsulation keys
-        s_sparse = e.create_sparse_secret_key(hw, seed)
-        self.to_sparse = e.create_switching_key(sk, s_sparse)
-        self.from_sparse = e.create_switching_key(s_sparse, sk)
+        self._sparse_id = (hw, seed)
+        if share is not None and share._sparse_id == self._sparse_id:
+            self.to_sparse, self.from_sparse = share.to_sparse, share.from_sparse
+        else:
+            s_sparse = e.create_sparse_secret_key(hw, seed)
+            self.to_sparse = e.create_switching_key(sk, s_sparse)
+            self.from_sparse = e.create_switching_key(s_sparse, sk)
         q0 = float(e.primes[0])
         D = e.scales
         n, N = self.n, self.N
@@ -169,10 +182,16 @@ class Bootstrapper:
         c_bits = q0 / (4.0 * D[0])
         stc_bits[-1] = {d: v * c_bits for d, v in stc_bits[-1].items()}
         self.cts = [self._prepare(M) for M in cts]
-        self.stc = [self._prepare(M, self.stc_baby_scale) for M in stc]
-        self.stc_bits = [self._prepare(M, self.stc_baby_scale) for M in stc_bits]
-        self._stc_bits_maps = stc_bits  # for the scaled-input variants (bootstrap_bits in_scale)
-        self._stc_bits_scaled: Dict[float, list] = {1.0: self.stc_bits}
+        # the StC plans depend on (groups, split, chain, the two output constants) only
+        self._stc_id = (groups, self.stc_baby_scale, self.L, c_out, c_bits)
+        if share is not None and share._stc_id == self._stc_id:
+            self.stc, self.stc_bits = share.stc, share.stc_bits
+            self._stc_bits_maps, self._stc_bits_scaled = share._stc_bits_maps, share._stc_bits_scaled
+        else:
+            self.stc = [self._prepare(M, self.stc_baby_scale) for M in stc]
+            self.stc_bits = [self._prepare(M, self.stc_baby_scale) for M in stc_bits]
+            self._stc_bits_maps = stc_bits  # for the scaled-input variants (bootstrap_bits in_scale)
+            self._stc_bits_scaled: Dict[float, list] = {1.0: self.stc_bits}
         self.cts_bits = [self._prepare(M) for M in cts_bits] if bits_opt else self.cts
         # rotation keys: hoisted keys for the baby steps (one ModUp per group input), ordinary
         # keys for the giant steps
@@ -181,8 +200,9 @@ class Bootstrapper:
             u, g = plan["u"], plan["g"]
             babies.update((k1 * u) % n for k2, tl in plan["terms"].items() for k1, _ in tl if k1)
             giants.update((g * k2 * u) % n for k2 in plan["giants"] if (g * k2 * u) % n)
-        self.hrot = {d: e.create_hoisted_rotation_key(sk, -d) for d in sorted(babies)}
-        self.rot = {d: e.create_fixed_rotation_key(sk, -d) for d in sorted(giants)}
+        hs, rs = (share.hrot, share.rot) if share is not None else ({}, {})
+        self.hrot = {d: hs[d] if d in hs else e.create_hoisted_rotation_key(sk, -d) for d in sorted(babies)}
+        self.rot = {d: rs[d] if d in rs else e.create_fixed_rotation_key(sk, -d) for d in sorted(giants)}
         # EvalMod: Chebyshev coefficients of cos(2 pi (Bnd x - 1/4) / 2^r) on [-1, 1], degree 31
         # and r = 3 (fit error 1.6e-13) in both modes.  A cheaper bit-mode fit (degree 15, r = 4:
         # same depth, 11 products instead of 14) leaves a sin error of 5.4e-5 that is the SAME

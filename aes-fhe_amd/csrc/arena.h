@@ -33,12 +33,13 @@ struct Arena {
     static constexpr size_t kAlign = 256;
     ArenaAllocator A{};
     size_t chunk_bytes = (size_t)1 << 33;
-    // growth cap: once the arena holds more than grow_cap x the largest live set seen, a new
-    // chunk is sized to its request alone -- fragmentation then grows the arena by what it needs,
-    // not by 8 GiB steps (round 3: 211.5 GB held for a 159.4 GB peak in the bench round; round 4
-    // at cap 1.2: 1.29 x; cap 1.0 measured the same, 1.35 x: the excess is fragmentation, which the
-    // engine now keeps down with a second arena for temporaries).  0 disables.
-    double grow_cap = 1.2;
+    // growth cap: a new chunk is clamped to what keeps the arena within grow_cap x the largest
+    // live set seen (counting the request), never below the request -- fragmentation then grows
+    // the arena by what it needs, not by 8 GiB steps.  Round 4 switched to request-sized chunks only
+    // once held exceeded the cap (1.29 x in the bench round); the replay of the round-5 bench's
+    // block events (tools/arena_replay.cpp, AESFHE_ARENA_TRACE) put the clamp at 1.1 at 1.24 x
+    // (bench round) and 1.19 x (config 5: 232 instead of 249 GB held).  0 disables.
+    double grow_cap = 1.1;
     std::map<char*, size_t> chunks_;                  // base -> size
     std::map<char*, size_t> free_addr_;               // free block -> size (address order)
     std::multimap<size_t, char*> free_size_;          // size -> free block (best fit)
@@ -68,9 +69,12 @@ struct Arena {
     }
     bool new_chunk(size_t need) {
         size_t want = std::max(chunk_bytes, need);
-        if (grow_cap > 0 && want > need && peak_live > 0 && (double)held > grow_cap * (double)peak_live) {
-            want = need;
-            exact_chunks++;
+        if (grow_cap > 0 && want > need && peak_live > 0) {
+            const double room = grow_cap * (double)std::max(peak_live, live + need) - (double)held;
+            if (room < (double)want) {
+                want = std::max(need, (size_t)std::max(0.0, room) & ~(kAlign - 1));
+                exact_chunks++;
+            }
         }
         void* p = A.alloc(want, A.ctx);
         if (!p && want > need) {  // nearly full: release empty chunks, then the exact need

@@ -144,10 +144,10 @@ struct aesfhe_engine {
     ChaKey ck;  // ChaCha20 key of every random stream
     Chain chain;
     hipStream_t stream;
-    // two arenas (round 5): `pool` for what outlives a call (ciphertexts, plaintexts, keys),
-    // `tpool` for the per-call temporaries (Tmp: extensions, accumulators, conversions).  In one
-    // arena the short-lived blocks landed between long-lived ones and left holes (round 4: 1.29-1.35x
-    // the peak live set held, 51 GB of fragmentation in the bench round).
+    // one arena for every block (`tpool` is unused): a second arena for the per-call temporaries
+    // (tried in round 5 against the holes short-lived blocks leave between long-lived ones) held
+    // more in the replay of the bench's block events (tools/arena_replay.cpp: bench round 1.28 vs
+    // 1.26 x its peak live set, config 5 249 vs 236 GB)
     Pool pool, tpool;
     size_t peak_total = 0;  // largest pool.live + tpool.live seen
     // device tables
@@ -314,13 +314,14 @@ static T* upload_small(aesfhe_engine* e, const T* src, size_t count) {
 // whatever the block held before
 static void* pool_get(aesfhe_engine* e, size_t bytes, bool tmp = false) {
     static const bool poison = getenv("AESFHE_POOL_POISON") && atoi(getenv("AESFHE_POOL_POISON"));
-    void* p = (tmp ? e->tpool : e->pool).get(bytes);
+    (void)tmp;  // one arena (round 5 replay: two arenas held more); tpool stays empty
+    void* p = e->pool.get(bytes);
     e->peak_total = std::max(e->peak_total, e->pool.live + e->tpool.live);
     if (poison && p) HIPC(hipMemsetAsync(p, 0xA5, bytes, e->stream));
     return p;
 }
 static u64* dalloc(aesfhe_engine* e, size_t words) { return (u64*)pool_get(e, words * 8, true); }
-static void dfree(aesfhe_engine* e, u64* p, size_t words) { e->tpool.put(p, words * 8); }
+static void dfree(aesfhe_engine* e, u64* p, size_t words) { e->pool.put(p, words * 8); }
 
 struct Tmp {  // RAII temporary device buffer from the pool
     aesfhe_engine* e;

@@ -445,7 +445,10 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
              for g in args.aes10_cts_groups]
     sched = R.schedule(L, cands)
     used = {b.cts_groups for _, _, b in sched if b is not None}
-    bs = [Bootstrapper(eng, sk, rlk, cjk, cts_groups=g) for g in args.aes10_cts_groups if g in used]
+    bs = []  # the second shares the first's keys and SlotToCoeff plans (Bootstrapper share=)
+    for g in args.aes10_cts_groups:
+        if g in used:
+            bs.append(Bootstrapper(eng, sk, rlk, cjk, cts_groups=g, share=bs[0] if bs else None))
     eng.synchronize()
     setup_s = time.perf_counter() - t0
     key = np.random.default_rng(25073103).integers(0, 256, 16, dtype=np.uint8)

@@ -25,7 +25,9 @@ def _run(lib, log_n, nb=1, seed=3, cls=AESRowRound, cts_groups=(3,), key_levels=
     sk = e.create_secret_key(1)
     rlk = e.create_relinearization_key(sk)
     R = cls(e, sk, e.create_public_key(sk), rlk)
-    bs = [Bootstrapper(e, sk, rlk, cts_groups=g) for g in cts_groups]
+    bs = []
+    for g in cts_groups:  # later ones share the first's keys and SlotToCoeff plans, as in bench.py
+        bs.append(Bootstrapper(e, sk, rlk, cts_groups=g, share=bs[0] if bs else None))
     rng = np.random.default_rng(seed)
     key = np.frombuffer(FIPS_C1_KEY, dtype=np.uint8)
     blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)

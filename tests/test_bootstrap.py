@@ -99,6 +99,31 @@ def test_bootstrap_bits_oracle(oracle_lib, opt):
         bs.bootstrap_bits(e.encrypt(a, pk, level=2))
 
 
+def test_bootstrapper_share(oracle_lib):
+    """Bootstrapper(share=...): a 3-map CoeffToSlot bootstrapper built beside a 5-map one reuses
+    its conjugation and sparse-secret keys, every rotation key of a common rotation and the
+    SlotToCoeff plans (the bench's and the AES drivers' pair), creates only the keys it alone
+    needs, and still squares the input error of the bit mode."""
+    e, sk, pk, rlk = _engine(oracle_lib, max_level=30, scale_bits=40)
+    b5 = Bootstrapper(e, sk, rlk, cts_groups=5)
+    b3 = Bootstrapper(e, sk, rlk, cts_groups=3, share=b5)
+    assert b3.cjk is b5.cjk and b3.to_sparse is b5.to_sparse and b3.from_sparse is b5.from_sparse
+    assert b3.stc_bits is b5.stc_bits and b3.stc is b5.stc
+    common = set(b3.hrot) & set(b5.hrot)
+    assert common and all(b3.hrot[d] is b5.hrot[d] for d in common)
+    assert all(b3.rot[d] is b5.rot[d] for d in set(b3.rot) & set(b5.rot))
+    with pytest.raises(ValueError):
+        e2, sk2, _, rlk2 = _engine(oracle_lib)
+        Bootstrapper(e2, sk2, rlk2, share=b5)
+    n = e.slot_count
+    rng = np.random.default_rng(6)
+    a, b = rng.choice([-1.0, 1.0], n), rng.choice([-1.0, 1.0], n)
+    noise = 0.03 * rng.standard_normal((2, n))
+    ya, yb = b3.bootstrap_bits(e.encrypt(a + noise[0], pk, level=3), e.encrypt(b + noise[1], pk, level=3))
+    for y, v, nz in ((ya, a, noise[0]), (yb, b, noise[1])):
+        assert np.all(np.abs(e.decrypt(y, sk) - v) <= 1.24 * nz ** 2 + 1e-5)
+
+
 @pytest.mark.parametrize("deg", [3, 7, 15, 29])
 def test_chebyshev_opt_depth_and_values(oracle_lib, deg):
     """chebyshev_opt (bootstrap.py): a random Chebyshev series of degree deg lands exactly

@@ -147,7 +147,8 @@ def test_config4_full_batch_ten_rounds(product_lib, gpu_available, seed):
     sk = e.create_secret_key()
     rlk = e.create_relinearization_key(sk)
     R = AESSlicedRound(e, sk, e.create_public_key(sk), rlk)
-    bs = [Bootstrapper(e, sk, rlk, cts_groups=g) for g in (5, 3)]
+    bs5 = Bootstrapper(e, sk, rlk, cts_groups=5)
+    bs = [bs5, Bootstrapper(e, sk, rlk, cts_groups=3, share=bs5)]  # as bench.py builds them
     L0 = R.fresh_level(e.max_level, bs)
     klv = R.key_levels(L0, bs)
     assert L0 == 25

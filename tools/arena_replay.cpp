@@ -49,6 +49,55 @@ struct Policy {
     double cap;
     size_t exact_round;  // exact chunks rounded up to this (0: the request)
     bool two;            // two arenas (ciphertexts / temporaries) or one
+    int fit = 0;         // 0 best fit (arena.h), 1 address-ordered first fit, 2 best fit from the top of a chunk
+    size_t big = 0;      // blocks >= big: exact-size cache (reused only by the same size), 0 off
+    bool clamp = false;  // new chunks clamped to cap x peak_live - held (never below the request)
+};
+
+// arena.h with another placement rule (replay only)
+struct ArenaX : Arena {
+    int fit = 0;
+    bool clamp = false;
+    void* getx(size_t bytes) {
+        const size_t n = round_up(bytes);
+        if (clamp && free_size_.lower_bound(n) == free_size_.end() && peak_live > 0) {
+            const double room = grow_cap * (double)std::max(peak_live, live + n) - (double)held;
+            const size_t want = std::max(n, (size_t)std::max(0.0, std::min((double)chunk_bytes, room)));
+            const size_t cb = chunk_bytes;
+            const double cap = grow_cap;
+            chunk_bytes = (want + kAlign - 1) & ~(kAlign - 1);
+            grow_cap = 0;
+            new_chunk(n);
+            chunk_bytes = cb;
+            grow_cap = cap;
+        }
+        if (fit == 0) return get(bytes);
+        std::map<char*, size_t>::iterator it = free_addr_.end();
+        if (fit == 1) {
+            for (auto f = free_addr_.begin(); f != free_addr_.end(); ++f)
+                if (f->second >= n) {
+                    it = f;
+                    break;
+                }
+        }
+        if (it == free_addr_.end()) {
+            if (fit == 2) return get(bytes);
+            if (!new_chunk(n)) return nullptr;
+            for (auto f = free_addr_.begin(); f != free_addr_.end(); ++f)
+                if (f->second >= n) {
+                    it = f;
+                    break;
+                }
+        }
+        char* p = it->first;
+        const size_t have = it->second;
+        del_free(p, have);
+        if (have > n) add_free(p + n, have - n);
+        live_[p] = n;
+        live += n;
+        peak_live = std::max(peak_live, live);
+        return p;
+    }
 };
 
 struct Fake {
@@ -72,6 +121,22 @@ int main(int argc, char** argv) {
         {"1G chunks, cap 1.05", G, 1.05, 0, true},
         {"8G chunks, cap 1.05, exact to 1G", 8 * G, 1.05, G, true},
         {"one arena, 8G, cap 1.2", 8 * G, 1.2, 0, false},
+        {"two, first fit", 8 * G, 1.2, 0, true, 1},
+        {"two, clamp 1.15", 8 * G, 1.15, 0, true, 0, 0, true},
+        {"two, clamp 1.1", 8 * G, 1.1, 0, true, 0, 0, true},
+        {"one, clamp 1.15", 8 * G, 1.15, 0, false, 0, 0, true},
+        {"one, clamp 1.1", 8 * G, 1.1, 0, false, 0, 0, true},
+        {"one, clamp 1.05", 8 * G, 1.05, 0, false, 0, 0, true},
+        {"one, clamp 1.02", 8 * G, 1.02, 0, false, 0, 0, true},
+        {"one, clamp 1.1, 16G", 16 * G, 1.1, 0, false, 0, 0, true},
+        {"one, clamp 1.1, first fit", 8 * G, 1.1, 0, false, 1, 0, true},
+        {"one, clamp 1.05, first fit", 8 * G, 1.05, 0, false, 1, 0, true},
+        {"one, first fit", 8 * G, 1.2, 0, false, 1},
+        {"one, first fit, 4G", 4 * G, 1.2, 0, false, 1},
+        {"two, big >= 2G exact cache", 8 * G, 1.2, 0, true, 0, 2 * G},
+        {"one, big >= 2G exact cache", 8 * G, 1.2, 0, false, 0, 2 * G},
+        {"one, first fit, big >= 2G cache", 8 * G, 1.2, 0, false, 1, 2 * G},
+        {"one, first fit, big >= 4G cache", 8 * G, 1.2, 0, false, 1, 4 * G},
     };
     for (int a = 1; a < argc; a++) {
         const auto ev = load(argv[a]);
@@ -85,8 +150,12 @@ int main(int argc, char** argv) {
                                   return p;
                               },
                               [](void*, void*) {}, [](void*) {}, &fk};
-            Arena ar[2];
-            for (auto& x : ar) x.A = al, x.chunk_bytes = pol.chunk, x.grow_cap = pol.cap;
+            ArenaX ar[2];
+            for (auto& x : ar) x.A = al, x.chunk_bytes = pol.chunk, x.grow_cap = pol.cap, x.fit = pol.fit, x.clamp = pol.clamp;
+            // exact-size cache for big blocks: free blocks by size; held = every block ever made
+            std::multimap<size_t, char*> bigfree;
+            std::unordered_map<char*, size_t> biglive;
+            size_t bigheld = 0, biglivesz = 0;
             std::unordered_map<unsigned long long, std::pair<int, char*>> map;
             size_t peak_total = 0, max_held = 0;
             for (const auto& e : ev) {
@@ -107,25 +176,49 @@ int main(int argc, char** argv) {
                             A.grow_cap = cap;
                         }
                     }
-                    char* p = (char*)ar[k].get(e.n);
-                    map[e.p] = {k, p};
+                    if (pol.big && e.n >= pol.big) {
+                        auto f = bigfree.find(e.n);
+                        char* p;
+                        if (f != bigfree.end()) {
+                            p = f->second;
+                            bigfree.erase(f);
+                        } else {
+                            p = (char*)fk.next;
+                            fk.next += (e.n + 4095) & ~(size_t)4095;
+                            bigheld += e.n;
+                        }
+                        biglive[p] = e.n;
+                        biglivesz += e.n;
+                        map[e.p] = {2, p};
+                    } else {
+                        char* p = (char*)ar[k].getx(e.n);
+                        map[e.p] = {k, p};
+                    }
                 } else if (e.op == 'p') {
                     auto it = map.find(e.p);
                     if (it == map.end()) continue;
-                    ar[it->second.first].put(it->second.second);
+                    if (it->second.first == 2) {
+                        const size_t n = biglive[it->second.second];
+                        biglive.erase(it->second.second);
+                        biglivesz -= n;
+                        bigfree.insert({n, it->second.second});
+                    } else {
+                        ar[it->second.first].put(it->second.second);
+                    }
                     map.erase(it);
                 } else if (e.op == 's') {
                     auto it = map.find(e.p);
                     if (it == map.end()) continue;
                     const int kk = it->second.first;
                     char* base = it->second.second;
+                    if (kk == 2) continue;  // (big blocks are never split in the traces)
                     ar[kk].split(base, e.parts, e.n);
                     for (int t = 0; t < e.parts; t++) map[e.p + (unsigned long long)t * e.n] = {kk, base + (size_t)t * e.n};
                 }
-                peak_total = std::max(peak_total, ar[0].live + ar[1].live);
-                max_held = std::max(max_held, ar[0].held + ar[1].held);
+                peak_total = std::max(peak_total, ar[0].live + ar[1].live + biglivesz);
+                max_held = std::max(max_held, ar[0].held + ar[1].held + bigheld);
             }
-            const size_t held = ar[0].held + ar[1].held;
+            const size_t held = ar[0].held + ar[1].held + bigheld;
             printf("  %-36s held %6.1f GB (max %6.1f)  peak live %6.1f GB  held/peak %.3f  mallocs %lld\n", pol.name, held / 1e9,
                    max_held / 1e9, peak_total / 1e9, (double)held / (double)std::max<size_t>(1, peak_total),
                    (long long)(ar[0].mallocs + ar[1].mallocs));
