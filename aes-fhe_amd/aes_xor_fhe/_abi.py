@@ -79,6 +79,7 @@ SIGNATURES = [
      [c_eng_p, c_key_p, _P(C.c_int32), _P(C.c_uint64), _P(C.c_uint64), _P(C.c_int64), _P(C.c_uint64)]),
     ("aesfhe_key_import", C.c_int,
      [c_eng_p, C.c_int32, C.c_uint64, C.c_uint64, _P(C.c_uint64), C.c_int64, _P(c_key_p)]),
+    ("aesfhe_key_trim", C.c_int, [c_eng_p, c_key_p, C.c_int32]),
     ("aesfhe_encrypt", C.c_int,
      [c_eng_p, c_key_p, _P(C.c_int64), C.c_int32, C.c_int32, C.c_uint64, _P(c_ct_p)]),
     ("aesfhe_decrypt", C.c_int, [c_eng_p, c_key_p, c_ct_p, _P(C.c_int64)]),

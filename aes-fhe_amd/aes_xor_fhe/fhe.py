@@ -1169,6 +1169,20 @@ class Engine:
             k.delta = hdr["delta"]
         return k
 
+    def key_bytes(self, key) -> int:
+        """Device bytes of a key's residues (aesfhe_key_export's word count x 8)."""
+        kind, g, seed, words = C.c_int32(), C.c_uint64(), C.c_uint64(), C.c_int64()
+        self._check(self._lib.key_export(self._h, key._h, C.byref(kind), C.byref(g), C.byref(seed),
+                                         C.byref(words), None))
+        return 8 * words.value
+
+    def trim_key(self, key, max_level: int):
+        """Keep only the key-switch digits a switch at level <= max_level reads
+        (aesfhe_key_trim): the kept digits are the full key's word for word; a later switch above
+        max_level raises.  Used for the bootstrapper's SlotToCoeff keys (trim_bootstrap_keys)."""
+        self._check(self._lib.key_trim(self._h, key._h, int(max_level)))
+        return key
+
     def pool_stats(self) -> dict:
         """Device pool counters (aesfhe_engine_pool_stats): bytes held / live, hipMalloc calls,
         trims, reuses of a larger cached block."""

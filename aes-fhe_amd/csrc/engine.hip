@@ -217,6 +217,7 @@ struct aesfhe_key {
     u64 keyseed;
     u64* d;
     size_t bytes;
+    int ndig = 0;  // switching keys: digits stored (dnum, or fewer after aesfhe_key_trim)
 };
 
 struct aesfhe_ct {
@@ -1146,6 +1147,7 @@ static aesfhe_key* make_ksk_t(aesfhe_engine* e, const u64* starget, u64 keyseed,
     aesfhe_key* k = key_new(e, kind, (size_t)e->dnum * 2 * np * N);
     k->galois = g;
     k->keyseed = keyseed;
+    k->ndig = e->dnum;
     u64 base = derive(derive(keyseed, 4 + (u64)kind), g);
     if (salt) base = derive(base, salt);
     Tmp et(e, (size_t)np * N);
@@ -1324,15 +1326,41 @@ extern "C" int aesfhe_key_export(aesfhe_engine* e, const aesfhe_key* k, int32_t*
 extern "C" int aesfhe_key_import(aesfhe_engine* e, int32_t kind, uint64_t galois, uint64_t keyseed,
                                  const uint64_t* in, int64_t words, aesfhe_key** out) {
     API_BEGIN
-    const size_t want = key_words(e, kind);
+    size_t want = key_words(e, kind);
     if (!in || !want) throw_err(AESFHE_EARG, "unknown key kind %d", kind);
+    int ndig = 0;
+    if (kind == 2 || kind == 3 || kind == 5) {  // switching keys: dnum digits, or a trimmed key's first ones
+        const size_t dw = (size_t)2 * e->np * e->N;
+        if (words > 0 && (size_t)words % dw == 0 && (size_t)words / dw >= 1 && (size_t)words / dw <= (size_t)e->dnum)
+            want = (size_t)words, ndig = (int)((size_t)words / dw);
+    }
     if ((size_t)words != want) throw_err(AESFHE_EARG, "key of kind %d needs %zu words, got %lld", kind, want, (long long)words);
     aesfhe_key* k = key_new(e, kind, want);
     k->galois = galois;
     k->keyseed = keyseed;
+    k->ndig = ndig;
     HIPC(hipMemcpyAsync(k->d, in, want * 8, hipMemcpyHostToDevice, e->stream));
     HIPC(hipStreamSynchronize(e->stream));
     *out = k;
+    API_END
+}
+// Drop a switching key's digits beyond those a key switch at level <= max_level reads (include/
+// aesfhe.h): digit d of a key is generated from its own random streams, so the first ones are
+// word for word the full key's and every switch at those levels is unchanged.
+extern "C" int aesfhe_key_trim(aesfhe_engine* e, aesfhe_key* k, int32_t max_level) {
+    API_BEGIN
+    if (!k || k->ndig < 1) throw_err(AESFHE_EARG, "only switching keys (relinearization, galois, hoisted rotation) can be trimmed");
+    if (max_level < 0 || max_level > e->L) throw_err(AESFHE_EARG, "bad level %d", max_level);
+    const int nd = (max_level + 1 + e->A - 1) / e->A;  // ks_beta(e, max_level)
+    if (nd < k->ndig) {
+        const size_t bytes = (size_t)nd * 2 * e->np * e->N * 8;
+        u64* d = (u64*)pool_get(e, bytes);
+        HIPC(hipMemcpyAsync(d, k->d, bytes, hipMemcpyDeviceToDevice, e->stream));
+        e->pool.put(k->d, k->bytes);  // stream-ordered: reused only by later work
+        k->d = d;
+        k->bytes = bytes;
+        k->ndig = nd;
+    }
     API_END
 }
 extern "C" int aesfhe_ct_copy(aesfhe_engine* e, const aesfhe_ct* c, aesfhe_ct** out) {
@@ -2148,6 +2176,12 @@ static int ks_beta(const aesfhe_engine* e, int l) {
     if (beta > 12) throw_err(AESFHE_EUNSUPPORTED, "more than 12 key-switch digits");
     return beta;
 }
+// a switching key serves a key switch at level l when it stores the beta(l) digits it reads
+// (aesfhe_key_trim keeps the first digits only; their words are the full key's, digit by digit)
+static void check_key_digits(aesfhe_engine* e, const aesfhe_key* k, int l) {
+    if (k && k->ndig > 0 && ks_beta(e, l) > k->ndig)
+        throw_err(AESFHE_ELEVEL, "key trimmed to %d digits cannot switch at level %d (%d digits)", k->ndig, l, ks_beta(e, l));
+}
 
 // Key switch, first half (ModUp): ext[j][b] = the NTT-domain extension of digit j of d to every
 // limb of Q_l u P outside the digit (the digit's own limbs are read from d by the inner product).
@@ -2260,6 +2294,7 @@ static void ks_inner_acc(aesfhe_engine* e, const u64* d, long dbs, const u64* ex
     const int N = e->N, K = e->K, ne = l + 1 + K;
     const long neN = (long)ne * N;
     const int beta = ks_beta(e, l);
+    check_key_digits(e, k, l);
     const double* pm = pmod ? (const double*)e->pmodf : (const double*)nullptr;
     if (pb && (!ext_cols || !pmod || accum)) throw_err(AESFHE_EARG, "product key switch needs the fused combined path");
     if (ext_cols) {
@@ -2415,6 +2450,7 @@ static void ks_finish_fused(aesfhe_engine* e, const u64* d, long dbs, const u64*
     const int N = e->N, K = e->K, ne = l + 1 + K, R = N / 256;
     const long neN = (long)ne * N;
     const int beta = ks_beta(e, l), lk = l - r;
+    check_key_digits(e, k, l);
     if (r < 0 || r > kMdrMaxR || K + r > kMdrMaxE || lk < 0) throw_err(AESFHE_EARG, "bad combined rescale depth %d", r);
     if (pb && r < 1) throw_err(AESFHE_EARG, "product key switch needs the fused combined path");
     const long kN = (long)(lk + 1) * N;
@@ -2763,8 +2799,10 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
         if (gkeys[j] && gkeys[j]->kind != 3) throw_err(AESFHE_EARG, "giant steps need galois keys");
         tot += nterm[j];
     }
-    for (int i = 0; i < nb; i++)
+    for (int i = 0; i < nb; i++) {
         if (bkeys[i] && bkeys[i]->kind != 5) throw_err(AESFHE_EARG, "baby steps need hoisted rotation keys");
+        check_key_digits(e, bkeys[i], l);
+    }
     for (int t = 0; t < tot; t++) {
         if (tbaby[t] < 0 || tbaby[t] >= nb) throw_err(AESFHE_EARG, "bad baby index");
         if (!pts[t] || !pts[t]->ext || pts[t]->level != l) throw_err(AESFHE_EARG, "linear_bsgs needs Q u P plaintexts at the input level");

@@ -430,7 +430,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     layouts (sliced / rows): a warm-up encryption of the same shape (bootstrap plaintexts, device pool), then one
     timed encryption of args.aes10_batch ciphertext sets (x 8192 blocks at N = 2^16)."""
     from aes_xor_fhe import aes_tables as T
-    from aes_xor_fhe.bootstrap import Bootstrapper
+    from aes_xor_fhe.bootstrap import Bootstrapper, trim_bootstrap_keys
     R = drv.R
     sk, _, rlk, cjk = drv.keys
     from types import SimpleNamespace
@@ -449,6 +449,8 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
     for g in args.aes10_cts_groups:
         if g in used:
             bs.append(Bootstrapper(eng, sk, rlk, cjk, cts_groups=g, share=bs[0] if bs else None))
+    # bit refreshes only: SlotToCoeff-only rotation keys keep the one digit they switch with
+    keys_trimmed = trim_bootstrap_keys(bs)
     eng.synchronize()
     setup_s = time.perf_counter() - t0
     key = np.random.default_rng(25073103).integers(0, 256, 16, dtype=np.uint8)
@@ -523,7 +525,8 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
             "blocks_per_gpu": nb * R.n_blk, "refreshes": nref,
             "bootstrap_share": round(tm.get("bootstrap", 0.0) / max(el, 1e-9), 3),
             "bootstrap_ms_per_bit_ct": round(1e3 * tm.get("bootstrap", 0.0) / max(nref * 32 * nb, 1), 2),
-            "bootstrap_setup_s": round(setup_s, 2), "verified": ok, "mismatch": wrong, "margin": margin,
+            "bootstrap_setup_s": round(setup_s, 2), "bootstrap_keys_trimmed_gb": round(keys_trimmed / 1e9, 2),
+            "verified": ok, "mismatch": wrong, "margin": margin,
             "bootstrap_cts_groups": [b.cts_groups for b in bs], "round_key_levels": klv,
             "state_level": L0,
             "block_rounds_per_s": round(10 * nb * R.n_blk * world / el, 2),

@@ -185,6 +185,14 @@ int aesfhe_key_export(aesfhe_engine *eng, const aesfhe_key *key, int32_t *kind, 
                       uint64_t *keyseed, int64_t *words, uint64_t *out);
 int aesfhe_key_import(aesfhe_engine *eng, int32_t kind, uint64_t galois_elt, uint64_t keyseed,
                       const uint64_t *in, int64_t words, aesfhe_key **out);
+/* Keep only the key-switch digits that a switch at level <= max_level reads (switching keys:
+ * relinearization, galois / key-switch, hoisted rotation).  Digit d of a key is generated from
+ * its own random streams, so the kept digits are word for word the full key's and every switch
+ * at those levels is unchanged; a switch above max_level fails with AESFHE_ELEVEL.  A trimmed key
+ * exports and imports with its digit count (words = digits x 2 x (L+1+K) x N).  No desilofhe
+ * counterpart (its key memory is internal): the bootstrapper's SlotToCoeff keys only ever switch
+ * at the bottom levels (bootstrap.py trim_bootstrap_keys). */
+int aesfhe_key_trim(aesfhe_engine *eng, aesfhe_key *key, int32_t max_level);
 
 /* ---- ciphertexts ------------------------------------------------------------------------ */
 /* coeffs: batch*N integer coefficients (encoded at the canonical scale of `level`);

@@ -253,6 +253,7 @@ struct aesfhe_key {
     u64 galois;
     u64 keyseed;
     u64 *data;
+    int ndig; /* switching keys: digits stored (dnum, or fewer after aesfhe_key_trim) */
 };
 
 struct aesfhe_ct {
@@ -893,6 +894,7 @@ static aesfhe_key *make_ksk_t(aesfhe_engine *e, const u64 *starget, u64 keyseed,
     k->galois = g;
     k->keyseed = keyseed;
     k->data = malloc(sizeof(u64) * (size_t)e->dnum * 2 * np * N);
+    k->ndig = e->dnum;
     u64 base = derive(derive(keyseed, 4 + (u64)kind), g);
     if (salt) base = derive(base, salt);
     /* P mod q_i */
@@ -1165,19 +1167,40 @@ int aesfhe_key_export(aesfhe_engine *e, const aesfhe_key *k, int32_t *kind, uint
     *kind = k->kind;
     *galois = k->galois;
     *keyseed = k->keyseed;
-    *words = (int64_t)key_words(e, k->kind);
+    *words = (int64_t)(k->ndig > 0 ? (size_t)k->ndig * 2 * e->np * e->N : key_words(e, k->kind));
     if (out) memcpy(out, k->data, sizeof(u64) * (size_t)*words);
+    return 0;
+}
+/* aesfhe_key_trim (include/aesfhe.h): the first beta(max_level) digits, word for word */
+int aesfhe_key_trim(aesfhe_engine *e, aesfhe_key *k, int32_t max_level) {
+    if (!k || k->ndig < 1) return fail(AESFHE_EARG, "only switching keys (relinearization, galois, hoisted rotation) can be trimmed");
+    if (max_level < 0 || max_level > e->L) return fail(AESFHE_EARG, "bad level %d", max_level);
+    const int nd = (max_level + 1 + e->A - 1) / e->A;
+    if (nd < k->ndig) {
+        u64 *d = malloc(sizeof(u64) * (size_t)nd * 2 * e->np * e->N);
+        memcpy(d, k->data, sizeof(u64) * (size_t)nd * 2 * e->np * e->N);
+        free(k->data);
+        k->data = d;
+        k->ndig = nd;
+    }
     return 0;
 }
 int aesfhe_key_import(aesfhe_engine *e, int32_t kind, uint64_t galois, uint64_t keyseed,
                       const uint64_t *in, int64_t words, aesfhe_key **out) {
     size_t want = key_words(e, kind);
     if (!in || !want) return fail(AESFHE_EARG, "unknown key kind %d", kind);
+    int ndig = 0;
+    if (kind == 2 || kind == 3 || kind == 5) { /* switching keys: dnum digits or a trimmed key's first ones */
+        const size_t dw = (size_t)2 * e->np * e->N;
+        if (words > 0 && (size_t)words % dw == 0 && (size_t)words / dw <= (size_t)e->dnum)
+            want = (size_t)words, ndig = (int)((size_t)words / dw);
+    }
     if ((size_t)words != want) return fail(AESFHE_EARG, "key of kind %d needs %zu words, got %lld", kind, want, (long long)words);
     aesfhe_key *k = calloc(1, sizeof *k);
     k->kind = kind;
     k->galois = galois;
     k->keyseed = keyseed;
+    k->ndig = ndig;
     k->data = malloc(sizeof(u64) * want);
     memcpy(k->data, in, sizeof(u64) * want);
     *out = k;
@@ -1545,6 +1568,10 @@ static u64 *ks_acc(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k) {
     u64 *acc = calloc((size_t)2 * ne * N, sizeof(u64));
     const int A = e->A;
     int beta = (l + 1 + A - 1) / A;
+    if (k->ndig > 0 && beta > k->ndig) {  /* a trimmed key used above its level: misuse, loudly */
+        fprintf(stderr, "ckks_oracle: key trimmed to %d digits switched at level %d (%d digits)\n", k->ndig, l, beta);
+        abort();
+    }
     for (int j = 0; j < beta; j++) {
         int lo = j * A, hi = lo + A < l + 1 ? lo + A : l + 1, na = hi - lo;
         u64 hatinv[MAXP], hat[MAXP][MAXP];

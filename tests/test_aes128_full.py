@@ -10,7 +10,7 @@ import pytest
 
 from aes_xor_fhe import aes_tables as T
 from aes_xor_fhe.aes_round_bits import AESRowRound, AESSlicedRound
-from aes_xor_fhe.bootstrap import Bootstrapper
+from aes_xor_fhe.bootstrap import Bootstrapper, trim_bootstrap_keys
 from aes_xor_fhe.fhe import Engine
 
 SCALE_BITS = 41
@@ -28,6 +28,7 @@ def _run(lib, log_n, nb=1, seed=3, cls=AESRowRound, cts_groups=(3,), key_levels=
     bs = []
     for g in cts_groups:  # later ones share the first's keys and SlotToCoeff plans, as in bench.py
         bs.append(Bootstrapper(e, sk, rlk, cts_groups=g, share=bs[0] if bs else None))
+    trim_bootstrap_keys(bs)  # bit refreshes only
     rng = np.random.default_rng(seed)
     key = np.frombuffer(FIPS_C1_KEY, dtype=np.uint8)
     blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)

@@ -124,6 +124,35 @@ def test_bootstrapper_share(oracle_lib):
         assert np.all(np.abs(e.decrypt(y, sk) - v) <= 1.24 * nz ** 2 + 1e-5)
 
 
+def test_trim_bootstrap_keys_residue_identical(oracle_lib):
+    """trim_bootstrap_keys on a 5-map CoeffToSlot bootstrapper alone (config 5's): the
+    SlotToCoeff-only rotation keys keep one digit of the three (L = 30, 12-prime digits);
+    bootstrap_bits then returns residue for residue what the untrimmed keys give (same engine seed,
+    same keys), the freed bytes are reported, general bootstrapping refuses, and a trimmed key
+    holds a third of a whole key's bytes.  (Beside a 3-map bootstrapper nothing is freed: its
+    CoeffToSlot uses the same rotations at the top levels.)"""
+    from aes_xor_fhe.bootstrap import trim_bootstrap_keys
+    outs = []
+    for trim in (False, True):
+        e, sk, pk, rlk = _engine(oracle_lib, max_level=30, scale_bits=40, special_primes=10, digit_primes=12)
+        b5 = Bootstrapper(e, sk, rlk, cts_groups=5)
+        if trim:
+            assert trim_bootstrap_keys([b5]) > 0
+            stc_only = {id(k) for p in b5.stc_bits for k in b5.plan_keys(p)} - \
+                       {id(k) for p in b5.cts + b5.cts_bits for k in b5.plan_keys(p)}
+            k = next(k for p in b5.stc_bits for k in b5.plan_keys(p) if id(k) in stc_only)
+            assert e.key_bytes(k) * 3 == e.key_bytes(b5.from_sparse)
+        rng = np.random.default_rng(8)
+        a, b = rng.choice([-1.0, 1.0], e.slot_count), rng.choice([-1.0, 1.0], e.slot_count)
+        ya, yb = b5.bootstrap_bits(e.encrypt(a, pk, level=5), e.encrypt(b, pk, level=5))
+        outs.append([e.export_residues(y) for y in (ya, yb)])
+        if trim:  # (after the encryptions above: this one draws encryption randomness too)
+            with pytest.raises(RuntimeError, match="trimmed"):
+                b5.bootstrap(e.encrypt(np.zeros(e.slot_count), pk, level=0))
+    for h, o in zip(*outs):
+        assert np.array_equal(h, o)
+
+
 @pytest.mark.parametrize("deg", [3, 7, 15, 29])
 def test_chebyshev_opt_depth_and_values(oracle_lib, deg):
     """chebyshev_opt (bootstrap.py): a random Chebyshev series of degree deg lands exactly
@@ -240,6 +269,26 @@ def test_bootstrap_bits_bit_exact_vs_oracle(product_lib, oracle_lib, gpu_availab
         g = e.bootstrap(e.encrypt(a + 0.5j * b, pk, level=0), rlk, bs.cjk,
                         _key_for(e, sk, bs))
         outs.append([e.export_residues(c) for c in (ya, yb, g)])
+    for h, o in zip(*outs):
+        assert np.array_equal(h, o)
+
+
+@pytest.mark.gpu
+def test_trimmed_keys_bit_exact_vs_oracle(product_lib, oracle_lib, gpu_available):
+    """Config 5's refresh path with the SlotToCoeff-only keys trimmed (trim_bootstrap_keys,
+    aesfhe_key_trim: device copy of the first digit, the old block back to the arena): HIP and
+    oracle residue for residue at the bench's chain, N = 2^10."""
+    from aes_xor_fhe.bootstrap import trim_bootstrap_keys
+    outs = []
+    for lib in (product_lib, oracle_lib):
+        e, sk, pk, rlk = _engine(lib, **BENCH_CHAIN)
+        bs = Bootstrapper(e, sk, rlk, cts_groups=5)
+        assert trim_bootstrap_keys([bs]) > 0
+        rng = np.random.default_rng(9)
+        a, b = rng.choice([-1.0, 1.0], e.slot_count), rng.choice([-1.0, 1.0], e.slot_count)
+        ya, yb = bs.bootstrap_bits(e.encrypt(a, pk, level=4), e.encrypt(b, pk, level=4))
+        outs.append([e.export_residues(c) for c in (ya, yb)])
+        assert np.abs(e.decrypt(ya, sk) - a).max() < 1e-2
     for h, o in zip(*outs):
         assert np.array_equal(h, o)
 

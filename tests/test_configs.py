@@ -139,7 +139,7 @@ def test_config4_full_batch_ten_rounds(product_lib, gpu_available, seed):
     3-map CoeffToSlot bootstrappers picked per refresh, 4 pairs per bootstrap call; every block
     checked against FIPS-197 and every round's input level against the schedule."""
     from aes_xor_fhe.aes_round_bits import AESSlicedRound
-    from aes_xor_fhe.bootstrap import Bootstrapper
+    from aes_xor_fhe.bootstrap import Bootstrapper, trim_bootstrap_keys
     from aes_xor_fhe.fhe import Engine, widest_digits
     alpha = widest_digits(**CONFIG4, lib=product_lib)
     assert alpha == 12
@@ -149,6 +149,7 @@ def test_config4_full_batch_ten_rounds(product_lib, gpu_available, seed):
     R = AESSlicedRound(e, sk, e.create_public_key(sk), rlk)
     bs5 = Bootstrapper(e, sk, rlk, cts_groups=5)
     bs = [bs5, Bootstrapper(e, sk, rlk, cts_groups=3, share=bs5)]  # as bench.py builds them
+    trim_bootstrap_keys(bs)
     L0 = R.fresh_level(e.max_level, bs)
     klv = R.key_levels(L0, bs)
     assert L0 == 25
