@@ -67,10 +67,10 @@ WORKLOAD = {
 SEED = 0x5EED5EED  # the CPU baseline's engine (reproducible); the GPU ranks share a 256-bit seed
 
 PEAK_FP64_TFLOPS = 78.6  # MI355X vector FP64 (AMD spec: 256 CUs x 128 FLOP/clk x 2.4 GHz)
-PMC_FILE = ROOT / "profiles" / "r04" / "pmc" / "round_traffic.json"
+PMC_FILE = ROOT / "profiles" / "r05" / "pmc" / "round_traffic.json"
 PMC_NOTE = ("HBM bytes per launch measured with rocprofv3 --pmc FETCH_SIZE (x2, the gfx950 "
             "correction of MI355X_MICROARCH.md) and --pmc WRITE_SIZE, separate passes, over exactly one "
-            "bench round step (tools/pmc_traffic.py -> profiles/r04/pmc/round_traffic.json, stamped "
+            "bench round step (tools/pmc_traffic.py -> profiles/r05/pmc/round_traffic.json, stamped "
             "with the git HEAD it measured and the hash of the kernel sources it ran)")
 # kernel instantiations (aesfhe_engine_profile_kernels labels "class.variant") -> the kernels they
 # launch.  EPI is k_nttf_rows_ks's epilogue template argument: 0 the canonical accumulators into acc,
@@ -78,18 +78,19 @@ PMC_NOTE = ("HBM bytes per launch measured with rocprofv3 --pmc FETCH_SIZE (x2, 
 # row pass of the accumulators written as raw doubles (dropped limbs: ModDown's INTT then runs only
 # its column pass).  PROD = the relinearisation of a ciphertext product (no tensor ciphertext).
 KERNEL_SYMBOLS = {
-    "ks_rows_fin.prod": "k_nttf_rows_ks<1, R, PROD=true, EPI=1> (kept limbs of a product's relinearisation: "
-                        "inner product + conv row pass + ModDown finish)",
-    "ks_rows_fin.ks": "k_nttf_rows_ks<1, R, PROD=false, EPI=1> (kept limbs of a plain key switch: relinearise / "
+    "ks_rows_fin.prod": "k_nttf_rows_ks_p<R, PROD=true, EPI=1> (kept limbs of a product's relinearisation: "
+                        "inner product + conv row pass + ModDown finish; LDS-DMA prefetch of the next digit)",
+    "ks_rows_fin.ks": "k_nttf_rows_ks_p<R, PROD=false, EPI=1> (kept limbs of a plain key switch: relinearise / "
                       "rotate / conjugate)",
-    "ks_rows_inner.prod": "k_nttf_rows_ks<1, R, PROD=true, EPI=2> (dropped limbs of a product's relinearisation; "
+    "ks_rows_inner.prod": "k_nttf_rows_ks_p<R, PROD=true, EPI=2> (dropped limbs of a product's relinearisation; "
                           "the accumulators leave as their inverse row pass, raw doubles)",
-    "ks_rows_inner.ks": "k_nttf_rows_ks<1, R, PROD=false, EPI=2> (dropped limbs of a plain key switch; raw-double "
+    "ks_rows_inner.ks": "k_nttf_rows_ks_p<R, PROD=false, EPI=2> (dropped limbs of a plain key switch; raw-double "
                         "inverse row pass)",
     "ks_rows_acc.ks": "k_nttf_rows_ks<1, R, PROD=false, EPI=0> (canonical accumulators of every limb)",
     "ntt_fwd_cols": "k_nttf_fwd_cols<R>",
-    "modup": "k_modup<A, 2>",
-    "moddown": "k_moddown<K + r>",
+    "modup": "k_bconv_mfma<NSTEP, VC=false> (i8 matrix-core ModUp)",
+    "moddown": "k_bconv_mfma<NSTEP, VC=true> (i8 matrix-core ModDown with the exact v slot)",
+    "bsgs_terms": "k_bsgs_terms<GM, BM, BB, PB> (BSGS term sums with the babies formed on the fly)",
     "poly2_int": "k_poly2_int_s<4, LAZY, BIG> / k_poly2_int (one call = the exact limbs + the 50-bit q_0 limb)",
 }
 NTT_TARGET = 0.5  # north_star: ">= 50% of HBM roofline on the NTT kernel"
