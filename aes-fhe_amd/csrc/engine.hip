@@ -3719,7 +3719,16 @@ static void poly2_int_impl(aesfhe_engine* e, const aesfhe_ct* const* xb, int32_t
                     int lb = la + 1;
                     while (lb < nl && is_big(lb) == big && (big || lazy_ok(lb) == lz)) lb++;
                     const dim3 grid(N / 256, lb - la, B);
-                    if (sbox) {
+                    // the folding limbs (q_0) with split inner sums when q < 2^51 (k_poly2_int_split)
+                    bool split = big;
+                    for (int li = la; li < lb; li++) split &= (double)e->chain.q[li] < 0x1p51;
+                    if (sbox && split) {
+                        hipLaunchKernelGGL(k_poly2_int_split<mo>, dim3(2 * N / 256, lb - la, B), dim3(256), 0, e->stream,
+                                           (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy,
+                                           (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, t0,
+                                           d3->d, (long)B * obs, obs, e->q, e->qinv, la, nl, e->logN, slab_rot);
+                        ps_.disp++;
+                    } else if (sbox) {
                         hipLaunchKernelGGL((big ? k_poly2_int_s<mo, false, true> : lz ? k_poly2_int_s<mo, true> : k_poly2_int_s<mo, false>), dim3(2 * N / 256, lb - la, B), dim3(256), 0, e->stream,
                                            (const u64* const*)dpx, (const long*)dsx, (const long*)dqx, nx, (const u64* const*)dpy, (const long*)dsy, (const long*)dqy,
                                            (const int*)dcx, (const int*)dcy, cxn, cyn, (const double*)dW, (const TwD*)dR, (const double*)dC0, t0,

@@ -1131,6 +1131,99 @@ __global__ void __launch_bounds__(256, 3) k_poly2_int_s(const u64* const* __rest
     }
 }
 
+// k_poly2_int_s for the limbs past the exact-FMA bound (the 50-bit q_0), the inner sums split
+// instead of folded: y' = yh 2^24 + yl (|yl| <= 2^23, |yh| <= 2^26: exact), so sum_j w_j yh_j and
+// sum_j w_j yl_j are exact fp64 FMA chains (row sums <= 512: below 2^35) and a = fmul_rem(ah, 2^24)
+// + al (|a| <= 1.5 q + 2^32 < 2^51).  16 + 16 FMAs and one remainder product per (output,
+// monomial, polynomial) instead of 16 remainder products with folds.  The two y polynomials run in
+// two passes over the monomials (one split y basis live: 60 VGPRs, not 120): pass 0 adds x_a a0
+// into d0 and x_b a0 into d1, pass 1 x_a a1 into d1 and x_b a1 into d2.  Same residues as the
+// folding kernel (every step exact mod q, canonical outputs).  grid (2 N/256, run, B) as
+// k_poly2_int_s (blocks b, b + 8: the two output blocks on one XCD).
+template <int MO>
+__global__ void __launch_bounds__(256, 3) k_poly2_int_split(const u64* const* __restrict__ xp, const long* __restrict__ xbs,
+                        const long* __restrict__ xps, int nx, const u64* const* __restrict__ yp,
+                        const long* __restrict__ ybs, const long* __restrict__ yps,
+                        const int* __restrict__ xstart, const int* __restrict__ ycls, int cxn,
+                        int cyn, const double* __restrict__ Wt, const TwD* __restrict__ Rt,
+                        const double* __restrict__ C0, int t0, u64* __restrict__ out, long oos, long obs,
+                        const u64* __restrict__ qs, const double* __restrict__ qinv, int l0, int nl,
+                        int logN, int orot) {
+    constexpr int NY = kPoly2Max;
+    constexpr double S = 16777216.0, Si = 1.0 / 16777216.0;  // 2^24
+    const int bx = blockIdx.x, half = (bx >> 3) & 1;
+    const int k = (((bx >> 4) << 3) | (bx & 7)) * blockDim.x + threadIdx.x;
+    const int l = l0 + blockIdx.y, bb = blockIdx.z;
+    t0 += half * MO;
+    const double q = (double)qs[l], qi = qinv[l], sq = S * qi;
+    const long off = ((long)l << logN) + k;
+    const TwD* Rl = Rt + (size_t)l * cxn * cyn;
+    double d0[MO], d1[MO], d2[MO];
+#pragma unroll
+    for (int t = 0; t < MO; t++) d0[t] = d1[t] = d2[t] = 0.0;
+#pragma unroll 1
+    for (int p = 0; p < 2; p++) {
+        double yh[NY - 1], yl[NY - 1];
+#pragma unroll 1
+        for (int c = 0; c < cxn; c++) {
+            const TwD* Rc = Rl + c * cyn;
+#pragma unroll
+            for (int j = 0; j < NY - 1; j++) {  // y' = H(c, cy(j)) y_j, reduced, split at 2^24
+                const u64* yq = yp[j] + (long)bb * ybs[j] + off + (p ? yps[j] : 0);
+                const TwD r = Rc[ycls[j + 1]];
+                const double v = fred(fmul_rem_r(u2d(*yq), r.w, r.wq, q), q, qi);
+                yh[j] = __builtin_rint(v * Si);
+                yl[j] = __builtin_fma(-yh[j], S, v);
+            }
+            const double c0 = p ? 0.0 : C0[(size_t)l * cxn + c];  // the x^0 term: polynomial 0 only
+            const double c0h = __builtin_rint(c0 * Si), c0l = __builtin_fma(-c0h, S, c0);
+#pragma unroll 1
+            for (int i = xstart[c]; i < xstart[c + 1]; i++) {  // class 0: i = 0, the x^0 term
+                double xa = 1.0, xb = 0.0;  // x^0: (1, 0)
+                if (i > 0) {
+                    const u64* xq = xp[i - 1] + (long)bb * xbs[i - 1] + off;
+                    xa = u2d(xq[0]);
+                    xb = u2d(xq[xps[i - 1]]);
+                }
+#pragma unroll
+                for (int t = 0; t < MO; t++) {
+                    const double* w = Wt + ((size_t)(t0 + t) * nx + i) * NY;
+                    double ah = w[0] * c0h, al = w[0] * c0l;
+#pragma unroll
+                    for (int j = 1; j < NY; j++) {
+                        ah = __builtin_fma(w[j], yh[j - 1], ah);
+                        al = __builtin_fma(w[j], yl[j - 1], al);
+                    }
+                    const double a = fmul_rem(ah, S, sq, q) + al, aq = a * qi;
+                    if (i == 0) {  // x^0: a itself
+                        if (p == 0) d0[t] += a;
+                        else d1[t] += a;
+                    } else if (p == 0) {
+                        d0[t] += fmul_rem(xa, a, aq, q);
+                        d1[t] += fmul_rem(xb, a, aq, q);
+                    } else {
+                        d1[t] += fmul_rem(xa, a, aq, q);
+                        d2[t] += fmul_rem(xb, a, aq, q);
+                    }
+                    d0[t] = fred(d0[t], q, qi);
+                    d1[t] = fred(d1[t], q, qi);
+                    d2[t] = fred(d2[t], q, qi);
+                }
+            }
+        }
+    }
+    const int ob = (bb & ~3) | ((bb - orot) & 3);  // aesfhe_poly2_int_rot
+    u64* o = out + (long)ob * obs + off;
+    const long pstr = (long)nl << logN;
+#pragma unroll
+    for (int t = 0; t < MO; t++) {
+        u64* ot = o + (long)(t0 + t) * oos;
+        ot[0] = fcanon(d0[t], q, qi);
+        ot[pstr] = fcanon(d1[t], q, qi);
+        ot[2 * pstr] = fcanon(d2[t], q, qi);
+    }
+}
+
 // ModRaise: x = limb 0 of every polynomial in coefficient form (mod q_0); out limb i =
 // centred x mod q_i for i < nl.  x: [P][N] (P = B * npoly), out: [P][nl][N].  grid (N/256, nl, P)
 __global__ void k_lift0(const u64* __restrict__ x, u64* __restrict__ out, int nl, u64 q0,
