@@ -875,6 +875,11 @@ extern "C" int aesfhe_engine_create(const aesfhe_params* pp, aesfhe_engine** out
     // arena chunks of 16384 limbs (8 GiB at N = 2^16), at least 256 MiB; AESFHE_ARENA_CHUNK_MB
     // overrides it (several engines sharing one GPU, small batches)
     e->pool.chunk_bytes = std::max((size_t)1 << 28, ((size_t)16384 * 8) << e->logN);
+    if (e->logN == 16) {  // the bench ring: first fit in 4 GiB chunks, cap 1.2 (arena.h)
+        e->pool.chunk_bytes = (size_t)8192 * 8 << e->logN;
+        e->pool.first_fit = true;
+        e->pool.grow_cap = 1.2;
+    }
     if (const char* cm = getenv("AESFHE_ARENA_CHUNK_MB")) {
         const long mb = atol(cm);
         if (mb > 0) e->pool.chunk_bytes = (size_t)mb << 20;

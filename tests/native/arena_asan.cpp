@@ -25,9 +25,10 @@ static int fail(const char* what, long step) {
     return 1;
 }
 
-int main() {
+int main(int argc, char** argv) {
     Counts cnt;
     Arena a;
+    a.first_fit = argc > 1 && std::strcmp(argv[1], "first_fit") == 0;  // the placement the engine takes at N = 2^16
     a.A.alloc = [](size_t n, void* c) -> void* {
         auto* k = (Counts*)c;
         if (n > k->fail_above) return nullptr;
@@ -143,6 +144,7 @@ int main() {
         if (b.held != 0) return fail("cap: trim", steps);
     }
     if (cnt.allocs != cnt.frees) return fail("allocator calls unbalanced (cap)", steps);
-    std::printf("arena_asan ok: %ld steps, %ld chunk allocations, peak live %zu bytes\n", steps, cnt.allocs, peak);
+    std::printf("arena_asan ok (%s): %ld steps, %ld chunk allocations, peak live %zu bytes\n", a.first_fit ? "first fit" : "best fit",
+                steps, cnt.allocs, peak);
     return 0;
 }

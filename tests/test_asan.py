@@ -42,11 +42,12 @@ def test_oracle_chacha_kat(tmp_path):
 
 
 def test_device_arena_asan(tmp_path):
-    """The engine's device arena (aes-fhe_amd/csrc/arena.h: best fit, neighbour merge, zero-copy
+    """The engine's device arena (aes-fhe_amd/csrc/arena.h: best fit and first fit, neighbour merge, zero-copy
     split, trim, peak_live / fragmentation counters) over malloc under ASan + UBSan, against a
     shadow model (tests/native/arena_asan.cpp)."""
     exe = tmp_path / "arena_asan"
     subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
                     "-o", str(exe), str(ROOT / "tests" / "native" / "arena_asan.cpp")], check=True)
-    r = subprocess.run([str(exe)], env=ENV, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0 and "arena_asan ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+    for mode in ([], ["first_fit"]):
+        r = subprocess.run([str(exe)] + mode, env=ENV, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "arena_asan ok" in r.stdout, (mode, r.stdout[-2000:], r.stderr[-4000:])

@@ -52,6 +52,7 @@ struct Policy {
     int fit = 0;         // 0 best fit (arena.h), 1 address-ordered first fit, 2 best fit from the top of a chunk
     size_t big = 0;      // blocks >= big: exact-size cache (reused only by the same size), 0 off
     bool clamp = false;  // new chunks clamped to cap x peak_live - held (never below the request)
+    int buckets = 0;     // > 0: one arena per size class (0.25 / 1 / 4 GB boundaries, up to 4 classes)
 };
 
 // arena.h with another placement rule (replay only)
@@ -72,6 +73,29 @@ struct ArenaX : Arena {
             grow_cap = cap;
         }
         if (fit == 0) return get(bytes);
+        if (fit == 5) {  // arena.h's own first-fit mode
+            first_fit = true;
+            return get(bytes);
+        }
+        if (fit == 4) {  // best fit, but a chunk made for one big request (> chunk_bytes) only serves requests >= half its size
+            for (auto f = free_size_.lower_bound(n); f != free_size_.end(); ++f) {
+                char* ch = chunk_of(f->second);
+                const size_t cs = chunks_[ch];
+                if (cs > chunk_bytes && 2 * n < cs) continue;
+                char* p = f->second;
+                const size_t have = f->first;
+                free_size_.erase(f);
+                free_addr_.erase(p);
+                if (have > n) add_free(p + n, have - n);
+                live_[p] = n;
+                live += n;
+                peak_live = std::max(peak_live, live);
+                return p;
+            }
+            // none: a new chunk (whole chunk_bytes, or the request alone when larger / capped)
+            if (!new_chunk(n)) return nullptr;
+            return getx(bytes);
+        }
         std::map<char*, size_t>::iterator it = free_addr_.end();
         if (fit == 1) {
             for (auto f = free_addr_.begin(); f != free_addr_.end(); ++f)
@@ -112,6 +136,7 @@ int main(int argc, char** argv) {
     const size_t G = 1ULL << 30;
     const Policy pols[] = {
         {"now: 8G chunks, cap 1.2, two arenas", 8 * G, 1.2, 0, true},
+        {"engine N=2^16: first fit (arena.h), 4G, cap 1.2", 4 * G, 1.2, 0, false, 5},
         {"cap 1.1", 8 * G, 1.1, 0, true},
         {"cap 1.05", 8 * G, 1.05, 0, true},
         {"cap 1.0", 8 * G, 1.0, 0, true},
@@ -133,10 +158,20 @@ int main(int argc, char** argv) {
         {"one, clamp 1.05, first fit", 8 * G, 1.05, 0, false, 1, 0, true},
         {"one, first fit", 8 * G, 1.2, 0, false, 1},
         {"one, first fit, 4G", 4 * G, 1.2, 0, false, 1},
+        {"one, first fit, 16G", 16 * G, 1.2, 0, false, 1},
+        {"one, first fit, cap 1.1", 8 * G, 1.1, 0, false, 1},
+        {"one, first fit, 16G, cap 1.1", 16 * G, 1.1, 0, false, 1},
         {"two, big >= 2G exact cache", 8 * G, 1.2, 0, true, 0, 2 * G},
         {"one, big >= 2G exact cache", 8 * G, 1.2, 0, false, 0, 2 * G},
         {"one, first fit, big >= 2G cache", 8 * G, 1.2, 0, false, 1, 2 * G},
         {"one, first fit, big >= 4G cache", 8 * G, 1.2, 0, false, 1, 4 * G},
+        {"one, big chunks reserved, cap 1.1", 8 * G, 1.1, 0, false, 4},
+        {"one, big chunks reserved, cap 1.2", 8 * G, 1.2, 0, false, 4},
+        {"one, big chunks reserved, 4G, cap 1.1", 4 * G, 1.1, 0, false, 4},
+        {"size classes, 8G, clamp 1.1", 8 * G, 1.1, 0, false, 0, 0, true, 4},
+        {"size classes, 8G, cap 1.2", 8 * G, 1.2, 0, false, 0, 0, false, 4},
+        {"size classes, 4G, clamp 1.1", 4 * G, 1.1, 0, false, 0, 0, true, 4},
+        {"size classes, first fit, 8G", 8 * G, 1.1, 0, false, 1, 0, true, 4},
     };
     for (int a = 1; a < argc; a++) {
         const auto ev = load(argv[a]);
@@ -150,7 +185,7 @@ int main(int argc, char** argv) {
                                   return p;
                               },
                               [](void*, void*) {}, [](void*) {}, &fk};
-            ArenaX ar[2];
+            ArenaX ar[4];
             for (auto& x : ar) x.A = al, x.chunk_bytes = pol.chunk, x.grow_cap = pol.cap, x.fit = pol.fit, x.clamp = pol.clamp;
             // exact-size cache for big blocks: free blocks by size; held = every block ever made
             std::multimap<size_t, char*> bigfree;
@@ -159,7 +194,9 @@ int main(int argc, char** argv) {
             std::unordered_map<unsigned long long, std::pair<int, char*>> map;
             size_t peak_total = 0, max_held = 0;
             for (const auto& e : ev) {
-                const int k = pol.two && e.tag == 't' ? 1 : 0;
+                int k = pol.two && e.tag == 't' ? 1 : 0;
+                if (pol.buckets && e.op == 'g')
+                    k = e.n < (G >> 2) ? 0 : e.n < G ? 1 : e.n < 4 * G ? 2 : 3;
                 if (e.op == 'g') {
                     if (pol.exact_round) {  // emulate rounding of exact chunks: pre-grow by the rounded need
                         Arena& A = ar[k];
@@ -189,7 +226,7 @@ int main(int argc, char** argv) {
                         }
                         biglive[p] = e.n;
                         biglivesz += e.n;
-                        map[e.p] = {2, p};
+                        map[e.p] = {9, p};
                     } else {
                         char* p = (char*)ar[k].getx(e.n);
                         map[e.p] = {k, p};
@@ -197,7 +234,7 @@ int main(int argc, char** argv) {
                 } else if (e.op == 'p') {
                     auto it = map.find(e.p);
                     if (it == map.end()) continue;
-                    if (it->second.first == 2) {
+                    if (it->second.first == 9) {
                         const size_t n = biglive[it->second.second];
                         biglive.erase(it->second.second);
                         biglivesz -= n;
@@ -211,17 +248,17 @@ int main(int argc, char** argv) {
                     if (it == map.end()) continue;
                     const int kk = it->second.first;
                     char* base = it->second.second;
-                    if (kk == 2) continue;  // (big blocks are never split in the traces)
+                    if (kk == 9) continue;  // (big blocks are never split in the traces)
                     ar[kk].split(base, e.parts, e.n);
                     for (int t = 0; t < e.parts; t++) map[e.p + (unsigned long long)t * e.n] = {kk, base + (size_t)t * e.n};
                 }
-                peak_total = std::max(peak_total, ar[0].live + ar[1].live + biglivesz);
-                max_held = std::max(max_held, ar[0].held + ar[1].held + bigheld);
+                peak_total = std::max(peak_total, ar[0].live + ar[1].live + ar[2].live + ar[3].live + biglivesz);
+                max_held = std::max(max_held, ar[0].held + ar[1].held + ar[2].held + ar[3].held + bigheld);
             }
-            const size_t held = ar[0].held + ar[1].held + bigheld;
+            const size_t held = ar[0].held + ar[1].held + ar[2].held + ar[3].held + bigheld;
             printf("  %-36s held %6.1f GB (max %6.1f)  peak live %6.1f GB  held/peak %.3f  mallocs %lld\n", pol.name, held / 1e9,
                    max_held / 1e9, peak_total / 1e9, (double)held / (double)std::max<size_t>(1, peak_total),
-                   (long long)(ar[0].mallocs + ar[1].mallocs));
+                   (long long)(ar[0].mallocs + ar[1].mallocs + ar[2].mallocs + ar[3].mallocs));
         }
     }
     return 0;
