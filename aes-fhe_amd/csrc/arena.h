@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <iterator>
 #include <map>
+#include <utility>
 #include <unordered_map>
 
 namespace aesfhe {
@@ -48,6 +49,13 @@ struct Arena {
     std::map<char*, size_t> chunks_;                  // base -> size
     std::map<char*, size_t> free_addr_;               // free block -> size (address order)
     std::multimap<size_t, char*> free_size_;          // size -> free block (best fit)
+    // first fit walks the free blocks in chunk-creation order, then by address within a chunk:
+    // device addresses of later chunks may lie below earlier ones, and an address-ordered walk
+    // would then fill the newest chunk first (measured: 1.87x held over peak on the GPU against
+    // the replay's 1.27x, whose fake allocator hands out rising addresses)
+    std::map<char*, uint64_t> chunk_seq_;
+    std::map<std::pair<uint64_t, char*>, size_t> free_ff_;
+    uint64_t next_seq_ = 0;
     std::unordered_map<void*, size_t> live_;          // live block -> size
     size_t held = 0, live = 0, peak_live = 0;
     int64_t mallocs = 0, trims = 0, reuse_larger = 0;  // reuse_larger: blocks split off a larger free one
@@ -58,9 +66,11 @@ struct Arena {
     void add_free(char* p, size_t n) {
         free_addr_[p] = n;
         free_size_.insert({n, p});
+        if (first_fit) free_ff_[{chunk_seq_[chunk_of(p)], p}] = n;
     }
     void del_free(char* p, size_t n) {
         free_addr_.erase(p);
+        if (first_fit) free_ff_.erase({chunk_seq_[chunk_of(p)], p});
         auto r = free_size_.equal_range(n);
         for (auto it = r.first; it != r.second; ++it)
             if (it->second == p) {
@@ -91,6 +101,7 @@ struct Arena {
         mallocs++;
         held += want;
         chunks_[(char*)p] = want;
+        chunk_seq_[(char*)p] = next_seq_++;
         add_free((char*)p, want);
         return true;
     }
@@ -100,15 +111,15 @@ struct Arena {
         char* p = nullptr;
         size_t have = 0;
         if (first_fit) {
-            auto f = free_addr_.begin();
-            for (; f != free_addr_.end() && f->second < n; ++f) {
+            auto f = free_ff_.begin();
+            for (; f != free_ff_.end() && f->second < n; ++f) {
             }
-            if (f == free_addr_.end()) {
+            if (f == free_ff_.end()) {
                 if (!new_chunk(n)) return nullptr;
-                for (f = free_addr_.begin(); f->second < n; ++f) {
+                for (f = free_ff_.begin(); f->second < n; ++f) {
                 }
             }
-            p = f->first;
+            p = f->first.second;
             have = f->second;
             del_free(p, have);
         } else {
@@ -171,6 +182,7 @@ struct Arena {
                 del_free(it->first, it->second);
                 A.release(it->first, A.ctx);
                 held -= it->second;
+                chunk_seq_.erase(it->first);
                 it = chunks_.erase(it);
             } else {
                 ++it;
@@ -204,6 +216,8 @@ struct Arena {
         chunks_.clear();
         free_addr_.clear();
         free_size_.clear();
+        chunk_seq_.clear();
+        free_ff_.clear();
         live_.clear();
         held = live = 0;
     }

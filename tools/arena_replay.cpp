@@ -125,7 +125,7 @@ struct ArenaX : Arena {
 };
 
 struct Fake {
-    unsigned long long next = 1ULL << 40;
+    unsigned long long next = 1ULL << 46;
 };
 
 int main(int argc, char** argv) {
@@ -178,10 +178,17 @@ int main(int argc, char** argv) {
         printf("%s: %zu events\n", argv[a], ev.size());
         for (const auto& pol : pols) {
             Fake fk;
+            // REPLAY_ADDR=down: each new chunk below the previous ones (device addresses need not rise)
+            static const bool down = getenv("REPLAY_ADDR") && !strcmp(getenv("REPLAY_ADDR"), "down");
             ArenaAllocator al{[](size_t n, void* ctx) -> void* {
                                   auto* f = (Fake*)ctx;
+                                  const size_t r = (n + 4095) & ~(size_t)4095;
+                                  if (down) {
+                                      f->next -= r;
+                                      return (void*)f->next;
+                                  }
                                   void* p = (void*)f->next;
-                                  f->next += (n + 4095) & ~(size_t)4095;
+                                  f->next += r;
                                   return p;
                               },
                               [](void*, void*) {}, [](void*) {}, &fk};
