@@ -137,6 +137,14 @@ int main(int argc, char** argv) {
     const Policy pols[] = {
         {"now: 8G chunks, cap 1.2, two arenas", 8 * G, 1.2, 0, true},
         {"engine N=2^16: first fit (arena.h), 4G, cap 1.2", 4 * G, 1.2, 0, false, 5},
+        {"ff(seq) 2G cap 1.2", 2 * G, 1.2, 0, false, 5},
+        {"ff(seq) 3G cap 1.2", 3 * G, 1.2, 0, false, 5},
+        {"ff(seq) 6G cap 1.2", 6 * G, 1.2, 0, false, 5},
+        {"ff(seq) 4G cap 1.1", 4 * G, 1.1, 0, false, 5},
+        {"ff(seq) 4G cap 1.3", 4 * G, 1.3, 0, false, 5},
+        {"ff(seq) 4G no cap", 4 * G, 0.0, 0, false, 5},
+        {"ff(seq) 8G cap 1.2", 8 * G, 1.2, 0, false, 5},
+        {"ff(seq) 16G cap 1.1", 16 * G, 1.1, 0, false, 5},
         {"cap 1.1", 8 * G, 1.1, 0, true},
         {"cap 1.05", 8 * G, 1.05, 0, true},
         {"cap 1.0", 8 * G, 1.0, 0, true},
