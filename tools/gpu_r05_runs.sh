@@ -29,5 +29,5 @@ while IFS='|' read -r name envs args; do
   env $envs timeout -k 10 600 python -u bench.py $args > gpurun_out/${TAG}_${name}.json 2> gpurun_out/${TAG}_${name}.err; rc=$?
   fatal $rc "bench $name"
   [ $rc -ne 0 ] && { tail -20 gpurun_out/${TAG}_${name}.err; continue; }
-  python3 tools/brief.py gpurun_out/${TAG}_${name}.json "$name" modup moddown ks_rows_fin ntt_fwd_cols bsgs dot_pt ks_inner
+  python3 tools/brief.py gpurun_out/${TAG}_${name}.json "$name" ${BRIEF:-modup moddown ks_rows_fin ntt_fwd_cols bsgs dot_pt ks_inner}
 done <<< "$RUNS"
