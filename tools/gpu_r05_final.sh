@@ -15,4 +15,6 @@ if [ -z "$NO_BENCH" ]; then
   python3 tools/brief.py gpurun_out/${T}_bench.json bench ks_rows_fin ntt_fwd_cols poly2 modup moddown
 fi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof -o round -- python3 bench.py --steps 5 --warmup 1 --aes10-batch 0 --no-configs --no-harness --client-batch 0 --no-cpu-baseline --config5 off > gpurun_out/${T}_prof.json 2> gpurun_out/${T}_prof.err \
- && rm -f gpurun_out/${T}_prof/*_kernel_trace.csv && echo "round profiled"
+ && rm -f gpurun_out/${T}_prof/*_kernel_trace.csv && echo "round profiled" \
+ && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_aprof -o aes10 -- python3 bench.py --steps 1 --warmup 0 --profile-steps 0 --no-configs --no-harness --client-batch 0 --no-cpu-baseline --config5 off > gpurun_out/${T}_aprof.json 2> gpurun_out/${T}_aprof.err \
+ && rm -f gpurun_out/${T}_aprof/*_kernel_trace.csv && echo "ten rounds profiled"
