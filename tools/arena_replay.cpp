@@ -53,12 +53,14 @@ struct Policy {
     size_t big = 0;      // blocks >= big: exact-size cache (reused only by the same size), 0 off
     bool clamp = false;  // new chunks clamped to cap x peak_live - held (never below the request)
     int buckets = 0;     // > 0: one arena per size class (0.25 / 1 / 4 GB boundaries, up to 4 classes)
+    size_t thr = 0;      // fit 6 / 7: blocks >= thr placed from the top of a free block
 };
 
 // arena.h with another placement rule (replay only)
 struct ArenaX : Arena {
     int fit = 0;
     bool clamp = false;
+    size_t thr = 0;
     void* getx(size_t bytes) {
         const size_t n = round_up(bytes);
         if (clamp && free_size_.lower_bound(n) == free_size_.end() && peak_live > 0) {
@@ -71,6 +73,46 @@ struct ArenaX : Arena {
             new_chunk(n);
             chunk_bytes = cb;
             grow_cap = cap;
+        }
+        if (fit == 6 || fit == 7) {  // two-ended first fit (creation order): blocks >= thr from the top
+            first_fit = true;
+            const bool big = n >= thr;
+            std::map<std::pair<uint64_t, char*>, size_t>::iterator f = free_ff_.end();
+            auto find = [&] {
+                f = free_ff_.end();
+                if (big && fit == 7) {  // big ones: the newest chunk first
+                    for (auto r = free_ff_.rbegin(); r != free_ff_.rend(); ++r)
+                        if (r->second >= n) {
+                            f = std::prev(r.base());
+                            break;
+                        }
+                } else {
+                    for (auto g = free_ff_.begin(); g != free_ff_.end(); ++g)
+                        if (g->second >= n) {
+                            f = g;
+                            break;
+                        }
+                }
+            };
+            find();
+            if (f == free_ff_.end()) {
+                if (!new_chunk(n)) return nullptr;
+                find();
+            }
+            char* b = f->first.second;
+            const size_t have = f->second;
+            del_free(b, have);
+            char* p = b;
+            if (big) {
+                p = b + (have - n);
+                if (have > n) add_free(b, have - n);
+            } else if (have > n) {
+                add_free(b + n, have - n);
+            }
+            live_[p] = n;
+            live += n;
+            peak_live = std::max(peak_live, live);
+            return p;
         }
         if (fit == 0) return get(bytes);
         if (fit == 5) {  // arena.h's own first-fit mode
@@ -137,6 +179,20 @@ int main(int argc, char** argv) {
     const Policy pols[] = {
         {"now: 8G chunks, cap 1.2, two arenas", 8 * G, 1.2, 0, true},
         {"engine N=2^16: first fit (arena.h), 4G, cap 1.2", 4 * G, 1.2, 0, false, 5},
+        {"two-ended ff, big >= 256M, 4G cap 1.2", 4 * G, 1.2, 0, false, 6, 0, false, 0, G / 4},
+        {"two-ended ff, big >= 1G, 4G cap 1.2", 4 * G, 1.2, 0, false, 6, 0, false, 0, G},
+        {"two-ended ff, big >= 64M, 4G cap 1.2", 4 * G, 1.2, 0, false, 6, 0, false, 0, G / 16},
+        {"two-ended ff, big >= 256M, 8G cap 1.2", 8 * G, 1.2, 0, false, 6, 0, false, 0, G / 4},
+        {"two-ended ff, big >= 256M, 4G cap 1.1", 4 * G, 1.1, 0, false, 6, 0, false, 0, G / 4},
+        {"two-ended, big newest-first >= 256M, 4G", 4 * G, 1.2, 0, false, 7, 0, false, 0, G / 4},
+        {"two-ended, big newest-first >= 1G, 4G", 4 * G, 1.2, 0, false, 7, 0, false, 0, G},
+        {"two-ended ff, big >= 4G, 16G cap 1.1", 16 * G, 1.1, 0, false, 6, 0, false, 0, 4 * G},
+        {"two-ended ff, big >= 8G, 16G cap 1.1", 16 * G, 1.1, 0, false, 6, 0, false, 0, 8 * G},
+        {"two-ended ff, big >= 2G, 32G cap 1.1", 32 * G, 1.1, 0, false, 6, 0, false, 0, 2 * G},
+        {"two-ended ff, big >= 8G, 32G cap 1.1", 32 * G, 1.1, 0, false, 6, 0, false, 0, 8 * G},
+        {"ff(seq) 32G cap 1.1", 32 * G, 1.1, 0, false, 5},
+        {"ff(seq) 64G cap 1.1", 64 * G, 1.1, 0, false, 5},
+        {"ff(seq) 32G cap 1.05", 32 * G, 1.05, 0, false, 5},
         {"ff(seq) 2G cap 1.2", 2 * G, 1.2, 0, false, 5},
         {"ff(seq) 3G cap 1.2", 3 * G, 1.2, 0, false, 5},
         {"ff(seq) 6G cap 1.2", 6 * G, 1.2, 0, false, 5},
@@ -201,7 +257,7 @@ int main(int argc, char** argv) {
                               },
                               [](void*, void*) {}, [](void*) {}, &fk};
             ArenaX ar[4];
-            for (auto& x : ar) x.A = al, x.chunk_bytes = pol.chunk, x.grow_cap = pol.cap, x.fit = pol.fit, x.clamp = pol.clamp;
+            for (auto& x : ar) x.A = al, x.chunk_bytes = pol.chunk, x.grow_cap = pol.cap, x.fit = pol.fit, x.clamp = pol.clamp, x.thr = pol.thr;
             // exact-size cache for big blocks: free blocks by size; held = every block ever made
             std::multimap<size_t, char*> bigfree;
             std::unordered_map<char*, size_t> biglive;
