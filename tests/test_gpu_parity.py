@@ -440,6 +440,29 @@ def test_poly2_int_sbox_shape_bit_exact(product_lib, oracle_lib, gpu_available, 
         _same(g, o, a, b)
 
 
+@pytest.mark.parametrize("scale_bits", [40, 44], ids=["s40", "s44"])
+def test_poly2_int_aes_sbox_weights_bit_exact(product_lib, oracle_lib, gpu_available, scale_bits):
+    """aesfhe_poly2_int with exactly the AES S-box's Walsh weights (64 W, den 64, 8 outputs: the
+    bench round's call, aes_round_bits.walsh_sbox) on +-1 bit inputs: residue for residue against
+    the oracle at N = 2^16 with mixed basis levels, a slab rotation, and q_0 on the split kernel
+    (reference: the S-box the bit-sliced round evaluates, sbox/sbox_service.py:116-138)."""
+    from aes_xor_fhe.aes_round_bits import walsh_sbox
+    W = np.rint(walsh_sbox() * 64).astype(np.int64)
+    kw = dict(log_n=16, max_level=7, special_primes=3, seed=43, scale_bits=scale_bits)
+    g, o = _pair(product_lib, oracle_lib, **kw)
+    rng = np.random.default_rng(16)
+    zx = rng.choice([-1.0, 1.0], (4, g.slot_count))
+    zy = rng.choice([-1.0, 1.0], (4, g.slot_count))
+    res = []
+    for eng in (g, o):
+        k = _keys(eng)
+        xb = eng.make_power_basis(eng.encrypt(zx, k["pk"], level=6), 15, k["rlk"])
+        yb = eng.make_power_basis(eng.encrypt(zy, k["pk"], level=6), 15, k["rlk"])
+        res.append(eng.poly2_int(xb, yb, W, 64, k["rlk"], slab_rot=1))
+    for a, b in zip(*res):
+        _same(g, o, a, b)
+
+
 @pytest.mark.parametrize("kw", [SMALL, dict(log_n=16, max_level=6, special_primes=3, seed=13)],
                          ids=["n4096", "n65536"])
 def test_cyclic_broadcast_mul_bit_exact(product_lib, oracle_lib, gpu_available, kw):
