@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
 #include <vector>
 
@@ -24,7 +25,22 @@
 using namespace aesfhe;
 #define HC(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-constexpr int LOGN = 16, N = 1 << LOGN, NS = 12, NT = 24, B = 32;
+#ifndef BC_NT
+#define BC_NT 24
+#endif
+#ifndef BC_SL
+#define BC_SL BC_NS_DEFAULT
+#endif
+// BC_NT targets; BC_SL / BC_DL: limbs per batch element of the source / destination buffers, and
+// BC_SKIP the digit's own limbs skipped in the destination (the round's digit 0 at l = 30:
+// -DBC_NT=29 -DBC_SL=31 -DBC_DL=41 -DBC_SKIP=12)
+#define BC_NS_DEFAULT 12
+constexpr int LOGN = 16, N = 1 << LOGN, NS = 12, NT = BC_NT, B = 32;
+#ifdef BC_DL
+constexpr int SL = BC_SL, DL = BC_DL, SKIP = BC_SKIP;
+#else
+constexpr int SL = NS, DL = NT, SKIP = 0;
+#endif
 
 template <bool NTS, int PASSES>
 __global__ __launch_bounds__(256) void k_skel(const u64* __restrict__ src, u64* __restrict__ dst) {
@@ -60,7 +76,7 @@ __global__ void k_copy(const v2u* __restrict__ a, v2u* __restrict__ b, long n, l
 
 int main() {
     u64 *src, *dst;
-    const size_t sb = (size_t)B * NS * N * 8, db = (size_t)B * NT * N * 8;
+    const size_t sb = (size_t)B * SL * N * 8, db = (size_t)B * DL * N * 8;
     HC(hipMalloc(&src, sb));
     HC(hipMalloc(&dst, db));
     HC(hipMemset(src, 1, sb));
@@ -118,11 +134,26 @@ int main() {
         HC(hipMemcpy(dq, q.data(), np * 8, hipMemcpyHostToDevice));
         HC(hipMemset(src, 0, sb));  // canonical inputs
         BconvArgs a{};
-        a.src = src, a.sbs = (long)NS * N, a.scs = 0, a.dst = dst, a.dbs = (long)NT * N, a.dcs = 0, a.nc = 1, a.ns = NS;
-        a.s_nq = NS, a.s_q0 = 30, a.s_p0 = 0, a.sinvf = dsinvf, a.einv = dsinvf, a.nt = NT, a.skip0 = NT, a.skipn = 0;
+        a.src = src, a.sbs = (long)SL * N, a.scs = 0, a.dst = dst, a.dbs = (long)DL * N, a.dcs = 0, a.nc = 1, a.ns = NS;
+        a.s_nq = NS, a.s_q0 = 30, a.s_p0 = 0, a.sinvf = dsinvf, a.einv = dsinvf, a.nt = NT, a.skip0 = SKIP ? 0 : NT, a.skipn = SKIP;
         a.tl_l = 1000, a.Lp1 = 0, a.tab = dtab, a.corr = dcorr, a.pc = dpc, a.qall = dq, a.qinvall = dqinv;
         a.tiles_per_group = (NT + 3) / 4;
         timeit("mfma", [&] { hipLaunchKernelGGL((k_bconv_mfma<3, false>), dim3(N / 256, 1, B), dim3(256), 0, 0, a, LOGN); });
+        {  // the same on random canonical words (< 2^40, every q above): the kernel's power draw, and so
+           // the clock it holds, depends on its data (MI355X_MICROARCH.md 'DVFS give-back')
+            std::vector<u64> h((size_t)B * SL * N);
+            uint64_t x = 88172645463325252ULL;
+            for (auto& v : h) {
+                x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+                v = x & ((1ULL << 40) - 1);
+                if (v >= (1ULL << 40) - 256) v -= 256;
+            }
+            HC(hipMemcpy(src, h.data(), sb, hipMemcpyHostToDevice));
+            timeit("mfma_rnd", [&] { hipLaunchKernelGGL((k_bconv_mfma<3, false>), dim3(N / 256, 1, B), dim3(256), 0, 0, a, LOGN); });
+            timeit("cur_rnd", [&] { hipLaunchKernelGGL((k_skel<true, 1>), dim3(N / 256, 1, B), dim3(256), 0, 0, src, dst); });
+            HC(hipMemset(src, 0, sb));
+            timeit("mfma_0", [&] { hipLaunchKernelGGL((k_bconv_mfma<3, false>), dim3(N / 256, 1, B), dim3(256), 0, 0, a, LOGN); });
+        }
         for (int tg = 1; tg <= 3; tg++) {  // target groups split over blockIdx.y (more, shorter workgroups)
             a.tiles_per_group = (NT / 4 + tg - 1) / tg;
             char nm[32];
