@@ -42,7 +42,7 @@ class Params(C.Structure):
 
 # (name, restype, argtypes) for every symbol of include/aesfhe.h
 _P = C.POINTER
-ABI_VERSION = 4  # include/aesfhe.h AESFHE_ABI_VERSION
+ABI_VERSION = 5  # include/aesfhe.h AESFHE_ABI_VERSION
 
 SIGNATURES = [
     ("aesfhe_last_error", C.c_char_p, []),

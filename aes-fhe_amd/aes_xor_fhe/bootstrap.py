@@ -125,6 +125,15 @@ class Bootstrapper:
         self.rlk = rlk
         if share is not None and share.e is not engine:
             raise ValueError("Bootstrapper(share=...) needs a bootstrapper of the same engine")
+        # the secret key's identity: shared key material is only valid under the same key
+        self._sk_seed = engine.key_seed(sk)
+        if share is not None and share._sk_seed != self._sk_seed:
+            raise ValueError("Bootstrapper(share=...) needs a bootstrapper of the same secret key")
+        # a trimmed share's keys switch only at the SlotToCoeff levels: this bootstrapper's
+        # CoeffToSlot (level L) would need the whole keys
+        if share is not None and getattr(share, "_bits_only", False):
+            raise ValueError("Bootstrapper(share=...) of a bootstrapper whose keys were trimmed "
+                             "(trim_bootstrap_keys): build every sharing bootstrapper before trimming")
         self.cjk = cjk if cjk is not None else share.cjk if share is not None else e.create_conjugation_key(sk)
         self.N = 1 << e.log_coeff_count
         self.n = self.N // 2

@@ -1176,6 +1176,14 @@ class Engine:
                                          C.byref(words), None))
         return 8 * words.value
 
+    def key_seed(self, key) -> int:
+        """The key seed a key was derived from (aesfhe_key_export's keyseed): two secret keys of
+        one engine with the same seed are the same key (Bootstrapper(share=) checks it)."""
+        kind, g, seed, words = C.c_int32(), C.c_uint64(), C.c_uint64(), C.c_int64()
+        self._check(self._lib.key_export(self._h, key._h, C.byref(kind), C.byref(g), C.byref(seed),
+                                         C.byref(words), None))
+        return int(seed.value)
+
     def trim_key(self, key, max_level: int):
         """Keep only the key-switch digits a switch at level <= max_level reads
         (aesfhe_key_trim): the kept digits are the full key's word for word; a later switch above

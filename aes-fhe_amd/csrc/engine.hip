@@ -25,6 +25,7 @@
 #include "ntt256f.h"
 #include "ks_fused.h"
 #include "bconv_mfma.h"
+#include "bconv_cols.h"
 #include "arena.h"
 #include "codec_dev.h"
 
@@ -165,6 +166,10 @@ struct aesfhe_engine {
     double *mdr_einv = nullptr, *mdr_dmodf = nullptr, *md_einv = nullptr;
     u64* mdr_dinv = nullptr;
     double *mu_hatinvf, *md_phatinvf, *md_pinvf, *rs_invf;
+    double* mu_nhatf = nullptr;  // [level l][limb i] N^{-1} hatinv_{l,i} / q_i: the INTT before a fused ModUp
+    // the same for a fused ModDown's sources: N^{-1} (D/e_j)^{-1} / e_j, plain ([kMdrMaxE]) and
+    // combined with r rescales ([cell][kMdrMaxE], as mdr_invf)
+    double *md_ninvf = nullptr, *mdr_ninvf = nullptr;
     TwD *mu_hatf, *md_phatf;  // base-conversion constants {w, w/q}
     // matrix-core base conversions (bconv_mfma.h): [set / cell][pid][8 planes][kBconvKT] signed
     // bytes, the XOR-0x80 corrections [set / cell][pid] and (2^32 mod p) / p per prime
@@ -454,7 +459,7 @@ static void ntt_inv_t(aesfhe_engine* e, Span src, Span dst, int total) {
 // N = 2^16 / 2^17: register-resident fp64-arithmetic passes over R = N / 256 rows of 256
 // (ntt256f.h): a column pass (the first log2 R stages) and a row pass (the last 8)
 template <int R>
-static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse) {
+static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse, const double* lf = nullptr) {
     Tabs T = e->tabs();
     // algorithmic bytes per pass: 8 B * N * limbs = half of the transform's read-once +
     // write-once 16 B per coefficient (the two-pass split itself is charged as overhead)
@@ -466,7 +471,8 @@ static void ntt256(aesfhe_engine* e, Span src, Span dst, int total, bool inverse
     }
     ProfScope ps(e, FAM_NTT, by, inverse ? "ntt_inv_cols" : "ntt_fwd_rows");
     if (!inverse) hipLaunchKernelGGL((k_nttf_fwd_rows_t<false, R>), dim3(R / 16, total), dim3(256), 0, e->stream, dst, T, RowFin{});
-    else hipLaunchKernelGGL(k_nttf_inv_cols<R>, dim3(16, total), dim3(256), 0, e->stream, dst, T);
+    else if (lf) hipLaunchKernelGGL((k_nttf_inv_cols<R, true>), dim3(16, total), dim3(256), 0, e->stream, dst, T, lf);
+    else hipLaunchKernelGGL((k_nttf_inv_cols<R, false>), dim3(16, total), dim3(256), 0, e->stream, dst, T, (const double*)nullptr);
 }
 
 // the N = 2^16 / 2^17 fp64 passes with fused epilogues (ModDown finish, key-switch inner product)
@@ -474,7 +480,8 @@ static bool fused_ntt(const aesfhe_engine* e) { return e->logN == 16 || e->logN 
 
 // inverse NTT of the product a (x) b (two canonical operand spans of one shape) into dst, the
 // product formed in the row pass's copy-in (fused_ntt engines)
-static void intt_prod(aesfhe_engine* e, Span a, Span b, Span dst, int total, const u64* fac) {
+// lf (N = 2^16): per-limb output factors replacing N^{-1} (k_nttf_inv_cols LF)
+static void intt_prod(aesfhe_engine* e, Span a, Span b, Span dst, int total, const u64* fac, const double* lf = nullptr) {
     if (total <= 0) return;
     Tabs T = e->tabs();
     const double by = 8.0 * e->N * (double)total;
@@ -489,8 +496,13 @@ static void intt_prod(aesfhe_engine* e, Span a, Span b, Span dst, int total, con
         }
     }
     ProfScope ps(e, FAM_NTT, by, "ntt_inv_cols");
-    if (e->logN == 16) hipLaunchKernelGGL(k_nttf_inv_cols<256>, dim3(16, total), dim3(256), 0, e->stream, dst, T);
-    else hipLaunchKernelGGL(k_nttf_inv_cols<512>, dim3(16, total), dim3(256), 0, e->stream, dst, T);
+    if (e->logN == 16) {
+        if (lf) hipLaunchKernelGGL((k_nttf_inv_cols<256, true>), dim3(16, total), dim3(256), 0, e->stream, dst, T, lf);
+        else hipLaunchKernelGGL((k_nttf_inv_cols<256, false>), dim3(16, total), dim3(256), 0, e->stream, dst, T, lf);
+    } else {
+        if (lf) throw_err(AESFHE_EUNSUPPORTED, "per-limb INTT factors at N = 2^17");
+        hipLaunchKernelGGL((k_nttf_inv_cols<512, false>), dim3(16, total), dim3(256), 0, e->stream, dst, T, lf);
+    }
     HIPC(hipGetLastError());
 }
 
@@ -674,6 +686,17 @@ static void build_tables(aesfhe_engine* e) {
         }
     up(hhatinv, &e->mu_hatinv);
     up(hhatinvf, &e->mu_hatinvf);
+    {  // the INTT in front of a fused ModUp (bconv_cols.h YIN) scales limb i of a level-l input by
+       // N^{-1} hatinv_{l,i} (its digit's width at level l) instead of N^{-1}: it emits y directly
+        std::vector<double> nh((size_t)Lp1 * Lp1, 0.0);
+        for (int l = 0; l < Lp1; l++)
+            for (int i = 0; i <= l; i++) {
+                const int lo = (i / A) * A, a = std::min(A, l + 1 - lo);
+                const u64 hv = hhatinv[((size_t)(i / A) * A + (a - 1)) * A + (i - lo)];
+                nh[(size_t)l * Lp1 + i] = (double)h_mulmod(hninv[i], hv, Q[i]) / (double)Q[i];
+            }
+        up(nh, &e->mu_nhatf);
+    }
     up(hhat, &e->mu_hat);
     up(hhatf, &e->mu_hatf);
     {  // matrix-core ModUp rows: [set][pid] (the digit's own pids are never targets)
@@ -760,6 +783,9 @@ static void build_tables(aesfhe_engine* e) {
         std::vector<double> heinv0(kMdrMaxE, 0.0);  // 1/p_k: the exact conversion of plain ModDown
         for (int k = 0; k < K; k++) heinv0[k] = 1.0 / (double)Q[Lp1 + k];
         up(heinv0, &e->md_einv);
+        std::vector<double> hn0(kMdrMaxE, 0.0);  // fused ModDown: N^{-1} phatinv_k folded into the INTT
+        for (int k = 0; k < K; k++) hn0[k] = (double)h_mulmod(hninv[Lp1 + k], hphatinv[k], Q[Lp1 + k]) / (double)Q[Lp1 + k];
+        up(hn0, &e->md_ninvf);
     }
     // combined ModDown + rescale: E = {q_{l-r+1}..q_l, p_0..p_{K-1}} (acc limb order), D = prod E
     //   mdr_invf[(r-1, l)][j]       = (D/e_j)^{-1} mod e_j, as w/e_j
@@ -770,7 +796,7 @@ static void build_tables(aesfhe_engine* e) {
         std::vector<double> hinvf(cells * kMdrMaxE, 0.0), hdinvf(cells * Lp1, 0.0);
         std::vector<TwD> hhatf(cells * kMdrMaxE * Lp1, TwD{0, 0});
         std::vector<u64> hdinv(cells * Lp1, 0);
-        std::vector<double> heinv(cells * kMdrMaxE, 0.0), hdmodf(cells * Lp1, 0.0);
+        std::vector<double> heinv(cells * kMdrMaxE, 0.0), hdmodf(cells * Lp1, 0.0), hninvf(cells * kMdrMaxE, 0.0);
         // matrix-core rows [cell][target i][8][kBconvKT] (bconv_mfma.h), v slot G = -D mod q_i
         const size_t brow = 8 * (size_t)kBconvKT;
         std::vector<int8_t> btab(cells * Lp1 * brow, 0);
@@ -789,6 +815,7 @@ static void build_tables(aesfhe_engine* e) {
                     for (size_t j2 = 0; j2 < E.size(); j2++)
                         if (j2 != j) prod = h_mulmod(prod, Q[E[j2]] % ej, ej);
                     hinvf[cell * kMdrMaxE + j] = (double)h_invmod(prod, ej) / (double)ej;
+                    hninvf[cell * kMdrMaxE + j] = (double)h_mulmod(hninv[E[j]], h_invmod(prod, ej), ej) / (double)ej;
                     heinv[cell * kMdrMaxE + j] = 1.0 / (double)ej;
                     for (int i = 0; i <= l - r; i++) {
                         const u64 qi = Q[i];
@@ -815,6 +842,7 @@ static void build_tables(aesfhe_engine* e) {
         up(btab, &e->bc_mdr_tab);
         up(bcorr, &e->bc_mdr_corr);
         up(hinvf, &e->mdr_invf);
+        up(hninvf, &e->mdr_ninvf);
         up(hhatf, &e->mdr_hatf);
         up(hdinv, &e->mdr_dinv);
         up(hdinvf, &e->mdr_dinvf);
@@ -929,7 +957,7 @@ static void engine_teardown(aesfhe_engine* e) {
                     e->md_pinvf, e->rs_invf, e->ring_d, e->tw, e->itw, e->mdr_invf, e->mdr_hatf,
                     e->mdr_dinv, e->mdr_dinvf, e->pmodf, e->mdr_einv, e->mdr_dmodf, e->md_einv,
                     e->bc_mu_tab, e->bc_md_tab, e->bc_mdr_tab, e->bc_mu_corr, e->bc_md_corr, e->bc_mdr_corr,
-                    e->bc_pc};
+                    e->bc_pc, e->mu_nhatf, e->md_ninvf, e->mdr_ninvf};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto& kv : e->poly2_tabs) hipFree(kv.second);
@@ -2118,6 +2146,31 @@ static void launch_bconv(aesfhe_engine* e, BconvArgs a, int nz, int nslots, bool
     HIPC(hipGetLastError());
 }
 
+// ModUp fused with the extension limbs' forward column pass (bconv_cols.h, N = 2^16; round 6,
+// VERDICT r5 item 1): the sources are y (the INTT folded qhat^{-1}), the extension limbs leave as
+// the column pass's raw-double intermediate.  AESFHE_MODUP_FUSED=0 selects k_bconv_mfma + the
+// column pass for A/B runs.  Same residues either way.
+static bool modup_fused_on() {
+    static const bool on = !(getenv("AESFHE_MODUP_FUSED") && !atoi(getenv("AESFHE_MODUP_FUSED")));
+    return on;
+}
+static void launch_bconv_cols(aesfhe_engine* e, const BconvArgs& a, int nz) {
+    const int nstep = (a.ns + 3) / 4, ntile = (a.nt + 3) / 4;
+    if (e->logN != 16 || nstep < 1 || nstep > 4 || ntile < 1 || (16 * nz) % 8)
+        throw_err(AESFHE_EUNSUPPORTED, "fused base conversion of %d slots to %d targets", a.ns, a.nt);
+    const dim3 g((unsigned)(16 * nz * ntile));
+    const Tabs T = e->tabs();
+#define BCC(S) hipLaunchKernelGGL((k_bconv_cols<S, true>), g, dim3(256), 0, e->stream, a, T, ntile)
+    switch (nstep) {
+        case 1: BCC(1); break;
+        case 2: BCC(2); break;
+        case 3: BCC(3); break;
+        default: BCC(4); break;
+    }
+#undef BCC
+    HIPC(hipGetLastError());
+}
+
 // The lazy-ModDown BSGS map with its babies formed inside the term sums (k_bsgs_terms) instead
 // of written (k_ks_inner_multi + k_dot_pt_ext_multi) is the default; AESFHE_BSGS_FUSED=0 selects
 // the unfused pair for A/B runs.  Its first form (one batch element per thread, every element
@@ -2200,6 +2253,12 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
     const long lN = (long)(l + 1) * N, neN = (long)ne * N;
     const int beta = ks_beta(e, l);
     Tmp dc(e, (size_t)B * lN);
+    // fused (N = 2^16): every digit wider than one limb converts and runs its extension limbs'
+    // column pass in one kernel (k_bconv_cols) from y = [x qhat^{-1}], which the INTT emits
+    // directly (its N^{-1} times the digit's qhat^{-1} per limb; a one-limb digit's qhat^{-1} is 1,
+    // so the spread path below reads the same words as before)
+    const bool fcols = cols_only && e->logN == 16 && bconv_mfma_on() && modup_fused_on();
+    const double* lf = fcols ? e->mu_nhatf + (size_t)l * e->Lp1 : nullptr;
     // 1. INTT copy of the input
     Span sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
     if (pa) {
@@ -2207,10 +2266,11 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
         Span sb = span_s((u64*)pb->ptr + pb->ps, pb->bs, l + 1, l + 1, 0, e->Lp1);
         sa.pmask = pa->bmask;  // cyclic broadcast of a product operand (check_cyclic)
         sb.pmask = pb->bmask;
-        intt_prod(e, sa, sb, sdc, B * (l + 1), fac);
+        intt_prod(e, sa, sb, sdc, B * (l + 1), fac, lf);
     } else {
         Span sd = span_s((u64*)d, dbs, l + 1, l + 1, 0, e->Lp1);
-        ntt(e, sd, sdc, B * (l + 1), true);
+        if (lf) ntt256<256>(e, sd, sdc, B * (l + 1), true, lf);
+        else ntt(e, sd, sdc, B * (l + 1), true);
     }
     // out of place (cols_only): ModUp writes a buffer recycled across the digits and the column
     // pass reads it into ext_j -- the in-place pass read and wrote the same lines; one digit's
@@ -2220,7 +2280,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
     std::unique_ptr<Tmp> mu;  // only when some digit runs k_modup (alpha > 1)
     bool any_wide = false;
     for (int j = 0; j < beta; j++) any_wide |= std::min((j + 1) * e->A, l + 1) - j * e->A > 1;
-    if (oop && any_wide) mu.reset(new Tmp(e, (size_t)B * neN));
+    if (oop && any_wide && !fcols) mu.reset(new Tmp(e, (size_t)B * neN));
     for (int j = 0; j < beta; j++) {
         const int A = e->A, lo = j * A, hi = std::min(lo + A, l + 1), alpha = hi - lo;
         const size_t set = (size_t)j * A + (alpha - 1);
@@ -2238,6 +2298,31 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
             if (lo > 0) cols(span_s(exj, neN, lo, lo, 0, e->Lp1), B * lo);
             cols(span_s(exj + (long)hi * N, neN, ne - hi, (l + 1) - hi, hi, e->Lp1), B * (ne - hi));
             HIPC(hipGetLastError());
+            continue;
+        }
+        if (fcols) {  // 2'. conversion + column pass in one launch, straight into ext_j
+            BconvArgs a{};
+            a.src = (const u64*)dc.p + (long)lo * N;
+            a.sbs = lN;
+            a.dst = exj;
+            a.dbs = neN;
+            a.nc = 1;
+            a.ns = alpha;
+            a.s_nq = alpha;
+            a.s_q0 = lo;
+            a.nt = ne - alpha;
+            a.skip0 = lo;
+            a.skipn = alpha;
+            a.tl_l = l;
+            a.Lp1 = e->Lp1;
+            a.tab = e->bc_mu_tab + set * e->np * 8 * kBconvKT;
+            a.corr = e->bc_mu_corr + set * e->np;
+            a.pc = e->bc_pc;
+            a.qall = e->q;
+            a.qinvall = e->qinv;
+            // algorithmic bytes: the digit's sources read once, the extension limbs written once
+            ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne, "modup_cols");
+            launch_bconv_cols(e, a, B);
             continue;
         }
         // 2. ModUp base conversion of digit j to every other limb, then NTT those limbs
@@ -2348,8 +2433,8 @@ static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int 
         const int total = B * 2 * (K + r);
         if (rows_done) {
             ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_inv_cols");
-            if (N == 65536) hipLaunchKernelGGL(k_nttf_inv_cols<256>, dim3(16, total), dim3(256), 0, e->stream, ssp, e->tabs());
-            else hipLaunchKernelGGL(k_nttf_inv_cols<512>, dim3(16, total), dim3(256), 0, e->stream, ssp, e->tabs());
+            if (N == 65536) hipLaunchKernelGGL((k_nttf_inv_cols<256, false>), dim3(16, total), dim3(256), 0, e->stream, ssp, e->tabs(), (const double*)nullptr);
+            else hipLaunchKernelGGL((k_nttf_inv_cols<512, false>), dim3(16, total), dim3(256), 0, e->stream, ssp, e->tabs(), (const double*)nullptr);
             HIPC(hipGetLastError());
         } else {
             ntt(e, ssp, ssp, total, true);
@@ -2394,6 +2479,71 @@ static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int 
                            r ? e->mdr_dmodf + cell * e->Lp1 : e->pmodf, e->Lp1, e->q, e->qinv, e->logN, hs);
     }
     HIPC(hipGetLastError());
+    return r ? e->mdr_dinvf + cell * e->Lp1 : e->md_pinvf;
+}
+
+// ModDown's conversion fused with conv's forward column pass (N = 2^16, rows_done accumulators;
+// bconv_cols.h VC): the inverse column pass of the dropped limbs scales them by N^{-1} (D/e_j)^{-1}
+// (md_ninvf / mdr_ninvf), so they leave as y_j, and k_bconv_cols writes conv's column-pass
+// intermediate straight into conv2 ([B][2][lk + 1][N], what the FIN row launch reads) -- conv's
+// coefficient form never reaches HBM.  Returns D^{-1} mod q_i (w / q) for the finish, as
+// moddown_conv.  Same residues as moddown_conv + ntt_fwd_cols.
+static bool moddown_cols_ok(const aesfhe_engine* e, int r) {
+    return e->logN == 16 && bconv_mfma_on() && modup_fused_on() && r >= 0 && r <= kMdrMaxR && e->K + r + 1 <= 16;
+}
+static const double* moddown_conv_cols(aesfhe_engine* e, u64* acc, int B, int l, int r, u64* conv2, long abs_, long acs) {
+    const int N = e->N, K = e->K;
+    const int lk = l - r;
+    const long kN = (long)(lk + 1) * N;
+    if (!moddown_cols_ok(e, r) || lk < 0) throw_err(AESFHE_EARG, "fused ModDown of depth %d", r);
+    const size_t cell = r ? (size_t)(r - 1) * e->Lp1 + l : 0;
+    {
+        Span ssp = span_s(acc + (long)(lk + 1) * N, acs, K + r, r, lk + 1, e->Lp1);
+        const int total = B * 2 * (K + r);
+        const double* lf = r ? e->mdr_ninvf + cell * kMdrMaxE : e->md_ninvf;
+        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_inv_cols");
+        hipLaunchKernelGGL((k_nttf_inv_cols<256, true>), dim3(16, total), dim3(256), 0, e->stream, ssp, e->tabs(), lf);
+        HIPC(hipGetLastError());
+    }
+    BconvArgs a{};
+    a.src = acc + (long)(lk + 1) * N;
+    a.sbs = abs_;
+    a.scs = acs;
+    a.dst = conv2;
+    a.dbs = 2 * kN;
+    a.dcs = kN;
+    a.nc = 2;
+    a.ns = K + r;
+    a.s_nq = r;
+    a.s_q0 = lk + 1;
+    a.s_p0 = e->Lp1;
+    a.einv = r ? e->mdr_einv + cell * kMdrMaxE : e->md_einv;
+    a.nt = lk + 1;
+    a.skip0 = lk + 1;
+    a.skipn = 0;
+    a.tl_l = lk;
+    a.Lp1 = e->Lp1;
+    a.tab = r ? e->bc_mdr_tab + cell * e->Lp1 * 8 * kBconvKT : e->bc_md_tab;
+    a.corr = r ? e->bc_mdr_corr + cell * e->Lp1 : e->bc_md_corr;
+    a.pc = e->bc_pc;
+    a.qall = e->q;
+    a.qinvall = e->qinv;
+    {
+        // algorithmic bytes: the dropped limbs read once, conv's intermediate written once
+        ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1), "moddown_cols");
+        const int nstep = (K + r + 1 + 3) / 4, ntile = (lk + 1 + 3) / 4;
+        const dim3 g((unsigned)(16 * 2 * B * ntile));
+        const Tabs T = e->tabs();
+#define BCC(S) hipLaunchKernelGGL((k_bconv_cols<S, true, true>), g, dim3(256), 0, e->stream, a, T, ntile)
+        switch (nstep) {
+            case 1: BCC(1); break;
+            case 2: BCC(2); break;
+            case 3: BCC(3); break;
+            default: BCC(4); break;
+        }
+#undef BCC
+        HIPC(hipGetLastError());
+    }
     return r ? e->mdr_dinvf + cell * e->Lp1 : e->md_pinvf;
 }
 
@@ -2501,23 +2651,36 @@ static void ks_finish_fused(aesfhe_engine* e, const u64* d, long dbs, const u64*
     const int nd = ne - (lk + 1);
     std::unique_ptr<Tmp> own;
     if (!acc_in) own.reset(new Tmp(e, (size_t)B * 2 * nd * N));
-    u64* acc = acc_in ? acc_in : own->p - (long)(lk + 1) * N;
+    // (an address, not a C++ pointer into the block: only limbs >= lk + 1 are ever formed from it,
+    // by the dropped limbs' launch and moddown_conv; the FIN launch gets no accumulators at all)
+    u64* acc = acc_in ? acc_in : reinterpret_cast<u64*>(reinterpret_cast<uintptr_t>(own->p) - (uintptr_t)(lk + 1) * N * sizeof(u64));
     const long abs_ = acc_in ? 2 * neN : 2L * nd * N, acs = acc_in ? neN : (long)nd * N;
     launch(lk + 1, nd, false, acc, abs_, acs, KsFin{});
-    std::unique_ptr<Tmp> conv(new Tmp(e, (size_t)B * 2 * kN));
-    const double* dinvf = moddown_conv(e, acc, B, l, r, conv->p, true, abs_, acs);
-    if (own) own.reset();  // the dropped limbs are converted: stream-ordered reuse from here on
-    Tmp conv2(e, (size_t)B * 2 * kN);
-    {
-        const int total = B * 2 * (lk + 1);
-        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
-        ntt_fwd_cols(e, span_s(conv->p, kN, lk + 1, lk + 1, 0, e->Lp1), span_s(conv2.p, kN, lk + 1, lk + 1, 0, e->Lp1), total);
+    const double* dinvf;
+    std::unique_ptr<Tmp> conv2;
+    if (moddown_cols_ok(e, r)) {  // conversion + conv's column pass in one launch (bconv_cols.h)
+        conv2.reset(new Tmp(e, (size_t)B * 2 * kN));
+        dinvf = moddown_conv_cols(e, acc, B, l, r, conv2->p, abs_, acs);
+        if (own) own.reset();
+    } else {
+        std::unique_ptr<Tmp> conv(new Tmp(e, (size_t)B * 2 * kN));
+        dinvf = moddown_conv(e, acc, B, l, r, conv->p, true, abs_, acs);
+        if (own) own.reset();  // the dropped limbs are converted: stream-ordered reuse from here on
+        conv2.reset(new Tmp(e, (size_t)B * 2 * kN));
+        {
+            const int total = B * 2 * (lk + 1);
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_cols");
+            ntt_fwd_cols(e, span_s(conv->p, kN, lk + 1, lk + 1, 0, e->Lp1), span_s(conv2->p, kN, lk + 1, lk + 1, 0, e->Lp1), total);
+        }
+        conv.reset();  // conv's coefficient form is read only by the column pass
     }
-    conv.reset();  // conv's coefficient form is read only by the column pass
     HIPC(hipGetLastError());
-    const KsFin kf{conv2.p, 2 * kN, kN, o->d, 2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf,
+    const KsFin kf{conv2->p, 2 * kN, kN, o->d, 2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf,
                    Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}};
-    launch(0, lk + 1, true, acc, abs_, acs, kf);
+    // the kept limbs' accumulators exist only in acc_in (accumulating giants); with an own block
+    // FIN reads none: nullptr, so that no later change can read conv2's reuse of that memory
+    if (own && accum) throw_err(AESFHE_EARG, "accumulating key switch without accumulators");
+    launch(0, lk + 1, true, own ? nullptr : acc, abs_, acs, kf);
 }
 
 // Key switch, second half: inner product of ext (ks_modup of d) with key k, ModDown (fused with

@@ -444,8 +444,11 @@ __global__ __launch_bounds__(256, 4) void k_nttf_inv_rows(Span src, Span dst, Ta
 // scaling: raw doubles in, canonical u64 out.  R = 512 (N = 2^17): both halves run the R = 256
 // stages (twiddle index multiplier 2 + h, as in the forward pass), stay in registers, and the
 // last stage (distance 256 rows) pairs them before the scaling.
-template <int R = 256>
-__global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T) {
+// LF (round 6): the final N^{-1} scaling is a per-limb factor lf[limb index within the span] (w/q)
+// instead -- the key switch's INTT folds the digit's qhat^{-1} into it (engine.hip ks_modup), so
+// the fused ModUp (bconv_cols.h YIN) reads y directly
+template <int R = 256, bool LF = false>
+__global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T, const double* __restrict__ lf) {
     static_assert(R == 256 || R == 512, "rows of 256: N = 2^16 or 2^17");
     constexpr int H = R / 256;
     __shared__ double s[256 * kPadF];
@@ -514,7 +517,8 @@ __global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T) {
             gs_f<false>(x[a], x[16 + a], w, q, qi);
         }
     }
-    const double ni = (double)T.ninv[pid], nif = T.ninvf[pid];
+    const double nif = LF ? lf[blockIdx.y % dst.nl] : T.ninvf[pid];
+    const double ni = LF ? tw_w(nif, q) : (double)T.ninv[pid];
 #pragma unroll
     for (int h = 0; h < H; h++)
 #pragma unroll

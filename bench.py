@@ -90,8 +90,12 @@ KERNEL_SYMBOLS = {
     "ntt_fwd_cols": "k_nttf_fwd_cols<R>",
     "modup": "k_bconv_mfma<NSTEP, VC=false> (i8 matrix-core ModUp)",
     "moddown": "k_bconv_mfma<NSTEP, VC=true> (i8 matrix-core ModDown with the exact v slot)",
+    "modup_cols": "k_bconv_cols<NSTEP, YIN=true, VC=false> (i8 matrix-core ModUp fused with the extension "
+                  "limbs' forward NTT column pass: the extension limbs leave as the column-pass intermediate)",
+    "moddown_cols": "k_bconv_cols<NSTEP, YIN=true, VC=true> (i8 matrix-core ModDown, exact v slot, fused with "
+                    "conv's forward NTT column pass)",
     "bsgs_terms": "k_bsgs_terms<GM, BM, BB, PB> (BSGS term sums with the babies formed on the fly)",
-    "poly2_int": "k_poly2_int_s<4, LAZY, BIG> / k_poly2_int (one call = the exact limbs + the 50-bit q_0 limb)",
+    "poly2_int": "k_poly2_int_s<4, LAZY, BIG> (the exact limbs) + k_poly2_int_split<MO> (the 50-bit q_0 limb, split inner sums): one call = 2 dispatches",
 }
 NTT_TARGET = 0.5  # north_star: ">= 50% of HBM roofline on the NTT kernel"
 

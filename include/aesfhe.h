@@ -64,8 +64,10 @@ extern "C" {
 
 /* ABI revision: bumped whenever a struct layout or an entry point's meaning changes (4: the
  * trailing aesfhe_params.digit_primes; a caller compiled against an older header passes a shorter
- * struct).  Callers check aesfhe_abi_version() == AESFHE_ABI_VERSION before anything else. */
-#define AESFHE_ABI_VERSION 4
+ * struct; 5: aesfhe_key_trim appended, and aesfhe_key_import accepts a switching key of 1..dnum
+ * digits -- a trimmed key's export -- instead of exactly dnum).  Callers check
+ * aesfhe_abi_version() == AESFHE_ABI_VERSION before anything else. */
+#define AESFHE_ABI_VERSION 5
 
 #define AESFHE_OK 0
 #define AESFHE_EARG (-1)      /* bad argument / shape / level mismatch */

@@ -1556,6 +1556,23 @@ int aesfhe_tensor(aesfhe_engine *e, const aesfhe_ct *a0, const aesfhe_ct *b0, ae
 /* ------------------------------------------------------------------------------------------ */
 /* hybrid key switching.  d: one polynomial, level l, NTT domain.             */
 /* out0/out1: (l+1) limbs each.                                                                */
+/* a trimmed key (aesfhe_key_trim) keeps its first digits only: it serves a key switch at level l
+ * iff it stores the beta(l) digits the switch reads -- the HIP engine's check_key_digits, checked
+ * at every entry point before any work (a misused trimmed key returns AESFHE_ELEVEL
+ * instead of aborting the process) */
+static int key_level_ok(const aesfhe_engine *e, const aesfhe_key *k, int l) {
+    if (!k || k->ndig <= 0) return 0;
+    const int beta = (l + 1 + e->A - 1) / e->A;
+    if (beta > k->ndig)
+        return fail(AESFHE_ELEVEL, "key trimmed to %d digits cannot switch at level %d (%d digits)", k->ndig, l, beta);
+    return 0;
+}
+#define KEY_LEVEL_OK(k, l)                         \
+    do {                                           \
+        const int kl_rc_ = key_level_ok(e, (k), (l)); \
+        if (kl_rc_) return kl_rc_;                 \
+    } while (0)
+
 /* inner product of the ModUp digits with the key: acc = 2 x (l+1+K) limbs over Q_l and P */
 static u64 *ks_acc(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k) {
     const int N = e->N, K = e->K, nq = e->L + 1, ne = l + 1 + K;
@@ -1568,7 +1585,7 @@ static u64 *ks_acc(aesfhe_engine *e, const u64 *d, int l, const aesfhe_key *k) {
     u64 *acc = calloc((size_t)2 * ne * N, sizeof(u64));
     const int A = e->A;
     int beta = (l + 1 + A - 1) / A;
-    if (k->ndig > 0 && beta > k->ndig) {  /* a trimmed key used above its level: misuse, loudly */
+    if (k->ndig > 0 && beta > k->ndig) {  /* unreachable: every entry point runs key_level_ok first */
         fprintf(stderr, "ckks_oracle: key trimmed to %d digits switched at level %d (%d digits)\n", k->ndig, l, beta);
         abort();
     }
@@ -1763,6 +1780,7 @@ static int relin_raw(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_key *rlk
 int aesfhe_relinearize(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_key *rlk, aesfhe_ct **out) {
     if (c->npoly != 3) return fail(AESFHE_EDEGREE, "Input ciphertext should have 3 polynomials");
     if (!rlk || rlk->kind != 2) return fail(AESFHE_EARG, "relinearize needs a relinearization key");
+    KEY_LEVEL_OK(rlk, c->level);
     if (c->is_zero) {
         aesfhe_ct *r = ct_new(e, c->B, 2, c->level);
         r->is_zero = 1;
@@ -1777,6 +1795,7 @@ int aesfhe_mul(aesfhe_engine *e, const aesfhe_ct *a, const aesfhe_ct *b, const a
     int l = a->level < b->level ? a->level : b->level;
     if (l < 1) return fail(AESFHE_ELEVEL, "no level left for a ciphertext multiplication");
     aesfhe_ct *t, *rl;
+    KEY_LEVEL_OK(rlk, l);
     int rc = aesfhe_tensor(e, a, b, &t);
     if (rc) return rc;
     if (t->is_zero) {
@@ -1795,6 +1814,7 @@ int aesfhe_mul(aesfhe_engine *e, const aesfhe_ct *a, const aesfhe_ct *b, const a
 int aesfhe_galois(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_key *gk, aesfhe_ct **out) {
     if (!gk || gk->kind != 3) return fail(AESFHE_EARG, "galois needs a rotation/conjugation key");
     if (c->npoly != 2) return fail(AESFHE_EDEGREE, "Input ciphertext should have 2 polynomials");
+    KEY_LEVEL_OK(gk, c->level);
     const int N = e->N, l = c->level;
     aesfhe_ct *r = ct_new(e, c->B, 2, l);
     if (c->is_zero) {
@@ -1831,6 +1851,7 @@ int aesfhe_rotate_hoisted(aesfhe_engine *e, const aesfhe_ct *c, const aesfhe_key
     if (n < 1) return fail(AESFHE_EARG, "rotate_hoisted needs at least one key");
     for (int i = 0; i < n; i++)
         if (!keys[i] || keys[i]->kind != 5) return fail(AESFHE_EARG, "rotate_hoisted needs hoisted rotation keys");
+    for (int i = 0; i < n; i++) KEY_LEVEL_OK(keys[i], c->level);
     if (c->npoly != 2) return fail(AESFHE_EDEGREE, "Input ciphertext should have 2 polynomials");
     const int N = e->N, l = c->level;
     u64 *k0 = malloc(sizeof(u64) * (size_t)(l + 1) * N), *k1 = malloc(sizeof(u64) * (size_t)(l + 1) * N);
@@ -1890,6 +1911,8 @@ int aesfhe_linear_bsgs(aesfhe_engine *e, const aesfhe_ct *c, int32_t nb, const a
     }
     for (int i = 0; i < nb; i++)
         if (bkeys[i] && bkeys[i]->kind != 5) return fail(AESFHE_EARG, "baby steps need hoisted rotation keys");
+    for (int i = 0; i < nb; i++) KEY_LEVEL_OK(bkeys[i], l);
+    for (int j = 0; j < ng; j++) KEY_LEVEL_OK(gkeys[j], l - 1);
     for (int t = 0; t < tot; t++) {
         if (tbaby[t] < 0 || tbaby[t] >= nb) return fail(AESFHE_EARG, "bad baby index");
         if (!pts[t] || !pts[t]->ext || pts[t]->level != l) return fail(AESFHE_EARG, "linear_bsgs needs Q u P plaintexts at the input level");
@@ -2011,6 +2034,7 @@ int aesfhe_power_basis(aesfhe_engine *e, const aesfhe_ct *c, int32_t d, const ae
     int need = 0;
     while ((1 << need) < d) need++;
     if (c->level < need) return fail(AESFHE_ELEVEL, "power basis of degree %d needs %d levels, have %d", d, need, c->level);
+    if (d > 1) KEY_LEVEL_OK(rlk, c->level);
     aesfhe_ct_copy(e, c, &outs[0]);
     for (int k = 2; k <= d; k++) {
         int hi = 1;
@@ -2087,6 +2111,7 @@ int aesfhe_mul_fma(aesfhe_engine *e, const aesfhe_ct *a, const aesfhe_ct *b, con
     }
     if ((a->B != B && a->B != 1) || (b->B != B && b->B != 1) || (c && c->B != B && c->B != 1))
         return fail(AESFHE_EARG, "batch mismatch");
+    KEY_LEVEL_OK(rlk, l);
     const int N = e->N;
     aesfhe_ct *t = ct_new(e, B, 3, l);
     if (!a->is_zero && !b->is_zero) {
@@ -2146,6 +2171,7 @@ int aesfhe_dot(aesfhe_engine *e, const aesfhe_ct *const *a, const aesfhe_ct *con
     for (int i = 0; i < n; i++)
         if ((a[i]->B != B && a[i]->B != 1) || (b[i]->B != B && b[i]->B != 1)) return fail(AESFHE_EARG, "batch mismatch");
     if (l < 1) return fail(AESFHE_ELEVEL, "no level left for a dot product");
+    KEY_LEVEL_OK(rlk, l);
     aesfhe_ct *acc = ct_new(e, B, 3, l);
     int any = 0;
     for (int i = 0; i < n; i++) {
@@ -2197,6 +2223,7 @@ int aesfhe_dot_fma(aesfhe_engine *e, const aesfhe_ct *const *a, const aesfhe_ct 
     for (int j = 0; j < nc; j++)
         if (c[j]->B != B && c[j]->B != 1) return fail(AESFHE_EARG, "batch mismatch");
     if (l < 1) return fail(AESFHE_ELEVEL, "no level left for a dot product");
+    KEY_LEVEL_OK(rlk, l);
     const int N = e->N;
     aesfhe_ct *acc = ct_new(e, B, 3, l);
     for (int i = 0; i < n; i++) {
@@ -2260,6 +2287,7 @@ int aesfhe_poly2(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, const
     for (int a = 0; a < na; a++)
         if (all[a]->B != B && all[a]->B != 1) return fail(AESFHE_EARG, "batch mismatch");
     if (l < 2) return fail(AESFHE_ELEVEL, "no level left for a bivariate polynomial");
+    KEY_LEVEL_OK(rlk, l);
     const double *D = e->scales;
     const double S1 = D[l - 2] / D[l] * ((double)e->q[l] / D[l]) * (double)e->q[l - 1];
     const i64 R = llround(D[l]);
@@ -2377,6 +2405,7 @@ int aesfhe_poly2_int(aesfhe_engine *e, const aesfhe_ct *const *xb, int32_t nx, c
     for (int a = 0; a < na; a++)
         if (all[a]->B != B && all[a]->B != 1) return fail(AESFHE_EARG, "batch mismatch");
     if (l < 2) return fail(AESFHE_ELEVEL, "no level left for a bivariate polynomial");
+    KEY_LEVEL_OK(rlk, l);
     for (int t = 0; t < m; t++)
         for (int i = 0; i < nx; i++) {
             long sum = 0;

@@ -122,6 +122,14 @@ def test_bootstrapper_share(oracle_lib):
     ya, yb = b3.bootstrap_bits(e.encrypt(a + noise[0], pk, level=3), e.encrypt(b + noise[1], pk, level=3))
     for y, v, nz in ((ya, a, noise[0]), (yb, b, noise[1])):
         assert np.all(np.abs(e.decrypt(y, sk) - v) <= 1.24 * nz ** 2 + 1e-5)
+    # a share under another secret key, or one whose keys were trimmed, is refused
+    # before any key is made (a trimmed CoeffToSlot key would fail mid-bootstrap)
+    with pytest.raises(ValueError, match="same secret key"):
+        Bootstrapper(e, e.create_secret_key(seed=99), rlk, share=b5)
+    from aes_xor_fhe.bootstrap import trim_bootstrap_keys
+    trim_bootstrap_keys([b5, b3])
+    with pytest.raises(ValueError, match="trimmed"):
+        Bootstrapper(e, sk, rlk, cts_groups=4, share=b5)
 
 
 def test_trim_bootstrap_keys_residue_identical(oracle_lib):
@@ -136,6 +144,7 @@ def test_trim_bootstrap_keys_residue_identical(oracle_lib):
     for trim in (False, True):
         e, sk, pk, rlk = _engine(oracle_lib, max_level=30, scale_bits=40, special_primes=10, digit_primes=12)
         b5 = Bootstrapper(e, sk, rlk, cts_groups=5)
+        stc_only = set()
         if trim:
             assert trim_bootstrap_keys([b5]) > 0
             stc_only = {id(k) for p in b5.stc_bits for k in b5.plan_keys(p)} - \
@@ -149,6 +158,12 @@ def test_trim_bootstrap_keys_residue_identical(oracle_lib):
         if trim:  # (after the encryptions above: this one draws encryption randomness too)
             with pytest.raises(RuntimeError, match="trimmed"):
                 b5.bootstrap(e.encrypt(np.zeros(e.slot_count), pk, level=0))
+            # the trimmed key itself, switched above its level: the oracle returns AESFHE_ELEVEL
+            # as the HIP engine does (it used to abort() the process)
+            top = e.encrypt(np.zeros(e.slot_count), pk, level=30)
+            kh = next(h for h in b5.hrot.values() if id(h) in stc_only)
+            with pytest.raises(RuntimeError, match="trimmed to 1 digits"):
+                e.rotate_hoisted(top, [kh])
     for h, o in zip(*outs):
         assert np.array_equal(h, o)
 

@@ -31,6 +31,8 @@ CLASSES = [
     (r"k_nttf_rows_ks_p<\d+, false, 2>", "ks_rows_inner.ks"),
     (r"k_nttf_rows_ks_p<\d+, true", "ks_rows_acc.prod"),
     (r"k_nttf_rows_ks_p<", "ks_rows_acc.ks"),
+    (r"k_bconv_cols<\d+, true, false", "modup_cols"),  # round 6: conversion + forward column pass
+    (r"k_bconv_cols<\d+, true, true", "moddown_cols"),
     (r"k_bconv_mfma<\d+, false", "modup"),  # matrix-core conversions: ModUp (no v slot), ModDown (v)
     (r"k_bconv_mfma<\d+, true", "moddown"),
     (r"k_bsgs_terms<", "bsgs_terms"),
@@ -45,7 +47,7 @@ CLASSES = [
     (r"k_modup<", "modup"),
     (r"k_moddown<", "moddown"),
     (r"k_moddown_finish", "moddown_finish"),
-    (r"k_poly2_int(_s)?<", "poly2_int"),
+    (r"k_poly2_int(_s|_split)?<", "poly2_int"),
     (r"k_poly2\b", "poly2"),
     (r"k_gather_batch", "gather"),
     (r"k_lincomb_many", "lincomb_many"),
