@@ -121,42 +121,98 @@ def _words(engine, npoly, level):
     return npoly * (level + 1) * (1 << engine.log_coeff_count)
 
 
-def scatter_ciphertext(engine, ct, src: int = 0, group=None, granule: int = 1):
-    """Split a batched ciphertext held by rank `src` across all ranks along the batch dimension
-    (shard_range: uneven batches allowed, in whole granules of `granule` elements -- 4 for the
-    sliced AES state, AESSlicedRound.GRANULE).  Non-source ranks pass ct=None.  Returns this
-    rank's share (None for a rank whose share is empty).  Raises on every rank if the batch is not
-    a whole number of granules."""
+# the torch staging bytes the last scatter on this process held at once (tests assert the source
+# rank's peak): {"staging_peak_bytes", "share_bytes_max", "role"}
+last_scatter: dict = {}
+
+
+def _scatter_stream(engine, src, group, granule, meta, fill, own, nitems=1):
+    """Rank `src` sends every other rank its share point to point, one rank at a time, through ONE
+    staging buffer (fill(a, b, k, buf) writes item k's elements [a, b) into it), and takes its own
+    share last (own(a, b) -> the list of nitems Ciphertexts), so the source holds its batch (or
+    nothing, for a producing source) plus one share -- never the world padded copies a collective
+    scatter needs (config 5's 512-ciphertext batch would not fit twice in
+    288 GB).  Receivers take each item into a buffer of their share's size and import it.
+    meta = (batch, npoly, level) on src, the same for every item.  Returns the list of this rank's
+    nitems shares (None for an empty share)."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     dev = _torch_device(engine, group)
     _check_keys(engine, group, dev)
-    meta = torch.zeros(3, dtype=torch.int64, device=dev)
+    m = torch.zeros(3, dtype=torch.int64, device=dev)
     if rank == src:
-        meta = torch.tensor([ct.batch, ct.npoly, ct.level], dtype=torch.int64, device=dev)
-    dist.broadcast(meta, src, group=group)
-    batch, npoly, level = (int(x) for x in meta.cpu())
+        m = torch.tensor(list(meta), dtype=torch.int64, device=dev)
+    dist.broadcast(m, src, group=group)
+    batch, npoly, level = (int(x) for x in m.cpu())
     shares = [shard_range(batch, world, r, granule) for r in range(world)]  # raises alike everywhere
     per = _words(engine, npoly, level)
-    smax = max(b - a for a, b in shares)  # padded share: scatter needs equal sizes
-    out = torch.empty((smax, per), dtype=torch.int64, device=dev)
-    parts = None
-    if rank == src:
-        parts = []
-        for r in range(world):
-            a, b = shares[r]
-            t = torch.empty((smax, per), dtype=torch.int64, device=dev)
-            _sync(dev)
-            if b > a:
-                _export(engine, ct, t, a, b - a)
-            parts.append(t)
-    dist.scatter(out, parts, src=src, group=group)
+    gsrc = dist.get_global_rank(group, src) if group is not None else src
     a, b = shares[rank]
+    if rank == src:
+        big = max([bb - aa for r, (aa, bb) in enumerate(shares) if r != src] + [0])
+        buf = torch.empty((big, per), dtype=torch.int64, device=dev) if big else None
+        for r in range(world):
+            ra, rb = shares[r]
+            if r == src or rb == ra:
+                continue
+            dst = dist.get_global_rank(group, r) if group is not None else r
+            for k in range(nitems):
+                _sync(dev)  # the previous send has left buf
+                fill(ra, rb, k, buf)
+                dist.send(buf[:rb - ra], dst, group=group)
+        _sync(dev)
+        last_scatter.update(role="src", staging_peak_bytes=(buf.numel() * 8 if buf is not None else 0),
+                            share_bytes_max=max(bb - aa for aa, bb in shares) * per * 8)
+        del buf
+        return own(a, b) if b > a else [None] * nitems
     if b == a:
-        return None
-    _sync(dev)  # RCCL wrote `out` on torch's stream
-    return _import(engine, out, b - a, npoly, level)
+        last_scatter.update(role="dst", staging_peak_bytes=0, share_bytes_max=0)
+        return [None] * nitems
+    out = torch.empty((b - a, per), dtype=torch.int64, device=dev)
+    res = []
+    for _ in range(nitems):
+        dist.recv(out, gsrc, group=group)
+        _sync(dev)  # the transfer wrote `out` on torch's stream
+        res.append(_import(engine, out, b - a, npoly, level))
+    last_scatter.update(role="dst", staging_peak_bytes=out.numel() * 8, share_bytes_max=(b - a) * per * 8)
+    return res
+
+
+def scatter_ciphertext(engine, ct, src: int = 0, group=None, granule: int = 1):
+    """Split a batched ciphertext held by rank `src` across all ranks along the batch dimension
+    (shard_range: uneven batches allowed, in whole granules of `granule` elements -- 4 for the
+    sliced AES state, AESSlicedRound.GRANULE).  Non-source ranks pass ct=None.  Returns this
+    rank's share (None for a rank whose share is empty).  Raises on every rank if the batch is not
+    a whole number of granules.  Streaming (_scatter_stream): the source holds ct plus one share."""
+    meta = (ct.batch, ct.npoly, ct.level) if ct is not None else None
+    return _scatter_stream(engine, src, group, granule, meta,
+                           lambda a, b, k, buf: _export(engine, ct, buf, a, b - a),
+                           lambda a, b: [engine.slice(ct, a, b - a)])[0]
+
+
+def scatter_produced(engine, batch: int, npoly: int, level: int, produce, src: int = 0, group=None,
+                     granule: int = 1, nitems: int = 1):
+    """The client form: rank `src` produces each rank's share on demand (produce(a, b) -> the
+    list of `nitems` ciphertexts of batch elements [a, b), all of one shape -- e.g. an AES state's
+    bit ciphertexts, those blocks encrypted) and sends them, so it never holds the whole batch:
+    one share in flight plus its own.  Other ranks pass produce=None (batch / npoly / level are
+    taken from src).  Returns this rank's list of nitems shares."""
+    held = {}
+
+    def fill(a, b, k, buf):
+        if k == 0:
+            held["cs"] = list(produce(a, b))
+            if len(held["cs"]) != nitems:
+                raise ValueError(f"scatter_produced: {len(held['cs'])} ciphertexts for {nitems} items")
+        c = held["cs"][k]
+        if (c.batch, c.npoly, c.level) != (b - a, npoly, level):
+            raise ValueError(f"scatter_produced: share [{a}, {b}) came back as batch {c.batch}, "
+                             f"npoly {c.npoly}, level {c.level}")
+        _export(engine, c, buf, 0, b - a)
+        held["cs"][k] = None  # sent: freed before the next is exported
+    return _scatter_stream(engine, src, group, granule, (batch, npoly, level), fill,
+                           lambda a, b: list(produce(a, b)), nitems)
 
 
 def gather_ciphertext(engine, ct, dst: int = 0, group=None):

@@ -2257,7 +2257,7 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
     // column pass in one kernel (k_bconv_cols) from y = [x qhat^{-1}], which the INTT emits
     // directly (its N^{-1} times the digit's qhat^{-1} per limb; a one-limb digit's qhat^{-1} is 1,
     // so the spread path below reads the same words as before)
-    const bool fcols = cols_only && e->logN == 16 && bconv_mfma_on() && modup_fused_on();
+    const bool fcols = e->logN == 16 && bconv_mfma_on() && modup_fused_on();
     const double* lf = fcols ? e->mu_nhatf + (size_t)l * e->Lp1 : nullptr;
     // 1. INTT copy of the input
     Span sdc = span_s(dc.p, lN, l + 1, l + 1, 0, e->Lp1);
@@ -2300,7 +2300,8 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
             HIPC(hipGetLastError());
             continue;
         }
-        if (fcols) {  // 2'. conversion + column pass in one launch, straight into ext_j
+        if (fcols) {  // 2'. conversion + column pass in one launch, straight into ext_j (+ the row pass
+                      // for callers that read the extension in NTT form: hoisted rotations, BSGS babies)
             BconvArgs a{};
             a.src = (const u64*)dc.p + (long)lo * N;
             a.sbs = lN;
@@ -2321,8 +2322,20 @@ static void ks_modup(aesfhe_engine* e, const u64* d, long dbs, int B, int l, u64
             a.qall = e->q;
             a.qinvall = e->qinv;
             // algorithmic bytes: the digit's sources read once, the extension limbs written once
-            ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne, "modup_cols");
-            launch_bconv_cols(e, a, B);
+            {
+                ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * ne, "modup_cols");
+                launch_bconv_cols(e, a, B);
+            }
+            if (!cols_only) {
+                auto rows = [&](long off, int n, int nq, int p0, int total) {
+                    ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_fwd_rows");
+                    hipLaunchKernelGGL((k_nttf_fwd_rows_t<false, 256>), dim3(16, total), dim3(256), 0, e->stream,
+                                       span_s(exj + off, neN, n, nq, p0, e->Lp1), e->tabs(), RowFin{});
+                    HIPC(hipGetLastError());
+                };
+                if (lo > 0) rows(0, lo, lo, 0, B * lo);
+                rows((long)hi * N, ne - hi, (l + 1) - hi, hi, B * (ne - hi));
+            }
             continue;
         }
         // 2. ModUp base conversion of digit j to every other limb, then NTT those limbs
@@ -2491,7 +2504,8 @@ static const double* moddown_conv(aesfhe_engine* e, u64* acc, int B, int l, int 
 static bool moddown_cols_ok(const aesfhe_engine* e, int r) {
     return e->logN == 16 && bconv_mfma_on() && modup_fused_on() && r >= 0 && r <= kMdrMaxR && e->K + r + 1 <= 16;
 }
-static const double* moddown_conv_cols(aesfhe_engine* e, u64* acc, int B, int l, int r, u64* conv2, long abs_, long acs) {
+static const double* moddown_conv_cols(aesfhe_engine* e, u64* acc, int B, int l, int r, u64* conv2, long abs_, long acs,
+                                       bool rows_done = true) {
     const int N = e->N, K = e->K;
     const int lk = l - r;
     const long kN = (long)(lk + 1) * N;
@@ -2501,6 +2515,12 @@ static const double* moddown_conv_cols(aesfhe_engine* e, u64* acc, int B, int l,
         Span ssp = span_s(acc + (long)(lk + 1) * N, acs, K + r, r, lk + 1, e->Lp1);
         const int total = B * 2 * (K + r);
         const double* lf = r ? e->mdr_ninvf + cell * kMdrMaxE : e->md_ninvf;
+        if (!rows_done) {  // canonical NTT-domain accumulators: the inverse row pass first
+            ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_inv_rows");
+            hipLaunchKernelGGL((k_nttf_inv_rows<256, false>), dim3(16, total), dim3(256), 0, e->stream, ssp, ssp, e->tabs(),
+                               Span{}, (const u64*)nullptr);
+            HIPC(hipGetLastError());
+        }
         ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total, "ntt_inv_cols");
         hipLaunchKernelGGL((k_nttf_inv_cols<256, true>), dim3(16, total), dim3(256), 0, e->stream, ssp, e->tabs(), lf);
         HIPC(hipGetLastError());
@@ -2552,6 +2572,18 @@ static void moddown_acc(aesfhe_engine* e, u64* acc, int B, int l, int r, Opnd fi
     const long neN = (long)ne * N;
     const int lk = l - r;  // output level
     const long kN = (long)(lk + 1) * N;
+    if (moddown_cols_ok(e, r)) {  // conversion + conv's column pass fused, then the finishing row pass
+        Tmp conv2(e, (size_t)B * 2 * kN);
+        const double* dinvf = moddown_conv_cols(e, acc, B, l, r, conv2.p, 2 * neN, neN, false);
+        const int total = B * 2 * (lk + 1);
+        RowFin f{(const u64*)acc, 2 * neN, neN, Opnd2{fin_add.ptr, fin_add.bs, fin_add.ps, fin_add.np}, o->d,
+                 2L * (lk + 1) * N, (long)(lk + 1) * N, dinvf, lk + 1};
+        ProfScope ps(e, FAM_NTT, 8.0 * N * (double)total * (3.0 + (fin_add.ptr ? 1.0 : 0.0)), "ntt_fwd_rows_fin");
+        hipLaunchKernelGGL((k_nttf_fwd_rows_t<true, 256>), dim3(16, total), dim3(256), 0, e->stream,
+                           span_s(conv2.p, kN, lk + 1, lk + 1, 0, e->Lp1), e->tabs(), f);
+        HIPC(hipGetLastError());
+        return;
+    }
     Tmp conv(e, (size_t)B * 2 * kN);
     const double* dinvf = moddown_conv(e, acc, B, l, r, conv.p);
     const size_t cell = r ? (size_t)(r - 1) * e->Lp1 + l : 0;

@@ -145,6 +145,14 @@ def dominant_roofline(kernels, steps_prof, pmc):
         return {"bound": "hbm", "kernel": None, "achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": None, "traffic": None}
     name, c = max(roll.items(), key=lambda kv: kv[1]["share_of_kernel_time"])
+    # the headline is the dominant CLASS (its instantiations summed); the single largest
+    # instantiation (one rocprof symbol) is reported beside it, so that both readings are in the
+    # line (the largest symbol may belong to another class)
+    big_n, big = max(((n, k) for n, k in kernels.items() if k.get("alg_bytes_per_launch")),
+                     key=lambda nk: nk[1]["share_of_kernel_time"])
+    largest = {"name": big_n, "kernel": KERNEL_SYMBOLS.get(big_n, big_n), "class": kernel_class(big_n),
+               "share_of_kernel_time": big["share_of_kernel_time"], "avg_us": big["avg_us"],
+               "frac": big.get("frac"), "hbm_bytes_per_launch": big.get("hbm_bytes_per_launch")}
     calls = c["calls_per_step"]
     tr = c["hbm_bytes_per_step"] / calls if c["hbm_complete"] and calls else None
     alg = c["alg_bytes_per_step"] / calls
@@ -169,6 +177,9 @@ def dominant_roofline(kernels, steps_prof, pmc):
                     "instantiation (instantiations.*.avg_us)",
         "alg_bytes_per_launch": round(alg), "share_of_kernel_time": round(c["share_of_kernel_time"], 4),
         "instantiations": inst,
+        "selected_by": "class (the instantiations of one kernel template summed); largest_instantiation is "
+                       "the single largest symbol",
+        "largest_instantiation": largest,
     }
 
 
@@ -299,6 +310,9 @@ def parse():
                          "the PMC records between them)")
     ap.add_argument("--no-harness", action="store_true",
                     help="skip the reference-harness leg (full_round on 32768 bytes, xor_cipher)")
+    ap.add_argument("--config5-sets", type=int, default=16,
+                    help="config 5 sets per rank (16 = 64 of the reference's 512 ciphertexts / 8 GPUs; fewer only "
+                         "for multi-rank rehearsals that share one GPU)")
     ap.add_argument("--config5", choices=("auto", "on", "off"), default="auto",
                     help="config 5's per-rank shard (N = 2^17, L = 35, K = 12, scale 44, 16 sets = 64 of the "
                          "reference's 512 ciphertexts / 8 GPUs): one round + ten rounds on a fresh engine after "
@@ -430,10 +444,15 @@ def setup_engine(args, device, rank):
     return eng, drv
 
 
-def aes128_full(args, eng, drv, rank, barrier, allmax):
+def aes128_full(args, eng, drv, rank, barrier, allmax, client_scatter=False):
     """Full AES-128 (ARK0 + 10 rounds, FIPS-197 5.1) with bit-mode bootstrapping on the bit
     layouts (sliced / rows): a warm-up encryption of the same shape (bootstrap plaintexts, device pool), then one
-    timed encryption of args.aes10_batch ciphertext sets (x 8192 blocks at N = 2^16)."""
+    timed encryption of args.aes10_batch ciphertext sets (x 8192 blocks at N = 2^16).
+    client_scatter (under torchrun; config 5 as BASELINE.json states it): rank 0 is the client --
+    it encrypts every rank's share of the whole batch's states, one rank at a time, and streams
+    them point to point (parallel.scatter_produced: it never holds the batch, at most one share
+    beside its own); the ranks run the ten rounds on their shares (the timed region, no
+    collective) and rank 0 gathers the outputs and verifies the whole batch."""
     from aes_xor_fhe import aes_tables as T
     from aes_xor_fhe.bootstrap import Bootstrapper, trim_bootstrap_keys
     R = drv.R
@@ -494,8 +513,32 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
                                keys, bs, pairs_per_call=ppc, progress=prog, consume=True, probe=probe)
     warm_final = R.bit_margin(warm)
     del warm
-    blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
-    st = R.encrypt_blocks(blocks, level=L0)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    scat = None
+    if client_scatter and world > 1:
+        from aes_xor_fhe.parallel import last_scatter, scatter_produced, shard_range
+        gran = getattr(R, "GRANULE", 1)
+        total = nb * world
+        allb = np.random.default_rng(2000).integers(0, 256, (total, R.n_blk, 16), dtype=np.uint8)
+        a0, b0 = shard_range(total, world, rank, gran)
+        blocks = allb[a0:b0]
+        nitems = 2 if drv.layout == "bytes" else 32  # ciphertexts per state (RoundDriver.cts)
+        barrier()
+        t0 = time.perf_counter()
+        mine = scatter_produced(eng, total, 2, L0, (lambda x, y: drv.cts(R.encrypt_blocks(allb[x:y], level=L0)))
+                                if rank == 0 else None, granule=gran, nitems=nitems)
+        barrier()
+        t_sc = allmax(time.perf_counter() - t0)
+        st = drv.from_cts(mine)
+        del mine
+        scat = {"sets_total": total, "sets_per_rank": [shard_range(total, world, r, gran) for r in range(world)],
+                "ms": round(t_sc * 1e3, 1), "client": "rank 0 encrypts each rank's share and streams it "
+                "(parallel.scatter_produced, point to point; RCCL over xGMI under nccl)",
+                "client_staging_peak_gb": round(last_scatter.get("staging_peak_bytes", 0) / 1e9, 3)
+                if rank == 0 else None}
+    else:
+        blocks = rng.integers(0, 256, (nb, R.n_blk, 16), dtype=np.uint8)
+        st = R.encrypt_blocks(blocks, level=L0)
     log("aes10: timed run")
     tm = {}
     barrier()
@@ -514,8 +557,19 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
               "refresh_inputs": refresh_in, "worst_refresh_input": max((r["max_abs_dev"] for r in refresh_in), default=None),
               "note": "max over every slot of | |v| / s - 1 | (a bit flips past 1); final = the timed run's output "
                       "(decrypted after the clock stopped), refresh inputs from the untimed warm-up of the same shape"}
-    if args.check:
-        got = R.decrypt_blocks(out, nb)
+    if scat is not None:  # the outputs back to the client, which verifies the whole batch
+        from aes_xor_fhe.parallel import gather_ciphertext
+        t0 = time.perf_counter()
+        full = [gather_ciphertext(eng, c) for row in out for c in row]
+        barrier()
+        scat["gather_ms"] = round(allmax(time.perf_counter() - t0) * 1e3, 1)
+        if rank == 0:
+            out, blocks, nbv = drv.from_cts(full), allb, nb * world
+        del full
+    else:
+        nbv = nb
+    if args.check and rank == 0 or args.check and scat is None:
+        got = R.decrypt_blocks(out, nbv)
         want = T.encrypt_block(blocks, key)  # vectorised over (..., 16)
         ok = bool(np.array_equal(got, want))
         if not ok:  # where: a few flipped bits (noise) look different from a systematic error
@@ -523,7 +577,6 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
             wrong = {"blocks": int(bad.sum()), "bits": int(np.unpackbits(got ^ want).sum()),
                      "sets": sorted({int(s) for s in np.nonzero(bad)[0]})[:16],
                      "byte_positions": sorted({int(b) for b in np.nonzero(got != want)[-1]})}
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     return {"metric": "AES-128 blocks/sec (10 rounds incl. bootstrapping)",
             "value": round(nb * R.n_blk * world / el, 2), "unit": "blocks/s",
             "ms": round(el * 1e3, 1), "ciphertext_sets_per_gpu": nb,
@@ -536,7 +589,7 @@ def aes128_full(args, eng, drv, rank, barrier, allmax):
             "state_level": L0,
             "block_rounds_per_s": round(10 * nb * R.n_blk * world / el, 2),
             "per_round_level_ms": tm.get("per_round"), "pool": eng.pool_stats(),
-            "timed_mallocs": timed_mallocs}
+            "timed_mallocs": timed_mallocs, "client_scatter": scat}
 
 
 def _materialize(out):
@@ -905,7 +958,7 @@ def config5_shard_leg(args, device, rank, barrier, allmax, cur):
     from aes_xor_fhe import aes_tables as T
     a = copy.copy(args)
     a.log_n, a.max_level, a.special_primes, a.scale_bits = 17, 35, 12, 44
-    a.digit_primes, a.batch, a.aes10_batch, a.aes10_ppc, a.layout = -1, 16, 16, 0, "sliced"
+    a.digit_primes, a.batch, a.aes10_batch, a.aes10_ppc, a.layout = -1, args.config5_sets, args.config5_sets, 0, "sliced"
     t0 = time.perf_counter()
     eng, drv = setup_engine(a, device, rank)
     cur[0] = eng  # the barrier drains this engine's stream
@@ -936,9 +989,9 @@ def config5_shard_leg(args, device, rank, barrier, allmax, cur):
         gc.collect()
         eng.pool_trim()
         log("config 5 shard: round done; ten rounds")
-        aes10 = aes128_full(a, eng, drv, rank, barrier, allmax)
-        return {"workload": ("config 5 per-rank shard: 16 sets x 16384 blocks (64 of the reference's 512 "
-                             "ciphertexts of 4096 blocks / 8 GPUs), fully sliced state"),
+        aes10 = aes128_full(a, eng, drv, rank, barrier, allmax, client_scatter=True)
+        return {"workload": (f"config 5 per-rank shard: {a.batch} sets x 16384 blocks ({4 * a.batch} of the "
+                             "reference's ciphertexts of 4096 blocks; 16 sets = 512 / 8 GPUs), fully sliced state"),
                 "log_n": a.log_n, "max_level": a.max_level, "special_primes": a.special_primes,
                 "digit_primes": eng.digit_primes, "scale_bits": a.scale_bits, "setup_s": round(setup_s, 1),
                 "round": rnd, "aes128_10_rounds": {k: v for k, v in aes10.items() if k != "pool"},
@@ -1111,7 +1164,9 @@ def main():
     if args.aes10_batch > 0 and args.layout != "bytes":
         aes10 = secondary("aes10", lambda: aes128_full(args, eng, R, rank, barrier, allmax))
     c5 = None
-    run_c5 = args.config5 == "on" or (args.config5 == "auto" and world == 1 and args.log_n == 16
+    # config 5 runs under torchrun too: every rank its shard, the ten-round
+    # leg's states streamed from the client rank (aes128_full client_scatter)
+    run_c5 = args.config5 == "on" or (args.config5 == "auto" and args.log_n == 16
                                       and args.max_level == 30 and args.layout == "sliced")
     backend, digits, dnum = eng._lib.backend, eng.digit_primes, eng.dnum
     if run_c5:

@@ -123,3 +123,23 @@ def test_dominant_class_over_two_instantiations():
     del pmc["per_kernel"]["ks_rows_fin.ks"]
     r = bench.dominant_roofline(bench.kernel_table(_FakeEngine(raw), pmc, steps), steps, pmc)
     assert r["traffic"] is None
+
+
+def test_headline_is_the_dominant_class_not_instantiation():
+    """the round-5 profile's largest single symbol was the column pass
+    (21.7 %), while the key-switch finishing class summed two instantiations to 22.3 %.  The line's
+    headline roofline is the CLASS with the largest share; the largest single instantiation is
+    reported beside it under largest_instantiation."""
+    steps = 1
+    raw = {"ks_rows_fin.prod": [228, 228 * 0.9257, 228 * 5.0e9, 228],
+           "ks_rows_fin.ks": [4, 4 * 6.976, 4 * 3.6e10, 4],
+           "ntt_fwd_cols": [1328, 1328 * 0.1737, 1328 * 4.457e8, 1328]}
+    t = bench.kernel_table(_FakeEngine(raw), {}, steps)
+    r = bench.dominant_roofline(t, steps, {})
+    assert r["kernel"].startswith("ks_rows_fin:")
+    assert r["selected_by"].startswith("class")
+    big = r["largest_instantiation"]
+    assert big["name"] == "ntt_fwd_cols" and big["class"] == "ntt_fwd_cols"
+    assert big["share_of_kernel_time"] > t["ks_rows_fin.prod"]["share_of_kernel_time"]
+    assert big["share_of_kernel_time"] < r["share_of_kernel_time"]
+    assert big["frac"] == t["ntt_fwd_cols"]["frac"]

@@ -167,6 +167,61 @@ def _worker_keys(rank, world, init, so, result_q):
         dist.destroy_process_group()
 
 
+def _worker_stream(rank, world, init, so, result_q):
+    """Streaming scatter: the source sends each share point to point through
+    one staging buffer, so its torch staging peak is one share (the old collective scatter built
+    world padded copies); uneven shares (10 elements over 3 ranks: 4 + 3 + 3); the producing form
+    (scatter_produced: the source encrypts each share on demand and never holds the batch);
+    residues equal the source's slices, and a gather restores the batch."""
+    sys.path.insert(0, str(ROOT / "aes-fhe_amd"))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+    try:
+        from aes_xor_fhe._abi import Lib
+        from aes_xor_fhe.fhe import Engine
+        from aes_xor_fhe import parallel as P
+        e = Engine(_lib=Lib(so), log_n=10, max_level=4, special_primes=2, seed=91)
+        sk = e.create_secret_key(3)
+        n = e.slot_count
+        vals = np.random.default_rng(2).uniform(-1, 1, (10, n))
+        ct = e.encrypt(vals, sk) if rank == 0 else None
+        mine = P.scatter_ciphertext(e, ct)
+        a, b = P.shard_range(10, world, rank)
+        per = ct.npoly * (ct.level + 1) * (1 << e.log_coeff_count) * 8 if ct is not None else None
+        ok = mine.batch == b - a
+        st = dict(P.last_scatter)
+        if rank == 0:  # the source: one staging share (the largest other share), never world copies
+            ok = ok and st["role"] == "src" and st["staging_peak_bytes"] == 3 * per
+            ok = ok and st["staging_peak_bytes"] <= st["share_bytes_max"] < world * 4 * per
+            ok = ok and np.array_equal(e.export_residues(mine), e.export_residues(e.slice(ct, a, b - a)))
+        else:
+            ok = ok and st["role"] == "dst" and st["staging_peak_bytes"] == st["share_bytes_max"]
+        ok = ok and np.allclose(e.decrypt(mine, sk), vals[a:b], atol=1e-6)
+        full = P.gather_ciphertext(e, mine)
+        if rank == 0:
+            ok = ok and np.array_equal(e.export_residues(full), e.export_residues(ct))
+        # the producing form: shares encrypted on demand at the source
+        made = []
+
+        def produce(x, y):  # two ciphertexts per share (as an AES state's bit ciphertexts)
+            made.append((x, y))
+            return [e.encrypt(vals[x:y], sk, level=3), e.encrypt(-vals[x:y], sk, level=3)]
+        got = P.scatter_produced(e, 10, 2, 3, produce if rank == 0 else None, nitems=2)
+        ok = ok and len(got) == 2 and all(g.batch == b - a and g.level == 3 for g in got)
+        ok = ok and np.allclose(e.decrypt(got[0], sk), vals[a:b], atol=1e-6)
+        ok = ok and np.allclose(e.decrypt(got[1], sk), -vals[a:b], atol=1e-6)
+        if rank == 0:  # every share made once, the source's own last
+            ok = ok and sorted(made) == [P.shard_range(10, world, r) for r in range(world)] and made[-1] == (a, b)
+            ok = ok and P.last_scatter["staging_peak_bytes"] == 3 * 2 * 4 * (1 << e.log_coeff_count) * 8
+        oks = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(oks, torch.tensor([int(ok)]))
+        if rank == 0:
+            result_q.put(all(int(t) == 1 for t in oks))
+    finally:
+        dist.destroy_process_group()
+
+
 def _spawn(target, so, world=2, timeout=900):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -226,6 +281,11 @@ def test_bench_launcher_rejects_mismatch():
 def test_two_rank_shared_seed_and_key_check(oracle_lib):
     from conftest import ORACLE_SO
     assert _spawn(_worker_keys, str(ORACLE_SO)) is True
+
+
+def test_three_rank_streaming_scatter_peak(oracle_lib):
+    from conftest import ORACLE_SO
+    assert _spawn(_worker_stream, str(ORACLE_SO), world=3, timeout=300) is True
 
 
 def test_two_rank_scatter_round_gather(oracle_lib):
