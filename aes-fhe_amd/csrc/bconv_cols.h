@@ -77,7 +77,9 @@ __device__ __forceinline__ void cols256_stages_store(double (&x)[16], double q, 
 
 // grid: 16 * nz * ntile workgroups (1-D, XCD-aware order above), 256 threads; nz = batch * nc
 // (a.nc components per element), ntile = ceil(nt / 4); 16 * nz must be a multiple of 8.
-template <int NSTEP, bool YIN, bool VC = false>
+// PF: row groups of source words in flight ahead of the one being converted (register prefetch;
+// 0 = load at use)
+template <int NSTEP, bool YIN, bool VC = false, int PF = 1>
 __global__ __launch_bounds__(256, 2) void k_bconv_cols(BconvArgs a, Tabs T, int ntile) {
     __shared__ double s[2][256 * kPadF];
     __shared__ double twq[4][256];
@@ -128,9 +130,22 @@ __global__ __launch_bounds__(256, 2) void k_bconv_cols(BconvArgs a, Tabs T, int 
             }
         }
     double xv[4][16];
+    // the source words of row group ar (group g's column c is coefficient
+    // (16 ar + 4 w + 2 g + (c >> 4), 16 bx + (c & 15))), PF row groups ahead of their use
+    u64 raw[PF + 1][NSTEP][2][2];
+    auto load = [&](u64 (&r)[NSTEP][2][2], int ar) {
+#pragma unroll
+        for (int st = 0; st < NSTEP; st++)
+#pragma unroll
+            for (int uu = 0; uu < 2; uu++)
+#pragma unroll
+                for (int g = 0; g < 2; g++) r[st][uu][g] = sp[st][uu][(16 * ar + 4 * w + 2 * g + (c >> 4)) * 256];
+    };
+#pragma unroll
+    for (int p = 0; p < PF; p++) load(raw[p], p);
 #pragma unroll
     for (int ar = 0; ar < 16; ar++) {
-        // group g's column c is coefficient (16 ar + 4 w + 2 g + (c >> 4), 16 bx + (c & 15))
+        if (ar + PF < 16) load(raw[(ar + PF) % (PF + 1)], ar + PF);
         bc_v4i bf[2][NSTEP];
         double ys[2][NSTEP][2];  // VC: the slots' y values (dead slots 0)
 #pragma unroll
@@ -139,8 +154,7 @@ __global__ __launch_bounds__(256, 2) void k_bconv_cols(BconvArgs a, Tabs T, int 
             for (int uu = 0; uu < 2; uu++)
 #pragma unroll
                 for (int g = 0; g < 2; g++) {
-                    const int rowg = 16 * ar + 4 * w + 2 * g + (c >> 4);
-                    u64 yb = sp[st][uu][rowg * 256];
+                    u64 yb = PF ? raw[ar % (PF + 1)][st][uu][g] : sp[st][uu][(16 * ar + 4 * w + 2 * g + (c >> 4)) * 256];
                     if (!YIN) {
                         const double q = sq[st][uu], f = sf[st][uu];
                         double y = fmul_rem(u2d(yb), tw_w(f, q), f, q);

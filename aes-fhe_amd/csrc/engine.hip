@@ -26,6 +26,7 @@
 #include "ks_fused.h"
 #include "bconv_mfma.h"
 #include "bconv_cols.h"
+#include "bsgs_plan.h"
 #include "arena.h"
 #include "codec_dev.h"
 
@@ -2154,22 +2155,32 @@ static bool modup_fused_on() {
     static const bool on = !(getenv("AESFHE_MODUP_FUSED") && !atoi(getenv("AESFHE_MODUP_FUSED")));
     return on;
 }
-static void launch_bconv_cols(aesfhe_engine* e, const BconvArgs& a, int nz) {
-    const int nstep = (a.ns + 3) / 4, ntile = (a.nt + 3) / 4;
+// source row groups prefetched ahead (bconv_cols.h PF; AESFHE_BCC_PF=0/1/2 for A/B runs)
+static int bcc_pf() {
+    static const int pf = getenv("AESFHE_BCC_PF") ? std::max(0, std::min(2, atoi(getenv("AESFHE_BCC_PF")))) : 1;
+    return pf;
+}
+template <bool VC>
+static void launch_bconv_cols_t(aesfhe_engine* e, const BconvArgs& a, int nz, int nslots) {
+    const int nstep = (nslots + 3) / 4, ntile = (a.nt + 3) / 4;
     if (e->logN != 16 || nstep < 1 || nstep > 4 || ntile < 1 || (16 * nz) % 8)
-        throw_err(AESFHE_EUNSUPPORTED, "fused base conversion of %d slots to %d targets", a.ns, a.nt);
+        throw_err(AESFHE_EUNSUPPORTED, "fused base conversion of %d slots to %d targets", nslots, a.nt);
     const dim3 g((unsigned)(16 * nz * ntile));
     const Tabs T = e->tabs();
-#define BCC(S) hipLaunchKernelGGL((k_bconv_cols<S, true>), g, dim3(256), 0, e->stream, a, T, ntile)
+    const int pf = bcc_pf();
+#define BCC(S, P) hipLaunchKernelGGL((k_bconv_cols<S, true, VC, P>), g, dim3(256), 0, e->stream, a, T, ntile)
+#define BCS(S) do { if (pf == 0) BCC(S, 0); else if (pf == 2) BCC(S, 2); else BCC(S, 1); } while (0)
     switch (nstep) {
-        case 1: BCC(1); break;
-        case 2: BCC(2); break;
-        case 3: BCC(3); break;
-        default: BCC(4); break;
+        case 1: BCS(1); break;
+        case 2: BCS(2); break;
+        case 3: BCS(3); break;
+        default: BCS(4); break;
     }
+#undef BCS
 #undef BCC
     HIPC(hipGetLastError());
 }
+static void launch_bconv_cols(aesfhe_engine* e, const BconvArgs& a, int nz) { launch_bconv_cols_t<false>(e, a, nz, a.ns); }
 
 // The lazy-ModDown BSGS map with its babies formed inside the term sums (k_bsgs_terms) instead
 // of written (k_ks_inner_multi + k_dot_pt_ext_multi) is the default; AESFHE_BSGS_FUSED=0 selects
@@ -2184,36 +2195,9 @@ static void launch_bconv_cols(aesfhe_engine* e, const BconvArgs& a, int nz) {
 // every keyed baby i is g^i (the BSGS babies: rotations by i x stride); otherwise 0, 1, 2, ...
 // Either order is a permutation of the blocks, so results do not depend on it.
 static std::vector<unsigned short> bsgs_block_order(int logN, const std::vector<u64>& gal) {
-    const int nblk = logN >= 8 ? 1 << (logN - 8) : 1;
-    const u64 M = 2ULL << logN;
-    std::vector<unsigned short> ord(nblk);
-    for (int i = 0; i < nblk; i++) ord[i] = (unsigned short)i;
-    u64 g1 = 0;
-    int i1 = -1;
-    for (int i = 0; i < (int)gal.size(); i++)
-        if (gal[i] > 1) {
-            g1 = gal[i], i1 = i;
-            break;
-        }
-    if (!g1) return ord;
-    u64 gp = 1;  // keyed babies must be g1^(i - i1 + 1), identity babies anywhere
-    for (int i = i1; i < (int)gal.size(); i++) {
-        gp = (gp * g1) & (M - 1);
-        if (gal[i] != 0 && gal[i] != gp) return ord;
-    }
-    auto brv = [&](u64 x) { return (u64)(__builtin_bitreverse32((unsigned)x) >> (32 - logN)); };
-    auto pi = [&](int kb) {
-        const u64 k = (u64)kb << 8, ek = 2 * brv(k) + 1;
-        return (int)(brv((((g1 * ek) & (M - 1)) - 1) >> 1) >> 8);
-    };
-    std::vector<char> seen(nblk, 0);
-    int n = 0;
-    for (int s = 0; s < nblk; s++)
-        for (int kb = s; !seen[kb]; kb = pi(kb)) {
-            seen[kb] = 1;
-            ord[n++] = (unsigned short)kb;
-        }
-    if (n != nblk) throw_err(AESFHE_EUNSUPPORTED, "bsgs block order is not a permutation");
+    std::vector<unsigned short> ord;  // bsgs_plan.h: the orbit walk, or 0, 1, 2, ...
+    if (!aesfhe::bsgs_block_order(logN, std::vector<uint64_t>(gal.begin(), gal.end()), ord))
+        throw_err(AESFHE_EUNSUPPORTED, "bsgs block order is not a permutation");
     return ord;
 }
 
@@ -2551,18 +2535,7 @@ static const double* moddown_conv_cols(aesfhe_engine* e, u64* acc, int B, int l,
     {
         // algorithmic bytes: the dropped limbs read once, conv's intermediate written once
         ProfScope ps(e, FAM_KS, 8.0 * N * (double)B * 2 * (K + r + lk + 1), "moddown_cols");
-        const int nstep = (K + r + 1 + 3) / 4, ntile = (lk + 1 + 3) / 4;
-        const dim3 g((unsigned)(16 * 2 * B * ntile));
-        const Tabs T = e->tabs();
-#define BCC(S) hipLaunchKernelGGL((k_bconv_cols<S, true, true>), g, dim3(256), 0, e->stream, a, T, ntile)
-        switch (nstep) {
-            case 1: BCC(1); break;
-            case 2: BCC(2); break;
-            case 3: BCC(3); break;
-            default: BCC(4); break;
-        }
-#undef BCC
-        HIPC(hipGetLastError());
+        launch_bconv_cols_t<true>(e, a, 2 * B, K + r + 1);
     }
     return r ? e->mdr_dinvf + cell * e->Lp1 : e->md_pinvf;
 }
@@ -3065,8 +3038,14 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
     aesfhe_ct* sumq = nullptr;
     try {
         constexpr int kGM = 8;
-        std::vector<int> first(ng + 1, 0);
-        for (int j = 0; j < ng; j++) first[j + 1] = first[j] + nterm[j];
+        // the term tables, validated and sized on the host (bsgs_plan.h, ASan-tested)
+        std::vector<BsgsChunk> plan;
+        {
+            std::vector<const void*> pd(tot);
+            for (int t = 0; t < tot; t++) pd[t] = pts[t]->d;
+            const std::string err = bsgs_plan_terms(nb, ng, nterm, tbaby, pd.data(), kGM, plan);
+            if (!err.empty()) throw_err(AESFHE_EARG, "%s", err.c_str());
+        }
         std::vector<const u64*> ep(nb);
         std::vector<u64> gal(nb, 0);
         for (int i = 0; i < nb; i++) {
@@ -3077,22 +3056,16 @@ extern "C" int aesfhe_linear_bsgs(aesfhe_engine* e, const aesfhe_ct* c, int32_t 
         auto dgal = upload_small(e, gal.data(), gal.size());
         const std::vector<unsigned short> kord = bsgs_block_order(e->logN, gal);
         auto dkord = upload_small(e, kord.data(), kord.size());
-        for (int j0 = 0; j0 < ng; j0 += kGM) {
-            const int gn = std::min(kGM, ng - j0);
-            std::vector<const u64*> pt((size_t)gn * nb, nullptr);
+        for (const BsgsChunk& ch : plan) {
+            const int j0 = ch.j0, gn = ch.gn;
+            const double terms = ch.terms;
             std::vector<std::unique_ptr<Tmp>> S;
             std::vector<u64*> so;
-            double terms = 0;
             for (int j = 0; j < gn; j++) {
-                for (int t = first[j0 + j]; t < first[j0 + j + 1]; t++) {
-                    if (pt[(size_t)j * nb + tbaby[t]]) throw_err(AESFHE_EARG, "two terms of one giant on the same baby");
-                    pt[(size_t)j * nb + tbaby[t]] = pts[t]->d;
-                    terms++;
-                }
                 S.emplace_back(new Tmp(e, (size_t)B * 2 * neN));
                 so.push_back(S.back()->p);
             }
-            auto dpt = upload_small(e, pt.data(), pt.size());
+            auto dpt = upload_small(e, ch.pt.data(), ch.pt.size());
             auto dso = upload_small(e, so.data(), so.size());
             if (fused_terms) {
                 // bytes: the extension (beta words per (b, t, k), read once; the permuted re-reads of

@@ -3,7 +3,8 @@ this pool; host code only):
   * the CPU oracle (oracle/ckks_oracle.c) driven over the whole ABI by oracle/asan_check.c,
     engine destroyed before its objects (make -C oracle asan);
   * the HIP engine's host pieces (aes-fhe_amd/csrc/ckks_host.h: prime chain, roots, PRNG, codec)
-    at every ring size, tests/native/host_asan.cpp.
+    at every ring size, tests/native/host_asan.cpp; its device arena (arena.h); the linear_bsgs
+    host planning (bsgs_plan.h).
 A sanitizer report makes the program exit non-zero."""
 import os
 import subprocess
@@ -51,3 +52,14 @@ def test_device_arena_asan(tmp_path):
     for mode in ([], ["first_fit"]):
         r = subprocess.run([str(exe)] + mode, env=ENV, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0 and "arena_asan ok" in r.stdout, (mode, r.stdout[-2000:], r.stderr[-4000:])
+
+
+def test_bsgs_plan_asan(tmp_path):
+    """aesfhe_linear_bsgs's host planning (aes-fhe_amd/csrc/bsgs_plan.h: term validation, the
+    giants' plaintext-pointer tables, the k-block walk order) under ASan + UBSan against a direct
+    model (tests/native/bsgs_plan_asan.cpp)."""
+    exe = tmp_path / "bsgs_plan_asan"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                    "-o", str(exe), str(ROOT / "tests" / "native" / "bsgs_plan_asan.cpp")], check=True)
+    r = subprocess.run([str(exe)], env=ENV, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "bsgs_plan_asan ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])

@@ -127,15 +127,23 @@ int main(int argc, char** argv) {
     };
     BconvArgs af = a;
     af.dst = dext2;
+    int pf = 1;
     auto fused = [&]() {
         const dim3 g(16 * B * ntile);
+#define FZ(S, P) hipLaunchKernelGGL((k_bconv_cols<S, true, false, P>), g, dim3(256), 0, 0, af, T, ntile)
+#define FS(S) do { if (pf == 0) FZ(S, 0); else if (pf == 2) FZ(S, 2); else FZ(S, 1); } while (0)
         switch (nstep) {
-            case 1: hipLaunchKernelGGL((k_bconv_cols<1, true>), g, dim3(256), 0, 0, af, T, ntile); break;
-            case 2: hipLaunchKernelGGL((k_bconv_cols<2, true>), g, dim3(256), 0, 0, af, T, ntile); break;
-            default: hipLaunchKernelGGL((k_bconv_cols<3, true>), g, dim3(256), 0, 0, af, T, ntile); break;
+            case 1: FS(1); break;
+            case 2: FS(2); break;
+            default: FS(3); break;
         }
+#undef FS
+#undef FZ
     };
     pair(true, true);
+    for (int chk = 0; chk <= 2; chk++) {
+    pf = chk;
+    HC(hipMemset(dext2, 0, (size_t)B * neN * 8));
     fused();
     HC(hipDeviceSynchronize());
     {  // check: every target limb, residue equality
@@ -162,8 +170,9 @@ int main(int argc, char** argv) {
                     tot++;
                 }
             }
-        printf("check: %ld / %ld words differ mod q (max |fused| = %.2f q)\n", bad, tot, maxr);
+        printf("check PF%d: %ld / %ld words differ mod q (max |fused| = %.2f q)\n", pf, bad, tot, maxr);
         if (bad) return 1;
+    }
     }
     hipEvent_t e0, e1;
     HC(hipEventCreate(&e0));
@@ -185,11 +194,42 @@ int main(int argc, char** argv) {
         printf("%-28s %8.1f us  (%.2f TB/s of the fused kernel's read + write)\n", name, best * 1e3, by / (best * 1e-3) / 1e12);
         return best;
     };
+    // cold: the 256 MiB Infinity Cache flushed (a 1 GiB memset) before every launch, so the sources
+    // come from HBM as in the engine, where the INTT wrote them with streaming stores; per-launch events
+    void* flush;
+    HC(hipMalloc(&flush, 1ULL << 30));
+    auto cold = [&](const char* name, auto launch) {
+        launch();
+        HC(hipDeviceSynchronize());
+        float tot = 0;
+        for (int r = 0; r < 10; r++) {
+            HC(hipMemsetAsync(flush, r, 1ULL << 30));
+            HC(hipEventRecord(e0));
+            launch();
+            HC(hipEventRecord(e1));
+            HC(hipEventSynchronize(e1));
+            float ms;
+            HC(hipEventElapsedTime(&ms, e0, e1));
+            tot += ms;
+        }
+        printf("%-28s %8.1f us  (cold: Infinity Cache flushed before each launch)\n", name, tot / 10 * 1e3);
+    };
+    cold("cold bconv_mfma", [&] { pair(true, false); });
+    cold("cold cols", [&] { pair(false, true); });
+    for (pf = 0; pf <= 2; pf++) {
+        char nm[32];
+        snprintf(nm, sizeof nm, "cold fused PF%d", pf);
+        cold(nm, fused);
+    }
     for (int rep = 0; rep < 2; rep++) {
         timeit("bconv_mfma", [&] { pair(true, false); });
         timeit("cols", [&] { pair(false, true); });
         timeit("pair", [&] { pair(true, true); });
-        timeit("fused", fused);
+        for (pf = 0; pf <= 2; pf++) {
+            char nm[32];
+            snprintf(nm, sizeof nm, "fused PF%d", pf);
+            timeit(nm, fused);
+        }
     }
     return 0;
 }
