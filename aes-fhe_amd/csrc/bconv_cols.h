@@ -75,14 +75,88 @@ __device__ __forceinline__ void cols256_stages_store(double (&x)[16], double q, 
     for (int bb = 0; bb < 16; bb++) st_d(&out[(ap * 16 + bb) * 256 + c], x[bb]);
 }
 
+// the same stages for two register tiles at once (two targets of the workgroup, LDS tiles s0 / s1,
+// one barrier): the two dependency chains interleave (the kernel is issue-latency bound at two
+// waves per SIMD: SQ wait-inst 0.40 with one target at a time)
+__device__ __forceinline__ void cols256_stages_store2(double (&x0)[16], double (&x1)[16], double q0, double qi0,
+                                                      bool big0, const double* tg0, const double* twq0, u64* out0,
+                                                      double q1, double qi1, bool big1, const double* tg1,
+                                                      const double* twq1, u64* out1, double* s0, double* s1, int b,
+                                                      int cl, int c) {
+#pragma unroll
+    for (int st = 0; st < 4; st++) {
+        const int m = 1 << st, hh = 8 >> st;
+        if (st == 2) {
+            if (big0) {
+#pragma unroll
+                for (int a = 0; a < 16; a++) x0[a] = fred(x0[a], q0, qi0);
+            }
+            if (big1) {
+#pragma unroll
+                for (int a = 0; a < 16; a++) x1[a] = fred(x1[a], q1, qi1);
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 16; a++) {
+            if (a & hh) continue;
+            ct_f(x0[a], x0[a + hh], tg0[m + (a >> (4 - st))], q0);
+            ct_f(x1[a], x1[a + hh], tg1[m + (a >> (4 - st))], q1);
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 16; a++) {
+        s0[(a * 16 + b) * kPadF + cl] = x0[a];
+        s1[(a * 16 + b) * kPadF + cl] = x1[a];
+    }
+    __syncthreads();
+    const int ap = b;
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) {
+        x0[bb] = s0[(ap * 16 + bb) * kPadF + cl];
+        x1[bb] = s1[(ap * 16 + bb) * kPadF + cl];
+    }
+#pragma unroll
+    for (int st = 4; st < 8; st++) {
+        const int m = 1 << st, hh = 128 >> st;
+        if ((st & 1) == 0) {
+            if (big0) {
+#pragma unroll
+                for (int bb = 0; bb < 16; bb++) x0[bb] = fred(x0[bb], q0, qi0);
+            }
+            if (big1) {
+#pragma unroll
+                for (int bb = 0; bb < 16; bb++) x1[bb] = fred(x1[bb], q1, qi1);
+            }
+        }
+#pragma unroll
+        for (int bb = 0; bb < 16; bb++) {
+            if (bb & hh) continue;
+            const int ti = m + ap * (m >> 4) + (bb >> (8 - st));
+            ct_f(x0[bb], x0[bb + hh], twq0[ti], q0);
+            ct_f(x1[bb], x1[bb + hh], twq1[ti], q1);
+        }
+    }
+#pragma unroll
+    for (int bb = 0; bb < 16; bb++) {
+        st_d(&out0[(ap * 16 + bb) * 256 + c], x0[bb]);
+        st_d(&out1[(ap * 16 + bb) * 256 + c], x1[bb]);
+    }
+}
+
 // grid: 16 * nz * ntile workgroups (1-D, XCD-aware order above), 256 threads; nz = batch * nc
 // (a.nc components per element), ntile = ceil(nt / 4); 16 * nz must be a multiple of 8.
 // PF: row groups of source words in flight ahead of the one being converted (register prefetch;
-// 0 = load at use)
-template <int NSTEP, bool YIN, bool VC = false, int PF = 1>
-__global__ __launch_bounds__(256, 2) void k_bconv_cols(BconvArgs a, Tabs T, int ntile) {
-    __shared__ double s[2][256 * kPadF];
-    __shared__ double twq[4][256];
+// 0 = load at use).  TT: targets per workgroup (4, or 2: the MFMA's other two target rows are
+// dummies -- half the registers for the column tiles, twice the workgroups and source reads);
+// LT: LDS transpose tiles (2 alternate with one barrier per target; 1 needs a second barrier
+// before each reuse, for a smaller LDS footprint).
+// PAIR (LT = 2): the column stages of two targets at a time (cols256_stages_store2)
+template <int NSTEP, bool YIN, bool VC = false, int PF = 1, int TT = 4, int LT = 2, bool PAIR = false>
+__global__ __launch_bounds__(256, TT == 4 ? 2 : 3) void k_bconv_cols(BconvArgs a, Tabs T, int ntile) {
+    static_assert(TT == 4 || TT == 2, "4 or 2 targets per workgroup");
+    static_assert(LT == 1 || LT == 2, "1 or 2 LDS tiles");
+    __shared__ double s[LT][256 * kPadF];
+    __shared__ double twq[TT][256];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
     const int cl = tid & 15, b = tid >> 4;
     const int id = blockIdx.x, x8 = id & 7, j = id >> 3;
@@ -93,34 +167,32 @@ __global__ __launch_bounds__(256, 2) void k_bconv_cols(BconvArgs a, Tabs T, int 
     u64* dst = a.dst + (long)zb * a.dbs + (long)zc * a.dcs;
     auto limb_of = [&](int tau) { return tau < a.skip0 ? tau : tau + a.skipn; };
     auto pid_of = [&](int tl) { return tl <= a.tl_l ? tl : a.Lp1 + tl - a.tl_l - 1; };
-    const int tau0 = 4 * tile;
-    const int nlive = min(4, a.nt - tau0);
+    const int tau0 = TT * tile;
+    const int nlive = min(TT, a.nt - tau0);
     // the tile's stage 4-7 twiddles into LDS (read after the first barrier of the column stages)
 #pragma unroll
-    for (int m = 0; m < 4; m++)
+    for (int m = 0; m < TT; m++)
         if (m < nlive) twq[m][tid] = T.psif[((long)pid_of(limb_of(tau0 + m)) << logN) + tid];
     // A fragments of the tile (row r = (target r >> 3, byte plane (r & 3) + 4 ((r >> 2) & 1))),
     // fixed for the whole workgroup
     bc_v4i af[NSTEP];
     {
         const int row = lane & 31, ta = row >> 3, pb = (row & 3) + 4 * ((row >> 2) & 1);
-        const int tau = tau0 + ta;
+        const int tau = tau0 + ta;  // TT = 2: rows of ta >= 2 are dummies (pid 0), never stored
         const bc_v4i* ap =
-            (const bc_v4i*)(a.tab + ((long)(tau < a.nt ? pid_of(limb_of(tau)) : 0) * 8 + pb) * kBconvKT + 16 * h);
+            (const bc_v4i*)(a.tab + ((long)(ta < TT && tau < a.nt ? pid_of(limb_of(tau)) : 0) * 8 + pb) * kBconvKT + 16 * h);
 #pragma unroll
         for (int st = 0; st < NSTEP; st++) af[st] = ap[2 * st];
     }
     // this lane's source slots (lane half h of step st: 4 st + 2 h + {0, 1}); a dead slot reads
     // slot 0's word and is zeroed
     const u64* sp[NSTEP][2];
-    bool slive[NSTEP][2];
     double sq[NSTEP][2], sf[NSTEP][2];
 #pragma unroll
     for (int st = 0; st < NSTEP; st++)
 #pragma unroll
         for (int uu = 0; uu < 2; uu++) {
             const int sl = 4 * st + 2 * h + uu;
-            slive[st][uu] = sl < a.ns;
             const int i = sl < a.ns ? sl : 0;
             sp[st][uu] = src + ((long)i << logN) + bx * 16 + (c & 15);
             if (!YIN) {
@@ -129,7 +201,10 @@ __global__ __launch_bounds__(256, 2) void k_bconv_cols(BconvArgs a, Tabs T, int 
                 sf[st][uu] = a.sinvf[i];
             }
         }
-    double xv[4][16];
+    double xv[TT][16];
+    double ev[VC ? 4 * NSTEP : 1];  // VC: 1 / e_j per slot (0 past the sources), uniform
+#pragma unroll
+    for (int sl = 0; sl < (VC ? 4 * NSTEP : 0); sl++) ev[sl] = a.einv[sl];
     // the source words of row group ar (group g's column c is coefficient
     // (16 ar + 4 w + 2 g + (c >> 4), 16 bx + (c & 15))), PF row groups ahead of their use
     u64 raw[PF + 1][NSTEP][2][2];
@@ -161,7 +236,8 @@ __global__ __launch_bounds__(256, 2) void k_bconv_cols(BconvArgs a, Tabs T, int 
                         y = y < 0.0 ? y + q : y;
                         yb = (u64)__double_as_longlong(y + 4503599627370496.0) & 0xFFFFFFFFFFFFFULL;
                     }
-                    yb = slive[st][uu] ? yb : 0;
+                    // (a dead slot holds slot 0's word: its A bytes are zero -- bconv_row places
+                    // only live slots, and only their residue bytes -- so it adds nothing)
                     if (VC) ys[g][st][uu] = u2d(yb);
                     bf[g][st][2 * uu] = (int)(unsigned)yb ^ (int)0x80808080;
                     bf[g][st][2 * uu + 1] = (int)(unsigned)(yb >> 32) ^ (int)0x80808080;
@@ -180,8 +256,11 @@ __global__ __launch_bounds__(256, 2) void k_bconv_cols(BconvArgs a, Tabs T, int 
                 for (int hh = 0; hh < 2; hh++)
 #pragma unroll
                     for (int uu = 0; uu < 2; uu++) {
+                        // unconditional: a dead slot's 1/e is 0 in the tables (+0 leaves the sum
+                        // unchanged), and a runtime-guarded scalar load per term cost a scalar-cache
+                        // round trip each (DESIGN 4.5's lesson)
                         const int sl = 4 * st + 2 * hh + uu;
-                        if (sl < a.ns) sum = sum + yl[st][uu][hh] * a.einv[sl];
+                        sum = sum + yl[st][uu][hh] * ev[sl];
                     }
             const int vown = (int)__builtin_rint(sum);  // group h's v
             const auto pr = __builtin_amdgcn_permlane32_swap((unsigned)vown, (unsigned)vown, false, false);
@@ -209,7 +288,7 @@ __global__ __launch_bounds__(256, 2) void k_bconv_cols(BconvArgs a, Tabs T, int 
         // epilogue (bconv_mfma.h): this half's 4 planes of target m, group g, as one exact double;
         // the swap gives lane (c, h) group h's column c = its own coefficient of the column layout
 #pragma unroll
-        for (int m = 0; m < 4; m++) {
+        for (int m = 0; m < TT; m++) {
             if (m >= nlive) break;  // block-uniform
             double part[2];
 #pragma unroll
@@ -225,16 +304,40 @@ __global__ __launch_bounds__(256, 2) void k_bconv_cols(BconvArgs a, Tabs T, int 
             xv[m][ar] = fred(lo + fmul_rem(hi, w32, f32, q) + cr, q, qi);
         }
     }
-    // the column stages of each live target; LDS tile m & 1 (the barrier inside the stages of
-    // target m + 1 orders every read of tile m & 1 for target m before its reuse by target m + 2)
+    // the column stages of each live target; LDS tile m % LT (LT = 2: the barrier inside the
+    // stages of target m + 1 orders every read of tile m & 1 for target m before its reuse by
+    // target m + 2; LT = 1: one more barrier before each reuse)
     __syncthreads();  // twq
+    if constexpr (LT == 2 && PAIR) {  // two targets at a time (interleaved chains, one barrier per pair)
 #pragma unroll
-    for (int m = 0; m < 4; m++) {
-        if (m >= nlive) break;
-        const int tl = limb_of(tau0 + m), pid = pid_of(tl);
-        const double q = (double)T.q[pid], qi = T.qinv[pid];
-        cols256_stages_store(xv[m], q, qi, q >= kBigPrime, T.psif + ((long)pid << logN), twq[m], s[m & 1],
-                             dst + ((long)tl << logN), b, cl, bx * 16 + cl);
+        for (int m = 0; m < TT; m += 2) {
+            if (m >= nlive) break;
+            if (m > 0) __syncthreads();  // the previous pair's LDS reads are done
+            const int tl0 = limb_of(tau0 + m), pid0 = pid_of(tl0);
+            const double q0 = (double)T.q[pid0], qi0 = T.qinv[pid0];
+            if (m + 1 < nlive) {
+                const int tl1 = limb_of(tau0 + m + 1), pid1 = pid_of(tl1);
+                const double q1 = (double)T.q[pid1], qi1 = T.qinv[pid1];
+                cols256_stages_store2(xv[m], xv[m + 1], q0, qi0, q0 >= kBigPrime, T.psif + ((long)pid0 << logN), twq[m],
+                                      dst + ((long)tl0 << logN), q1, qi1, q1 >= kBigPrime,
+                                      T.psif + ((long)pid1 << logN), twq[m + 1], dst + ((long)tl1 << logN), s[0], s[1],
+                                      b, cl, bx * 16 + cl);
+            } else {
+                cols256_stages_store(xv[m], q0, qi0, q0 >= kBigPrime, T.psif + ((long)pid0 << logN), twq[m], s[0],
+                                     dst + ((long)tl0 << logN), b, cl, bx * 16 + cl);
+            }
+        }
+    } else {  // one target at a time; LT = 2: tiles alternate (the barrier inside the stages of
+              // target m + 1 orders the reads of tile m & 1 before its reuse), LT = 1: a second barrier
+#pragma unroll
+        for (int m = 0; m < TT; m++) {
+            if (m >= nlive) break;
+            if (LT == 1 && m > 0) __syncthreads();
+            const int tl = limb_of(tau0 + m), pid = pid_of(tl);
+            const double q = (double)T.q[pid], qi = T.qinv[pid];
+            cols256_stages_store(xv[m], q, qi, q >= kBigPrime, T.psif + ((long)pid << logN), twq[m], s[m % LT],
+                                 dst + ((long)tl << logN), b, cl, bx * 16 + cl);
+        }
     }
 }
 

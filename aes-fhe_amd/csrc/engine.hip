@@ -2155,9 +2155,10 @@ static bool modup_fused_on() {
     static const bool on = !(getenv("AESFHE_MODUP_FUSED") && !atoi(getenv("AESFHE_MODUP_FUSED")));
     return on;
 }
-// source row groups prefetched ahead (bconv_cols.h PF; AESFHE_BCC_PF=0/1/2 for A/B runs)
+// source row groups prefetched ahead (bconv_cols.h PF; AESFHE_BCC_PF=0/1/2 for A/B runs); 3 = PF 1
+// with the column stages of two targets interleaved (PAIR)
 static int bcc_pf() {
-    static const int pf = getenv("AESFHE_BCC_PF") ? std::max(0, std::min(2, atoi(getenv("AESFHE_BCC_PF")))) : 1;
+    static const int pf = getenv("AESFHE_BCC_PF") ? std::max(0, std::min(3, atoi(getenv("AESFHE_BCC_PF")))) : 1;
     return pf;
 }
 template <bool VC>
@@ -2169,7 +2170,9 @@ static void launch_bconv_cols_t(aesfhe_engine* e, const BconvArgs& a, int nz, in
     const Tabs T = e->tabs();
     const int pf = bcc_pf();
 #define BCC(S, P) hipLaunchKernelGGL((k_bconv_cols<S, true, VC, P>), g, dim3(256), 0, e->stream, a, T, ntile)
-#define BCS(S) do { if (pf == 0) BCC(S, 0); else if (pf == 2) BCC(S, 2); else BCC(S, 1); } while (0)
+#define BCS(S) do { if (pf == 0) BCC(S, 0); else if (pf == 2) BCC(S, 2); else if (pf == 3) \
+        hipLaunchKernelGGL((k_bconv_cols<S, true, VC, 1, 4, 2, true>), g, dim3(256), 0, e->stream, a, T, ntile); \
+        else BCC(S, 1); } while (0)
     switch (nstep) {
         case 1: BCS(1); break;
         case 2: BCS(2); break;
