@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256, TT == 4 ? 2 : 3) void k_bconv_cols(BconvArgs a
     for (int ar = 0; ar < 16; ar++) {
         if (ar + PF < 16) load(raw[(ar + PF) % (PF + 1)], ar + PF);
         bc_v4i bf[2][NSTEP];
-        double ys[2][NSTEP][2];  // VC: the slots' y values (dead slots 0)
+        double ys[2][NSTEP][2];  // VC: the slots' y values (a dead slot's 1/e is 0)
 #pragma unroll
         for (int st = 0; st < NSTEP; st++)
 #pragma unroll
