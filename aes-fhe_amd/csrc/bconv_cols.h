@@ -202,6 +202,15 @@ __global__ __launch_bounds__(256, TT == 4 ? 2 : 3) void k_bconv_cols(BconvArgs a
             }
         }
     double xv[TT][16];
+    // the epilogue's per-target constants, loaded once (unguarded: a target past nt reads pid 0's),
+    // not per row group behind the live-target check (a scalar-cache round trip each)
+    double eq[TT], eqi[TT], ew32[TT], ef32[TT], ecr[TT];
+#pragma unroll
+    for (int m = 0; m < TT; m++) {
+        const int pid = tau0 + m < a.nt ? pid_of(limb_of(tau0 + m)) : 0;
+        const double* pc = a.pc + 4 * pid;
+        eq[m] = pc[0], eqi[m] = pc[1], ew32[m] = pc[2], ef32[m] = pc[3], ecr[m] = a.corr[pid];
+    }
     double ev[VC ? 4 * NSTEP : 1];  // VC: 1 / e_j per slot (0 past the sources), uniform
 #pragma unroll
     for (int sl = 0; sl < (VC ? 4 * NSTEP : 0); sl++) ev[sl] = a.einv[sl];
@@ -298,10 +307,7 @@ __global__ __launch_bounds__(256, TT == 4 ? 2 : 3) void k_bconv_cols(BconvArgs a
             }
             double lo, hi;
             swap_halves(part[0], part[1], lo, hi);
-            const int pid = pid_of(limb_of(tau0 + m));
-            const double* pc = a.pc + 4 * pid;
-            const double q = pc[0], qi = pc[1], w32 = pc[2], f32 = pc[3], cr = a.corr[pid];
-            xv[m][ar] = fred(lo + fmul_rem(hi, w32, f32, q) + cr, q, qi);
+            xv[m][ar] = fred(lo + fmul_rem(hi, ew32[m], ef32[m], eq[m]) + ecr[m], eq[m], eqi[m]);
         }
     }
     // the column stages of each live target; LDS tile m % LT (LT = 2: the barrier inside the
