@@ -67,10 +67,10 @@ WORKLOAD = {
 SEED = 0x5EED5EED  # the CPU baseline's engine (reproducible); the GPU ranks share a 256-bit seed
 
 PEAK_FP64_TFLOPS = 78.6  # MI355X vector FP64 (AMD spec: 256 CUs x 128 FLOP/clk x 2.4 GHz)
-PMC_FILE = ROOT / "profiles" / "r05" / "pmc" / "round_traffic.json"
+PMC_FILE = ROOT / "profiles" / "r06" / "pmc" / "round_traffic.json"
 PMC_NOTE = ("HBM bytes per launch measured with rocprofv3 --pmc FETCH_SIZE (x2, the gfx950 "
             "correction of MI355X_MICROARCH.md) and --pmc WRITE_SIZE, separate passes, over exactly one "
-            "bench round step (tools/pmc_traffic.py -> profiles/r05/pmc/round_traffic.json, stamped "
+            "bench round step (tools/pmc_traffic.py -> profiles/r06/pmc/round_traffic.json, stamped "
             "with the git HEAD it measured and the hash of the kernel sources it ran)")
 # kernel instantiations (aesfhe_engine_profile_kernels labels "class.variant") -> the kernels they
 # launch.  EPI is k_nttf_rows_ks's epilogue template argument: 0 the canonical accumulators into acc,
