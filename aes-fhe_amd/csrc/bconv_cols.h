@@ -36,9 +36,11 @@ namespace aesfhe {
 // the 8 forward column stages (R = 256) of the register tile x (x[a] = row 16 a + b of column c),
 // transposed through the LDS tile s (all 256 threads of the workgroup; s must not be read by any
 // thread from an earlier use -- the caller's barrier discipline), twiddles: stages 0-3 from the
-// prime's table tg (uniform: scalar loads), 4-7 from its LDS copy twq; raw doubles stored to out
+// prime's tables tg (w / q) and cw (w, Tabs::cw) -- uniform: scalar loads, no w = rint(wq q) on the
+// VALU --, 4-7 from the LDS copy twq of w / q; raw doubles stored to out
 __device__ __forceinline__ void cols256_stages_store(double (&x)[16], double q, double qi, bool big, const double* tg,
-                                                     const double* twq, double* s, u64* out, int b, int cl, int c) {
+                                                     const double* cw, const double* twq, double* s, u64* out, int b,
+                                                     int cl, int c) {
 #pragma unroll
     for (int st = 0; st < 4; st++) {
         const int m = 1 << st, hh = 8 >> st;
@@ -49,7 +51,8 @@ __device__ __forceinline__ void cols256_stages_store(double (&x)[16], double q, 
 #pragma unroll
         for (int a = 0; a < 16; a++) {
             if (a & hh) continue;
-            ct_f(x[a], x[a + hh], tg[m + (a >> (4 - st))], q);
+            const int ti = m + (a >> (4 - st));
+            ct_fw(x[a], x[a + hh], cw[ti], tg[ti], q);
         }
     }
 #pragma unroll
@@ -75,83 +78,15 @@ __device__ __forceinline__ void cols256_stages_store(double (&x)[16], double q, 
     for (int bb = 0; bb < 16; bb++) st_d(&out[(ap * 16 + bb) * 256 + c], x[bb]);
 }
 
-// the same stages for two register tiles at once (two targets of the workgroup, LDS tiles s0 / s1,
-// one barrier): the two dependency chains interleave (the kernel is issue-latency bound at two
-// waves per SIMD: SQ wait-inst 0.40 with one target at a time)
-__device__ __forceinline__ void cols256_stages_store2(double (&x0)[16], double (&x1)[16], double q0, double qi0,
-                                                      bool big0, const double* tg0, const double* twq0, u64* out0,
-                                                      double q1, double qi1, bool big1, const double* tg1,
-                                                      const double* twq1, u64* out1, double* s0, double* s1, int b,
-                                                      int cl, int c) {
-#pragma unroll
-    for (int st = 0; st < 4; st++) {
-        const int m = 1 << st, hh = 8 >> st;
-        if (st == 2) {
-            if (big0) {
-#pragma unroll
-                for (int a = 0; a < 16; a++) x0[a] = fred(x0[a], q0, qi0);
-            }
-            if (big1) {
-#pragma unroll
-                for (int a = 0; a < 16; a++) x1[a] = fred(x1[a], q1, qi1);
-            }
-        }
-#pragma unroll
-        for (int a = 0; a < 16; a++) {
-            if (a & hh) continue;
-            ct_f(x0[a], x0[a + hh], tg0[m + (a >> (4 - st))], q0);
-            ct_f(x1[a], x1[a + hh], tg1[m + (a >> (4 - st))], q1);
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < 16; a++) {
-        s0[(a * 16 + b) * kPadF + cl] = x0[a];
-        s1[(a * 16 + b) * kPadF + cl] = x1[a];
-    }
-    __syncthreads();
-    const int ap = b;
-#pragma unroll
-    for (int bb = 0; bb < 16; bb++) {
-        x0[bb] = s0[(ap * 16 + bb) * kPadF + cl];
-        x1[bb] = s1[(ap * 16 + bb) * kPadF + cl];
-    }
-#pragma unroll
-    for (int st = 4; st < 8; st++) {
-        const int m = 1 << st, hh = 128 >> st;
-        if ((st & 1) == 0) {
-            if (big0) {
-#pragma unroll
-                for (int bb = 0; bb < 16; bb++) x0[bb] = fred(x0[bb], q0, qi0);
-            }
-            if (big1) {
-#pragma unroll
-                for (int bb = 0; bb < 16; bb++) x1[bb] = fred(x1[bb], q1, qi1);
-            }
-        }
-#pragma unroll
-        for (int bb = 0; bb < 16; bb++) {
-            if (bb & hh) continue;
-            const int ti = m + ap * (m >> 4) + (bb >> (8 - st));
-            ct_f(x0[bb], x0[bb + hh], twq0[ti], q0);
-            ct_f(x1[bb], x1[bb + hh], twq1[ti], q1);
-        }
-    }
-#pragma unroll
-    for (int bb = 0; bb < 16; bb++) {
-        st_d(&out0[(ap * 16 + bb) * 256 + c], x0[bb]);
-        st_d(&out1[(ap * 16 + bb) * 256 + c], x1[bb]);
-    }
-}
-
 // grid: 16 * nz * ntile workgroups (1-D, XCD-aware order above), 256 threads; nz = batch * nc
 // (a.nc components per element), ntile = ceil(nt / 4); 16 * nz must be a multiple of 8.
 // PF: row groups of source words in flight ahead of the one being converted (register prefetch;
 // 0 = load at use).  TT: targets per workgroup (4, or 2: the MFMA's other two target rows are
 // dummies -- half the registers for the column tiles, twice the workgroups and source reads);
 // LT: LDS transpose tiles (2 alternate with one barrier per target; 1 needs a second barrier
-// before each reuse, for a smaller LDS footprint).
-// PAIR (LT = 2): the column stages of two targets at a time (cols256_stages_store2)
-template <int NSTEP, bool YIN, bool VC = false, int PF = 1, int TT = 4, int LT = 2, bool PAIR = false>
+// before each reuse, for a smaller LDS footprint).  (Two targets' column stages interleaved -- PAIR,
+// round 6 -- measured slower and were removed: DESIGN 4.8.)
+template <int NSTEP, bool YIN, bool VC = false, int PF = 1, int TT = 4, int LT = 2>
 __global__ __launch_bounds__(256, TT == 4 ? 2 : 3) void k_bconv_cols(BconvArgs a, Tabs T, int ntile) {
     static_assert(TT == 4 || TT == 2, "4 or 2 targets per workgroup");
     static_assert(LT == 1 || LT == 2, "1 or 2 LDS tiles");
@@ -314,36 +249,14 @@ __global__ __launch_bounds__(256, TT == 4 ? 2 : 3) void k_bconv_cols(BconvArgs a
     // stages of target m + 1 orders every read of tile m & 1 for target m before its reuse by
     // target m + 2; LT = 1: one more barrier before each reuse)
     __syncthreads();  // twq
-    if constexpr (LT == 2 && PAIR) {  // two targets at a time (interleaved chains, one barrier per pair)
 #pragma unroll
-        for (int m = 0; m < TT; m += 2) {
-            if (m >= nlive) break;
-            if (m > 0) __syncthreads();  // the previous pair's LDS reads are done
-            const int tl0 = limb_of(tau0 + m), pid0 = pid_of(tl0);
-            const double q0 = (double)T.q[pid0], qi0 = T.qinv[pid0];
-            if (m + 1 < nlive) {
-                const int tl1 = limb_of(tau0 + m + 1), pid1 = pid_of(tl1);
-                const double q1 = (double)T.q[pid1], qi1 = T.qinv[pid1];
-                cols256_stages_store2(xv[m], xv[m + 1], q0, qi0, q0 >= kBigPrime, T.psif + ((long)pid0 << logN), twq[m],
-                                      dst + ((long)tl0 << logN), q1, qi1, q1 >= kBigPrime,
-                                      T.psif + ((long)pid1 << logN), twq[m + 1], dst + ((long)tl1 << logN), s[0], s[1],
-                                      b, cl, bx * 16 + cl);
-            } else {
-                cols256_stages_store(xv[m], q0, qi0, q0 >= kBigPrime, T.psif + ((long)pid0 << logN), twq[m], s[0],
-                                     dst + ((long)tl0 << logN), b, cl, bx * 16 + cl);
-            }
-        }
-    } else {  // one target at a time; LT = 2: tiles alternate (the barrier inside the stages of
-              // target m + 1 orders the reads of tile m & 1 before its reuse), LT = 1: a second barrier
-#pragma unroll
-        for (int m = 0; m < TT; m++) {
-            if (m >= nlive) break;
-            if (LT == 1 && m > 0) __syncthreads();
-            const int tl = limb_of(tau0 + m), pid = pid_of(tl);
-            const double q = (double)T.q[pid], qi = T.qinv[pid];
-            cols256_stages_store(xv[m], q, qi, q >= kBigPrime, T.psif + ((long)pid << logN), twq[m], s[m % LT],
-                                 dst + ((long)tl << logN), b, cl, bx * 16 + cl);
-        }
+    for (int m = 0; m < TT; m++) {
+        if (m >= nlive) break;
+        if (LT == 1 && m > 0) __syncthreads();
+        const int tl = limb_of(tau0 + m), pid = pid_of(tl);
+        const double q = (double)T.q[pid], qi = T.qinv[pid];
+        cols256_stages_store(xv[m], q, qi, q >= kBigPrime, T.psif + ((long)pid << logN), T.cw + (long)pid * kColW,
+                             twq[m], s[m % LT], dst + ((long)tl << logN), b, cl, bx * 16 + cl);
     }
 }
 

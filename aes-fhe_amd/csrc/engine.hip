@@ -157,6 +157,7 @@ struct aesfhe_engine {
     double *qinv, *psif, *ipsif, *ninvf;
     double *rtwf = nullptr, *irtwf = nullptr;  // N = 2^16 row-pass twiddle factors [np][256][8] (ntt256f.h)
     Tw *tw, *itw;
+    double *cw = nullptr, *icw = nullptr;  // [np][kColW] uniform column-stage twiddles w (kernels.h)
     u64* iroot;  // host copy only needed
     std::vector<u64> h_iroot;
     // base conversion tables
@@ -210,6 +211,8 @@ struct aesfhe_engine {
         t.ninvf = ninvf;
         t.tw = tw;
         t.itw = itw;
+        t.cw = cw;
+        t.icw = icw;
         t.logN = logN;
         t.Lp1 = Lp1;
         return t;
@@ -655,6 +658,16 @@ static void build_tables(aesfhe_engine* e) {
         up(htw, &e->tw);
         up(hitw, &e->itw);
     }
+    {
+        std::vector<double> hcw((size_t)np * kColW), hicw((size_t)np * kColW);
+        for (int p = 0; p < np; p++)
+            for (int k = 0; k < kColW; k++) {
+                hcw[(size_t)p * kColW + k] = (double)hpsi[(size_t)p * N + (k < N ? k : 0)];
+                hicw[(size_t)p * kColW + k] = (double)hipsi[(size_t)p * N + (k < N ? k : 0)];
+            }
+        up(hcw, &e->cw);
+        up(hicw, &e->icw);
+    }
 
     // ModUp tables per (digit j, width a <= alpha): hatinv[i], hat[i][pid]; stride A = alpha
     const int A = e->A;
@@ -958,7 +971,7 @@ static void engine_teardown(aesfhe_engine* e) {
                     e->md_pinvf, e->rs_invf, e->ring_d, e->tw, e->itw, e->mdr_invf, e->mdr_hatf,
                     e->mdr_dinv, e->mdr_dinvf, e->pmodf, e->mdr_einv, e->mdr_dmodf, e->md_einv,
                     e->bc_mu_tab, e->bc_md_tab, e->bc_mdr_tab, e->bc_mu_corr, e->bc_md_corr, e->bc_mdr_corr,
-                    e->bc_pc, e->mu_nhatf, e->md_ninvf, e->mdr_ninvf};
+                    e->bc_pc, e->mu_nhatf, e->md_ninvf, e->mdr_ninvf, e->cw, e->icw};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto& kv : e->poly2_tabs) hipFree(kv.second);
@@ -2155,10 +2168,10 @@ static bool modup_fused_on() {
     static const bool on = !(getenv("AESFHE_MODUP_FUSED") && !atoi(getenv("AESFHE_MODUP_FUSED")));
     return on;
 }
-// source row groups prefetched ahead (bconv_cols.h PF; AESFHE_BCC_PF=0/1/2 for A/B runs); 3 = PF 1
-// with the column stages of two targets interleaved (PAIR)
+// source row groups prefetched ahead (bconv_cols.h PF; AESFHE_BCC_PF=0 for A/B runs; PF 2 measured
+// slower and was dropped)
 static int bcc_pf() {
-    static const int pf = getenv("AESFHE_BCC_PF") ? std::max(0, std::min(3, atoi(getenv("AESFHE_BCC_PF")))) : 1;
+    static const int pf = getenv("AESFHE_BCC_PF") ? std::max(0, std::min(1, atoi(getenv("AESFHE_BCC_PF")))) : 1;
     return pf;
 }
 template <bool VC>
@@ -2170,9 +2183,7 @@ static void launch_bconv_cols_t(aesfhe_engine* e, const BconvArgs& a, int nz, in
     const Tabs T = e->tabs();
     const int pf = bcc_pf();
 #define BCC(S, P) hipLaunchKernelGGL((k_bconv_cols<S, true, VC, P>), g, dim3(256), 0, e->stream, a, T, ntile)
-#define BCS(S) do { if (pf == 0) BCC(S, 0); else if (pf == 2) BCC(S, 2); else if (pf == 3) \
-        hipLaunchKernelGGL((k_bconv_cols<S, true, VC, 1, 4, 2, true>), g, dim3(256), 0, e->stream, a, T, ntile); \
-        else BCC(S, 1); } while (0)
+#define BCS(S) do { if (pf == 0) BCC(S, 0); else BCC(S, 1); } while (0)
     switch (nstep) {
         case 1: BCS(1); break;
         case 2: BCS(2); break;

@@ -119,6 +119,8 @@ __device__ __forceinline__ u64* span_ptr(const Span& s, int y, int logN, int Lp1
     return s.base + (long)(p & s.pmask) * s.pstride + ((long)l << logN);
 }
 
+constexpr int kColW = 64;  // Tabs::cw / icw entries per prime (R = 512 reads up to index 47)
+
 struct Tabs {
     const u64* q;
     const double* qinv;
@@ -132,6 +134,11 @@ struct Tabs {
     const double* ninvf;
     const struct Tw* tw;   // [np][N] {psi^{brv(k)}, psi^{brv(k)}/q} interleaved (16 B)
     const struct Tw* itw;  // [np][N] inverse
+    // [np][kColW] psi^{brv(k)} (cw) / psi^{-brv(k)} (icw) as exact doubles, k < kColW: the column
+    // passes' wave-uniform stages read w by scalar load beside w/q instead of recomputing
+    // w = rint(wq q) on the VALU (2 instructions per twiddle per wave; round 6)
+    const double* cw;
+    const double* icw;
     int logN;
     int Lp1;
 };

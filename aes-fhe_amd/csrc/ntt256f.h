@@ -120,6 +120,7 @@ __device__ __forceinline__ void nttf_fwd_cols_body(const Span& src, const Span& 
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* tg = T.psif + ((long)pid << T.logN);
+    const double* cw = T.cw + (long)pid * kColW;
 #pragma unroll
     for (int h = 0; h < H; h++) twq[tid + 256 * h] = tg[tid + 256 * h];
     double x[16 * H];
@@ -139,9 +140,9 @@ __device__ __forceinline__ void nttf_fwd_cols_body(const Span& src, const Span& 
         }
     __syncthreads();
     if (H == 2) {  // stage m = 1 across the halves: canonical in, (-q, 2q) out
-        const double w = tg[1];
+        const double w = cw[1], wq = tg[1];
 #pragma unroll
-        for (int a = 0; a < 16; a++) ct_f(x[a], x[16 + a], w, q);
+        for (int a = 0; a < 16; a++) ct_fw(x[a], x[16 + a], w, wq, q);
     }
 #pragma unroll
     for (int h = 0; h < H; h++) {
@@ -157,7 +158,8 @@ __device__ __forceinline__ void nttf_fwd_cols_body(const Span& src, const Span& 
 #pragma unroll
             for (int a = 0; a < 16; a++) {
                 if (a & hh) continue;
-                ct_f(xh[a], xh[a + hh], tg[m * mul + (a >> (4 - st))], q);  // uniform: scalar load
+                const int ti = m * mul + (a >> (4 - st));  // uniform: scalar loads of w and w/q
+                ct_fw(xh[a], xh[a + hh], cw[ti], tg[ti], q);
             }
         }
         if (h > 0) __syncthreads();  // the previous half's LDS reads are done
@@ -460,6 +462,7 @@ __global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T, const d
     const double q = (double)T.q[pid], qi = T.qinv[pid];
     const bool big = q >= kBigPrime;
     const double* tg = T.ipsif + ((long)pid << T.logN);
+    const double* icw = T.icw + (long)pid * kColW;
 #pragma unroll
     for (int h = 0; h < H; h++) twq[tid + 256 * h] = tg[tid + 256 * h];
     const int ap = b;
@@ -501,7 +504,8 @@ __global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T, const d
 #pragma unroll
                 for (int a = 0; a < 16; a++) {
                     if (a & ta) continue;
-                    gs_f<decltype(fold)::value>(xh[a], xh[a + ta], tg[base + (a >> (st - 3))], q, qi);  // uniform
+                    const int ti = base + (a >> (st - 3));  // uniform: scalar loads of w and w/q
+                    gs_fw<decltype(fold)::value>(xh[a], xh[a + ta], icw[ti], tg[ti], q, qi);
                 }
             }
         };
@@ -509,12 +513,12 @@ __global__ __launch_bounds__(256) void k_nttf_inv_cols(Span dst, Tabs T, const d
         else stages_hi(std::false_type{});
     }
     if (H == 2) {  // stage m = 1 across the halves (inputs folded to |x| <= q/2 + 1)
-        const double w = tg[1];
+        const double w = icw[1], wq = tg[1];
 #pragma unroll
         for (int a = 0; a < 16; a++) {
             x[a] = fred(x[a], q, qi);
             x[16 + a] = fred(x[16 + a], q, qi);
-            gs_f<false>(x[a], x[16 + a], w, q, qi);
+            gs_fw<false>(x[a], x[16 + a], w, wq, q, qi);
         }
     }
     const double nif = LF ? lf[blockIdx.y % dst.nl] : T.ninvf[pid];

@@ -23,6 +23,7 @@
 
 #include "../aes-fhe_amd/csrc/kernels_ops.h"
 #include "../aes-fhe_amd/csrc/ntt256f.h"
+#include "tabs_cw.h"
 using namespace aesfhe;
 
 #define CK(x)                                                                    \
@@ -194,6 +195,7 @@ int main(int argc, char** argv) {
     T.qinv = dqinv;
     T.psif = dpsif;
     T.logN = logN;
+    T.cw = tools_make_cw(dpsif, dq, np, logN);
     T.Lp1 = Lp1;
     hipStream_t s;
     CK(hipStreamCreate(&s));

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../aes-fhe_amd/csrc/bconv_cols.h"
+#include "tabs_cw.h"
 using namespace aesfhe;
 #define HC(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
@@ -116,6 +117,7 @@ int main(int argc, char** argv) {
     HC(hipMemset(dext2, 0, ow * 8));
     Tabs T{};
     T.q = dq, T.qinv = dqinv, T.psif = dpsif, T.logN = LOGN, T.Lp1 = Lp1;
+    T.cw = tools_make_cw(dpsif, dq, np, LOGN);
     std::vector<double> einv(16, 0.0), sinvmd(16, 0.0);  // ModDown: 1 / e_j of the sources q_30, p_0 .. p_9
     for (int j = 0; j < K + 1; j++) einv[j] = sinvmd[j] = 1.0 / (double)q[j == 0 ? l : Lp1 + j - 1];
     double* deinv = (double*)up(einv.data(), einv.size() * 8);

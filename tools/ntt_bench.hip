@@ -8,6 +8,7 @@
 #include <vector>
 #include "../aes-fhe_amd/csrc/ntt256.h"
 #include "../aes-fhe_amd/csrc/ntt256f.h"
+#include "tabs_cw.h"
 using namespace aesfhe;
 #define CK(x) do { hipError_t e_ = (x); if (e_) { printf("%s @%d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
@@ -120,6 +121,7 @@ int main() {
     timeit("rows var2 (no tw load)", [&] { hipLaunchKernelGGL(k_rows_var<2>, dim3(16, L), dim3(256), 0, 0, s, T, dw8); });
     {   // fp64 passes need the w/q tables: reuse the 8 B table for both directions
         T.psif = dw8; T.ipsif = dw8;
+        T.cw = T.icw = tools_make_cw(dw8, dq, 1, logN);
         std::vector<double> hf(1, 1.0 / q); double* dnf; CK(hipMalloc(&dnf, 8)); CK(hipMemcpy(dnf, hf.data(), 8, hipMemcpyHostToDevice));
         T.ninvf = dnf;
         timeit("f64 fwd_cols", [&] { hipLaunchKernelGGL(k_nttf_fwd_cols, dim3(16, L), dim3(256), 0, 0, s, s2, T); });

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <vector>
 #include "../aes-fhe_amd/csrc/ntt256f.h"
+#include "tabs_cw.h"
 using namespace aesfhe;
 #define CK(x) do { hipError_t e_ = (x); if (e_) { printf("%s @%d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
@@ -21,6 +22,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&src, (size_t)L * N * 8)); CK(hipMalloc(&dst, (size_t)L * N * 8));
     CK(hipMemset(src, 0, (size_t)L * N * 8));
     Tabs T{}; T.q = dq; T.qinv = dqi; T.psif = dw8; T.ipsif = dw8; T.logN = logN; T.Lp1 = 1;
+    T.cw = T.icw = tools_make_cw(dw8, dq, 1, logN);
     hipStream_t s1, s2; CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking)); CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
     std::vector<hipEvent_t> ev(1024);
     for (auto& e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../aes-fhe_amd/csrc/ntt256f.h"
+#include "tabs_cw.h"
 using namespace aesfhe;
 
 __global__ __launch_bounds__(256) void k_fused_fwd(Span src, Span mid, Tabs T, unsigned* head, unsigned* cnt,
@@ -121,6 +122,7 @@ int main(int argc, char** argv) {
     T.psif = up(hpsif);
     T.rtwf = up(hr);
     T.logN = logN;
+    T.cw = tools_make_cw(T.psif, T.q, np, logN);
     T.Lp1 = np;
     std::vector<u64> h((size_t)limbs * N);
     std::mt19937_64 rng(7);

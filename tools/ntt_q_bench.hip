@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../aes-fhe_amd/csrc/ntt256f.h"
+#include "tabs_cw.h"
 using namespace aesfhe;
 
 // ===== experimental one-launch forward NTT kernels (not in the engine: measured slower than
@@ -484,6 +485,7 @@ int main(int argc, char** argv) {
     T.psif = up(hpsif);
     T.rtwf = up(hr);
     T.logN = logN;
+    T.cw = tools_make_cw(T.psif, T.q, np, logN);
     T.Lp1 = np;
     // limb y uses prime y % np: one "poly" per np limbs
     std::vector<u64> h((size_t)limbs * N);
