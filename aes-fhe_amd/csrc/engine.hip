@@ -2179,6 +2179,8 @@ static void launch_bconv_cols_t(aesfhe_engine* e, const BconvArgs& a, int nz, in
     const int nstep = (nslots + 3) / 4, ntile = (a.nt + 3) / 4;
     if (e->logN != 16 || nstep < 1 || nstep > 4 || ntile < 1 || (16 * nz) % 8)
         throw_err(AESFHE_EUNSUPPORTED, "fused base conversion of %d slots to %d targets", nslots, a.nt);
+    if (!a.src || !a.dst || !a.tab || !a.corr || !a.pc || (VC && !a.einv))
+        throw_err(AESFHE_EUNSUPPORTED, "fused base conversion with a missing table");  // never launch on a null table
     const dim3 g((unsigned)(16 * nz * ntile));
     const Tabs T = e->tabs();
     const int pf = bcc_pf();
