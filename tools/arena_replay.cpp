@@ -3,6 +3,7 @@
 // policy, at the end of the trace and at its largest.  Dev tool for VERDICT r4 item 7.
 //   g++ -O2 -std=c++17 -o tools/arena_replay tools/arena_replay.cpp
 //   tools/arena_replay TRACE [TRACE ...]
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -264,6 +265,10 @@ int main(int argc, char** argv) {
             size_t bigheld = 0, biglivesz = 0;
             std::unordered_map<unsigned long long, std::pair<int, char*>> map;
             size_t peak_total = 0, max_held = 0;
+            // host time of the allocator's get / put (first fit scans the free list)
+            double get_ns = 0, put_ns = 0, get_max_ns = 0;
+            long ngets = 0, nputs = 0;
+            using clk = std::chrono::steady_clock;
             for (const auto& e : ev) {
                 int k = pol.two && e.tag == 't' ? 1 : 0;
                 if (pol.buckets && e.op == 'g')
@@ -299,7 +304,10 @@ int main(int argc, char** argv) {
                         biglivesz += e.n;
                         map[e.p] = {9, p};
                     } else {
+                        const auto t0 = clk::now();
                         char* p = (char*)ar[k].getx(e.n);
+                        const double dt = std::chrono::duration<double, std::nano>(clk::now() - t0).count();
+                        get_ns += dt, get_max_ns = std::max(get_max_ns, dt), ngets++;
                         map[e.p] = {k, p};
                     }
                 } else if (e.op == 'p') {
@@ -311,7 +319,9 @@ int main(int argc, char** argv) {
                         biglivesz -= n;
                         bigfree.insert({n, it->second.second});
                     } else {
+                        const auto t0 = clk::now();
                         ar[it->second.first].put(it->second.second);
+                        put_ns += std::chrono::duration<double, std::nano>(clk::now() - t0).count(), nputs++;
                     }
                     map.erase(it);
                 } else if (e.op == 's') {
@@ -327,9 +337,11 @@ int main(int argc, char** argv) {
                 max_held = std::max(max_held, ar[0].held + ar[1].held + ar[2].held + ar[3].held + bigheld);
             }
             const size_t held = ar[0].held + ar[1].held + ar[2].held + ar[3].held + bigheld;
-            printf("  %-36s held %6.1f GB (max %6.1f)  peak live %6.1f GB  held/peak %.3f  mallocs %lld\n", pol.name, held / 1e9,
+            printf("  %-36s held %6.1f GB (max %6.1f)  peak live %6.1f GB  held/peak %.3f  mallocs %lld"
+                   "  get %.2f us avg (max %.1f) / put %.2f us over %ld / %ld\n", pol.name, held / 1e9,
                    max_held / 1e9, peak_total / 1e9, (double)held / (double)std::max<size_t>(1, peak_total),
-                   (long long)(ar[0].mallocs + ar[1].mallocs + ar[2].mallocs + ar[3].mallocs));
+                   (long long)(ar[0].mallocs + ar[1].mallocs + ar[2].mallocs + ar[3].mallocs),
+                   get_ns / 1e3 / std::max(1L, ngets), get_max_ns / 1e3, put_ns / 1e3 / std::max(1L, nputs), ngets, nputs);
         }
     }
     return 0;
