@@ -86,7 +86,10 @@ __device__ __forceinline__ void cols256_stages_store(double (&x)[16], double q, 
 // LT: LDS transpose tiles (2 alternate with one barrier per target; 1 needs a second barrier
 // before each reuse, for a smaller LDS footprint).  (Two targets' column stages interleaved -- PAIR,
 // round 6 -- measured slower and were removed: DESIGN 4.8.)
-template <int NSTEP, bool YIN, bool VC = false, int PF = 1, int TT = 4, int LT = 2>
+// MODE (dev decomposition, tools/modup_fused_bench.hip; the engine runs 0): 1 = the conversion
+// alone (the column stages skipped, xv stored as is), 2 = the column stages alone (loads kept, the
+// MFMAs and their epilogue skipped)
+template <int NSTEP, bool YIN, bool VC = false, int PF = 1, int TT = 4, int LT = 2, int MODE = 0>
 __global__ __launch_bounds__(256, TT == 4 ? 2 : 3) void k_bconv_cols(BconvArgs a, Tabs T, int ntile) {
     static_assert(TT == 4 || TT == 2, "4 or 2 targets per workgroup");
     static_assert(LT == 1 || LT == 2, "1 or 2 LDS tiles");
@@ -222,6 +225,11 @@ __global__ __launch_bounds__(256, TT == 4 ? 2 : 3) void k_bconv_cols(BconvArgs a
                         }
                     }
         }
+        if constexpr (MODE == 2) {
+#pragma unroll
+            for (int m = 0; m < TT; m++) xv[m][ar] = (double)(bf[0][0][0] & 0xffffff) + (double)(bf[1][NSTEP - 1][3] & 0xff);
+            continue;
+        }
         bc_v16i acc[2];
 #pragma unroll
         for (int g = 0; g < 2; g++) {
@@ -249,6 +257,16 @@ __global__ __launch_bounds__(256, TT == 4 ? 2 : 3) void k_bconv_cols(BconvArgs a
     // stages of target m + 1 orders every read of tile m & 1 for target m before its reuse by
     // target m + 2; LT = 1: one more barrier before each reuse)
     __syncthreads();  // twq
+    if constexpr (MODE == 1) {
+#pragma unroll
+        for (int m = 0; m < TT; m++) {
+            if (m >= nlive) break;
+            u64* o = dst + ((long)limb_of(tau0 + m) << logN);
+#pragma unroll
+            for (int ar = 0; ar < 16; ar++) st_d(&o[(ar * 16 + b) * 256 + bx * 16 + cl], xv[m][ar]);
+        }
+        return;
+    }
 #pragma unroll
     for (int m = 0; m < TT; m++) {
         if (m >= nlive) break;

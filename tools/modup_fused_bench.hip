@@ -169,9 +169,12 @@ int main(int argc, char** argv) {
         const dim3 g(16 * B * nc * nti);
 #define FV(S, P, TT_, LT_) do { if (md) hipLaunchKernelGGL((k_bconv_cols<S, true, true, P, TT_, LT_>), g, dim3(256), 0, 0, af, T, nti); \
                       else hipLaunchKernelGGL((k_bconv_cols<S, true, false, P, TT_, LT_>), g, dim3(256), 0, 0, af, T, nti); } while (0)
+#define FM(S, MD) do { if (md) hipLaunchKernelGGL((k_bconv_cols<S, true, true, 1, 4, 2, MD>), g, dim3(256), 0, 0, af, T, nti); \
+                      else hipLaunchKernelGGL((k_bconv_cols<S, true, false, 1, 4, 2, MD>), g, dim3(256), 0, 0, af, T, nti); } while (0)
 #define FZ(S, P) do { if (P == 1 && pf == 3) FV(S, 1, 2, 2); else if (P == 1 && pf == 4) FV(S, 1, 2, 1); \
+                      else if (P == 1 && pf == 5) FM(S, 1); else if (P == 1 && pf == 6) FM(S, 2); \
                       else FV(S, P, 4, 2); } while (0)
-#define FS(S) do { if (pf == 0) FZ(S, 0); else if (pf == 2) FZ(S, 2); else FZ(S, 1); } while (0)  // 3, 4: PF 1
+#define FS(S) do { if (pf == 0) FZ(S, 0); else if (pf == 2) FZ(S, 2); else FZ(S, 1); } while (0)  // 3..6: PF 1
         switch (nstep) {
             case 1: FS(1); break;
             case 2: FS(2); break;
@@ -179,6 +182,7 @@ int main(int argc, char** argv) {
         }
 #undef FS
 #undef FZ
+#undef FM
 #undef FV
     };
     pair(true, true);
@@ -265,7 +269,7 @@ int main(int argc, char** argv) {
         cold(nm, fused);
         return 0;
     }
-    for (pf = 0; pf <= 4; pf++) {
+    for (pf = 0; pf <= 6; pf++) {  // 5 / 6: the conversion alone / the column stages alone (MODE 1 / 2)
         char nm[32];
         snprintf(nm, sizeof nm, "cold fused V%d", pf);
         cold(nm, fused);
@@ -274,7 +278,7 @@ int main(int argc, char** argv) {
         timeit("bconv_mfma", [&] { pair(true, false); });
         timeit("cols", [&] { pair(false, true); });
         timeit("pair", [&] { pair(true, true); });
-        for (pf = 0; pf <= 4; pf++) {
+        for (pf = 0; pf <= 6; pf++) {
             char nm[32];
             snprintf(nm, sizeof nm, "fused V%d", pf);
             timeit(nm, fused);
