@@ -37,6 +37,17 @@ def test_csrc_hash_gates_the_pmc_record(tmp_path, monkeypatch):
     assert bench.pmc_record() is None
 
 
+def test_committed_pmc_record_is_the_trees_own():
+    """The PMC record bench.py reads (profiles/rNN/pmc/round_traffic.json) measured exactly these
+    kernel sources and the default workload: a kernel edit without a retaken record would leave
+    the driver's line without `traffic` (tools/gpu_r06_pmc.sh + tools/pmc_traffic.py retake it)."""
+    rec = bench.pmc_record(_args())
+    assert rec is not None, f"{bench.PMC_FILE} was not measured on this tree's kernel sources"
+    per = rec["per_kernel"]
+    for cls in ("ks_rows_fin.prod", "modup_cols", "moddown_cols", "poly2_int"):
+        assert per[cls]["hbm_bytes_per_launch"] > 0
+
+
 class _FakeEngine:
     """engine_profile_kernels of two classes over 2 profiled steps: 'a' one dispatch per call,
     'b' three dispatches per call (as poly2_int's)."""
